@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X MS-MPI reduction path.
+
+Metric (BASELINE.json): GiB/s of a device-resident MPI_SUM local reduce over
+MPI_FLOAT, 256 MiB per operand per GPU (config 2), at 1/2/4/8 GPUs, and the
+fraction of the HBM roofline.
+
+* A "step" is one MPI_SUM combine `inout[i] += in[i]` over the whole 256 MiB
+  buffers (67,108,864 fp32), issued through the C ABI msx_reduce_local_dev
+  (the device entry point of MPI_Reduce_local) on one HIP stream, inputs
+  already resident in HBM.
+* `value` = whole-job HBM traffic rate: ranks x steps x 12 B/element (two 4-B
+  reads + one 4-B write) / max-over-ranks wall time, in GiB/s.  The payload
+  rate (4 B/element) is reported beside it.
+* N > 1: one process per GPU (torchrun), each rank reduces its own shard
+  (weak scaling, no data-path collective: the elements are independent).
+* roofline: algorithmic bytes per launch / mean kernel duration from HIP
+  events on the launch stream, against 8 TB/s (MI355X_MICROARCH.md).
+  `traffic` comes from the committed rocprofv3 PMC summary (FETCH_SIZE
+  doubled per the gfx950 calibration + WRITE_SIZE) when present.
+* cpu_baseline: the oracle (C restatement of op.cpp's Op<float>::Sum) timed
+  on this host, one thread = one MS-MPI rank, on a bounded sample.
+"""
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+N_ELEM = 64 << 20              # 256 MiB of fp32 per operand (config 2)
+BYTES_PER_ELEM = 12            # 2 x 4 B read + 4 B write
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--variant", type=int, default=-1, help="fp32 SUM kernel variant (-1: default)")
+    ap.add_argument("--sweep", action="store_true", help="time every kernel variant (rank 0 stderr)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--elems", type=int, default=N_ELEM)
+    return ap.parse_args()
+
+
+def traffic_from_profiles(kernel_substr="k_combineILi3EffLi4ELi256ELb0ELb0"):
+    """Per-launch HBM bytes from the newest committed PMC counter collection."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_*counter_collection.csv"))):
+        fetch, write, n = {}, {}, 0
+        with open(path) as f:
+            hdr = f.readline().strip().split(",")
+            idx = {k.strip('"'): i for i, k in enumerate(hdr)}
+            for line in f:
+                cols = line.rstrip("\n").split(",")
+                if len(cols) < len(hdr):
+                    continue
+                name = cols[idx["Kernel_Name"]]
+                if kernel_substr not in name:
+                    continue
+                disp = cols[idx["Dispatch_Id"]]
+                cn, val = cols[idx["Counter_Name"]].strip('"'), float(cols[idx["Counter_Value"]])
+                if cn == "FETCH_SIZE":
+                    fetch[disp] = val
+                elif cn == "WRITE_SIZE":
+                    write[disp] = val
+        if fetch and write:
+            f_kb = sum(fetch.values()) / len(fetch)
+            w_kb = sum(write.values()) / len(write)
+            # gfx950: FETCH_SIZE reads 1/2 of a 16-B/lane streaming read; KiB units
+            best = (2.0 * f_kb + w_kb) * 1024.0
+    return best
+
+
+def cpu_baseline(seconds, elems):
+    import numpy as np
+    import oracle
+    import msx
+    C = msx.C
+    n = elems
+    rng = np.random.default_rng(0x5EED)
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b)      # warm-up / page-in
+    calls, t0 = 0, time.perf_counter()
+    while True:
+        oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b)
+        calls += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gib = calls * n * BYTES_PER_ELEM / el / 2**30
+    return {"value": round(gib, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{calls} calls of oracle Op<float>::Sum over 2 x {n * 4 >> 20} MiB host buffers "
+                      f"({el:.1f} s, 1 thread = one MS-MPI rank)",
+            "payload_GiB_s": round(calls * n * 4 / el / 2**30, 3)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import msx
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # the library is a per-rank singleton here (no collective in the data path)
+    os.environ["MSX_SIZE"], os.environ["MSX_RANK"], os.environ["MSX_DEVICE"] = "1", "0", str(local)
+    L = msx.init(errors_return=True)
+    C = msx.C
+    if args.variant >= 0:
+        assert L.msx_tune_set(args.variant, 0) == 0
+
+    n = args.elems
+    g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
+    src = torch.rand(n, device=dev, generator=g) * 2 - 1
+    acc = torch.rand(n, device=dev, generator=g) * 2 - 1
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        rc = L.msx_reduce_local_dev(src.data_ptr(), acc.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, sp)
+        if rc:
+            raise RuntimeError(f"msx_reduce_local_dev: {rc} {msx.last_error()}")
+
+    # correctness of the timed kernel on this exact data (one IEEE add / element)
+    ref = acc + src
+    step()
+    torch.cuda.synchronize()
+    if not torch.equal(acc.view(torch.int32), ref.view(torch.int32)):
+        raise RuntimeError("parity check failed before timing")
+    del ref
+
+    sweep = {}
+    if args.sweep and rank == 0:
+        for v in range(L.msx_tune_variant_count()):
+            L.msx_tune_set(v, 0)
+            for _ in range(5):
+                step()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(20):
+                step()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 20
+            sweep[L.msx_tune_variant_name(v).decode()] = round(n * BYTES_PER_ELEM / ms / 1e6, 1)
+            print(f"variant {v} {L.msx_tune_variant_name(v).decode()}: {ms * 1e3:.1f} us "
+                  f"{n * BYTES_PER_ELEM / ms / 1e6:.0f} GB/s", file=sys.stderr)
+        L.msx_tune_set(max(args.variant, 0), 0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = float(t[0]), float(t[1])
+
+    # host-memory path (the MPI buffers start and end in host memory): measured
+    # on rank 0 only, reported beside the device-resident value.
+    host = None
+    if rank == 0 and world == 1 and not args.no_host_path:
+        host = {}
+        a_h = src.cpu()
+        for label, pin in (("pageable", False), ("pinned", True)):
+            ah = a_h.pin_memory() if pin else a_h.clone()
+            bh = acc.cpu()
+            bh = bh.pin_memory() if pin else bh
+            L.MPI_Reduce_local(ah.data_ptr(), bh.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM)
+            reps, t1 = 3, time.perf_counter()
+            for _ in range(reps):
+                rc = L.MPI_Reduce_local(ah.data_ptr(), bh.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM)
+                assert rc == 0, msx.last_error()
+            dt_h = (time.perf_counter() - t1) / reps
+            host[label] = {"ms_per_call": round(dt_h * 1e3, 2),
+                           "payload_GiB_s": round(n * 4 / dt_h / 2**30, 2),
+                           "traffic_GiB_s": round(n * BYTES_PER_ELEM / dt_h / 2**30, 2)}
+        # blocking MPI_Reduce_local on device buffers (adds launch + sync per call)
+        reps, t1 = 10, time.perf_counter()
+        for _ in range(reps):
+            L.MPI_Reduce_local(src.data_ptr(), acc.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM)
+        dt_b = (time.perf_counter() - t1) / reps
+        host["device_blocking_MPI_Reduce_local_GiB_s"] = round(n * BYTES_PER_ELEM / dt_b / 2**30, 1)
+
+    if rank == 0:
+        total_bytes = world * args.steps * n * BYTES_PER_ELEM
+        value = total_bytes / elapsed / 2**30
+        achieved = n * BYTES_PER_ELEM / (kern_ms / 1e3) / 1e9      # GB/s, rank 0's kernel
+        traffic = traffic_from_profiles()
+        out = {
+            "metric": "GiB/s device-resident MPI_SUM local-reduce fp32 (HBM traffic, 12 B/element)",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic uniform[-1,1) fp32, seeded per rank, resident in HBM",
+            "config": {"workload": "MPI_SUM MPI_FLOAT local-reduce, 256 MiB per operand per GPU "
+                                   "(BASELINE.json configs[1])",
+                       "elements_per_gpu": n, "bytes_per_operand": n * 4,
+                       "parallelism": f"{world} rank(s), one per GPU, independent shards"},
+            "payload_GiB_s": round(world * args.steps * n * 4 / elapsed / 2**30, 2),
+            "pct_hbm_peak": round(100 * value * 2**30 / 1e9 / (world * HBM_PEAK_GBS), 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": (round(traffic) if traffic else None),
+                         "bytes_per_launch": n * BYTES_PER_ELEM,
+                         "kernel_us_mean": round(kern_ms * 1e3, 2),
+                         "kernel_us_mean_max_rank": round(kern_ms_max * 1e3, 2)},
+        }
+        if host is not None:
+            out["host_path"] = host
+        if sweep:
+            out["variant_sweep_GB_s"] = sweep
+        if world == 1:
+            del src, acc
+            torch.cuda.empty_cache()
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

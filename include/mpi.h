@@ -1,0 +1,274 @@
+/*
+ * mpi.h — MPI-2.2 C API subset for the MI355X-native MS-MPI reduction path.
+ *
+ * This header is written for this project.  It keeps the numeric ABI of
+ * MS-MPI (handle values, error classes, typedef widths) so that code compiled
+ * against MS-MPI's reduction API keeps its meaning when linked against
+ * libmsmpi_mi355x.so.  Values are cited against the reference header
+ * /root/reference/src/include/mpi.h (file:line).
+ *
+ * Scope: the local-reduction path (MPI_Op kernels) and the reduction
+ * collectives that call it.  See DESIGN.md.
+ */
+#ifndef MSX_MPI_H_INCLUDED
+#define MSX_MPI_H_INCLUDED
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* mpi.h:185 — __stdcall is a no-op on x64; keep the spelling for drop-in. */
+#define MPIAPI
+/* mpi.h:515 */
+#define MPI_METHOD int MPIAPI
+
+#define MPI_VERSION    2
+#define MPI_SUBVERSION 2
+
+/* ---- error classes (mpi.h:192-250) -------------------------------------- */
+#define MPI_SUCCESS          0
+#define MPI_ERR_BUFFER       1
+#define MPI_ERR_COUNT        2
+#define MPI_ERR_TYPE         3
+#define MPI_ERR_TAG          4
+#define MPI_ERR_COMM         5
+#define MPI_ERR_RANK         6
+#define MPI_ERR_ROOT         7
+#define MPI_ERR_GROUP        8
+#define MPI_ERR_OP           9
+#define MPI_ERR_TOPOLOGY    10
+#define MPI_ERR_DIMS        11
+#define MPI_ERR_ARG         12
+#define MPI_ERR_UNKNOWN     13
+#define MPI_ERR_TRUNCATE    14
+#define MPI_ERR_OTHER       15
+#define MPI_ERR_INTERN      16
+#define MPI_ERR_IN_STATUS   17
+#define MPI_ERR_PENDING     18
+#define MPI_ERR_REQUEST     19
+#define MPI_ERR_NO_MEM      34
+#define MPI_ERR_NOT_SAME    35
+#define MPI_ERR_LASTCODE    0x3fffffff
+
+#define MPI_MAX_ERROR_STRING 512
+
+/* ---- basic integer types (mpi.h:258-270, Win64 / LLP64) ------------------ */
+typedef int64_t MPI_Aint;
+typedef int     MPI_Fint;
+typedef int64_t MPI_Offset;
+typedef int64_t MPI_Count;
+
+/* ---- MPI_Datatype (mpi.h:281-368): 0x4c00SSII, SS = element bytes -------- */
+typedef int MPI_Datatype;
+#define MPI_DATATYPE_NULL           ((MPI_Datatype)0x0c000000)
+
+#define MPI_CHAR                    ((MPI_Datatype)0x4c000101)
+#define MPI_UNSIGNED_CHAR           ((MPI_Datatype)0x4c000102)
+#define MPI_SHORT                   ((MPI_Datatype)0x4c000203)
+#define MPI_UNSIGNED_SHORT          ((MPI_Datatype)0x4c000204)
+#define MPI_INT                     ((MPI_Datatype)0x4c000405)
+#define MPI_UNSIGNED                ((MPI_Datatype)0x4c000406)
+#define MPI_LONG                    ((MPI_Datatype)0x4c000407)   /* LLP64: 4 bytes */
+#define MPI_UNSIGNED_LONG           ((MPI_Datatype)0x4c000408)   /* LLP64: 4 bytes */
+#define MPI_LONG_LONG_INT           ((MPI_Datatype)0x4c000809)
+#define MPI_LONG_LONG               MPI_LONG_LONG_INT
+#define MPI_FLOAT                   ((MPI_Datatype)0x4c00040a)
+#define MPI_DOUBLE                  ((MPI_Datatype)0x4c00080b)
+#define MPI_LONG_DOUBLE             ((MPI_Datatype)0x4c00080c)   /* MSVC: 8 bytes */
+#define MPI_BYTE                    ((MPI_Datatype)0x4c00010d)
+#define MPI_WCHAR                   ((MPI_Datatype)0x4c00020e)
+#define MPI_PACKED                  ((MPI_Datatype)0x4c00010f)
+#define MPI_LB                      ((MPI_Datatype)0x4c000010)
+#define MPI_UB                      ((MPI_Datatype)0x4c000011)
+#define MPI_C_COMPLEX               ((MPI_Datatype)0x4c000812)
+#define MPI_C_FLOAT_COMPLEX         ((MPI_Datatype)0x4c000813)
+#define MPI_C_DOUBLE_COMPLEX        ((MPI_Datatype)0x4c001014)
+#define MPI_C_LONG_DOUBLE_COMPLEX   ((MPI_Datatype)0x4c001015)
+#define MPI_2INT                    ((MPI_Datatype)0x4c000816)
+#define MPI_C_BOOL                  ((MPI_Datatype)0x4c000117)
+#define MPI_SIGNED_CHAR             ((MPI_Datatype)0x4c000118)
+#define MPI_UNSIGNED_LONG_LONG      ((MPI_Datatype)0x4c000819)
+#define MPI_CHARACTER               ((MPI_Datatype)0x4c00011a)
+#define MPI_INTEGER                 ((MPI_Datatype)0x4c00041b)
+#define MPI_REAL                    ((MPI_Datatype)0x4c00041c)
+#define MPI_LOGICAL                 ((MPI_Datatype)0x4c00041d)
+#define MPI_COMPLEX                 ((MPI_Datatype)0x4c00081e)
+#define MPI_DOUBLE_PRECISION        ((MPI_Datatype)0x4c00081f)
+#define MPI_2INTEGER                ((MPI_Datatype)0x4c000820)
+#define MPI_2REAL                   ((MPI_Datatype)0x4c000821)
+#define MPI_DOUBLE_COMPLEX          ((MPI_Datatype)0x4c001022)
+#define MPI_2DOUBLE_PRECISION       ((MPI_Datatype)0x4c001023)
+#define MPI_2COMPLEX                ((MPI_Datatype)0x4c001024)
+#define MPI_2DOUBLE_COMPLEX         ((MPI_Datatype)0x4c002025)
+#define MPI_REAL2                   MPI_DATATYPE_NULL
+#define MPI_REAL4                   ((MPI_Datatype)0x4c000427)
+#define MPI_COMPLEX8                ((MPI_Datatype)0x4c000828)
+#define MPI_REAL8                   ((MPI_Datatype)0x4c000829)
+#define MPI_COMPLEX16               ((MPI_Datatype)0x4c00102a)
+#define MPI_REAL16                  MPI_DATATYPE_NULL
+#define MPI_COMPLEX32               MPI_DATATYPE_NULL
+#define MPI_INTEGER1                ((MPI_Datatype)0x4c00012d)
+#define MPI_COMPLEX4                MPI_DATATYPE_NULL
+#define MPI_INTEGER2                ((MPI_Datatype)0x4c00022f)
+#define MPI_INTEGER4                ((MPI_Datatype)0x4c000430)
+#define MPI_INTEGER8                ((MPI_Datatype)0x4c000831)
+#define MPI_INTEGER16               MPI_DATATYPE_NULL
+#define MPI_INT8_T                  ((MPI_Datatype)0x4c000133)
+#define MPI_INT16_T                 ((MPI_Datatype)0x4c000234)
+#define MPI_INT32_T                 ((MPI_Datatype)0x4c000435)
+#define MPI_INT64_T                 ((MPI_Datatype)0x4c000836)
+#define MPI_UINT8_T                 ((MPI_Datatype)0x4c000137)
+#define MPI_UINT16_T                ((MPI_Datatype)0x4c000238)
+#define MPI_UINT32_T                ((MPI_Datatype)0x4c000439)
+#define MPI_UINT64_T                ((MPI_Datatype)0x4c00083a)
+#define MPI_AINT                    ((MPI_Datatype)0x4c00083b)   /* _WIN64 value */
+#define MPI_OFFSET                  ((MPI_Datatype)0x4c00083c)
+#define MPI_COUNT                   ((MPI_Datatype)0x4c00083d)
+/* value/location pair types (mpi.h:364-368) */
+#define MPI_FLOAT_INT               ((MPI_Datatype)0x8c000000)
+#define MPI_DOUBLE_INT              ((MPI_Datatype)0x8c000001)
+#define MPI_LONG_INT                ((MPI_Datatype)0x8c000002)
+#define MPI_SHORT_INT               ((MPI_Datatype)0x8c000003)
+#define MPI_LONG_DOUBLE_INT         ((MPI_Datatype)0x8c000004)
+
+/* ---- MPI_Comm (mpi.h:375-379) ------------------------------------------- */
+typedef int MPI_Comm;
+#define MPI_COMM_NULL  ((MPI_Comm)0x04000000)
+#define MPI_COMM_WORLD ((MPI_Comm)0x44000000)
+#define MPI_COMM_SELF  ((MPI_Comm)0x44000001)
+
+/* ---- MPI_Op (mpi.h:410-426) --------------------------------------------- */
+typedef int MPI_Op;
+#define MPI_OP_NULL ((MPI_Op)0x18000000)
+#define MPI_MAX     ((MPI_Op)0x58000001)
+#define MPI_MIN     ((MPI_Op)0x58000002)
+#define MPI_SUM     ((MPI_Op)0x58000003)
+#define MPI_PROD    ((MPI_Op)0x58000004)
+#define MPI_LAND    ((MPI_Op)0x58000005)
+#define MPI_BAND    ((MPI_Op)0x58000006)
+#define MPI_LOR     ((MPI_Op)0x58000007)
+#define MPI_BOR     ((MPI_Op)0x58000008)
+#define MPI_LXOR    ((MPI_Op)0x58000009)
+#define MPI_BXOR    ((MPI_Op)0x5800000a)
+#define MPI_MINLOC  ((MPI_Op)0x5800000b)
+#define MPI_MAXLOC  ((MPI_Op)0x5800000c)
+#define MPI_REPLACE ((MPI_Op)0x5800000d)
+#define MPI_NO_OP   ((MPI_Op)0x5800000e)
+
+/* ---- MPI_Request / MPI_Errhandler / MPI_Status (mpi.h:441-489) ----------- */
+typedef int MPI_Request;
+#define MPI_REQUEST_NULL ((MPI_Request)0x2c000000)
+
+typedef int MPI_Errhandler;
+#define MPI_ERRHANDLER_NULL  ((MPI_Errhandler)0x14000000)
+#define MPI_ERRORS_ARE_FATAL ((MPI_Errhandler)0x54000000)
+#define MPI_ERRORS_RETURN    ((MPI_Errhandler)0x54000001)
+
+typedef struct MPI_Status
+{
+    int internal[2];
+    int MPI_SOURCE;
+    int MPI_TAG;
+    int MPI_ERROR;
+} MPI_Status;
+
+#define MPI_STATUS_IGNORE   ((MPI_Status*)(MPI_Aint)1)
+#define MPI_STATUSES_IGNORE ((MPI_Status*)(MPI_Aint)1)
+
+#define MPI_UNDEFINED   (-32766)
+#define MPI_BOTTOM      ((void*)0)
+/* mpi.h:1956 */
+#define MPI_IN_PLACE    ((void*)(MPI_Aint)-1)
+
+/* thread levels */
+#define MPI_THREAD_SINGLE     0
+#define MPI_THREAD_FUNNELED   1
+#define MPI_THREAD_SERIALIZED 2
+#define MPI_THREAD_MULTIPLE   3
+
+/* ---- user reduction function (mpi.h:2258-2265) --------------------------- */
+typedef void (MPIAPI MPI_User_function)(void* invec, void* inoutvec, int* len,
+                                         MPI_Datatype* datatype);
+
+/* ---- environment ---------------------------------------------------------- */
+MPI_METHOD MPI_Init(int* argc, char*** argv);
+MPI_METHOD MPI_Init_thread(int* argc, char*** argv, int required, int* provided);
+MPI_METHOD MPI_Finalize(void);
+MPI_METHOD MPI_Initialized(int* flag);
+MPI_METHOD MPI_Finalized(int* flag);
+MPI_METHOD MPI_Abort(MPI_Comm comm, int errorcode);
+double MPIAPI MPI_Wtime(void);
+MPI_METHOD MPI_Comm_rank(MPI_Comm comm, int* rank);
+MPI_METHOD MPI_Comm_size(MPI_Comm comm, int* size);
+MPI_METHOD MPI_Barrier(MPI_Comm comm);
+MPI_METHOD MPI_Comm_set_errhandler(MPI_Comm comm, MPI_Errhandler errhandler);
+MPI_METHOD MPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler* errhandler);
+MPI_METHOD MPI_Error_class(int errorcode, int* errorclass);
+MPI_METHOD MPI_Error_string(int errorcode, char* string, int* resultlen);
+MPI_METHOD MPI_Type_size(MPI_Datatype datatype, int* size);
+
+/* ---- reduction operations (mpi.h:2266-2300) ------------------------------ */
+MPI_METHOD MPI_Op_commutative(MPI_Op op, int* commute);
+MPI_METHOD MPI_Op_create(MPI_User_function* user_fn, int commute, MPI_Op* op);
+MPI_METHOD MPI_Op_free(MPI_Op* op);
+
+/* ---- reduction collectives (mpi.h:2305-2560) ----------------------------- */
+MPI_METHOD MPI_Reduce(const void* sendbuf, void* recvbuf, int count,
+                      MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm);
+MPI_METHOD MPI_Allreduce(const void* sendbuf, void* recvbuf, int count,
+                         MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD MPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
+                            MPI_Datatype datatype, MPI_Op op);
+MPI_METHOD MPI_Reduce_scatter_block(const void* sendbuf, void* recvbuf, int recvcount,
+                                    MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD MPI_Reduce_scatter(const void* sendbuf, void* recvbuf, const int recvcounts[],
+                              MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD MPI_Scan(const void* sendbuf, void* recvbuf, int count,
+                    MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD MPI_Exscan(const void* sendbuf, void* recvbuf, int count,
+                      MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD MPI_Iallreduce(const void* sendbuf, void* recvbuf, int count,
+                          MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                          MPI_Request* request);
+MPI_METHOD MPI_Ireduce(const void* sendbuf, void* recvbuf, int count,
+                       MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
+                       MPI_Request* request);
+MPI_METHOD MPI_Ireduce_scatter_block(const void* sendbuf, void* recvbuf, int recvcount,
+                                     MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                                     MPI_Request* request);
+MPI_METHOD MPI_Ireduce_scatter(const void* sendbuf, void* recvbuf, const int recvcounts[],
+                               MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                               MPI_Request* request);
+
+/* ---- request completion --------------------------------------------------- */
+MPI_METHOD MPI_Wait(MPI_Request* request, MPI_Status* status);
+MPI_METHOD MPI_Test(MPI_Request* request, int* flag, MPI_Status* status);
+MPI_METHOD MPI_Waitall(int count, MPI_Request array_of_requests[],
+                       MPI_Status array_of_statuses[]);
+
+/* ---- profiling interface aliases (msmpi.def:101-102,422-423,478-483,...) -- */
+MPI_METHOD PMPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
+                             MPI_Datatype datatype, MPI_Op op);
+MPI_METHOD PMPI_Reduce(const void* sendbuf, void* recvbuf, int count,
+                       MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm);
+MPI_METHOD PMPI_Allreduce(const void* sendbuf, void* recvbuf, int count,
+                          MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD PMPI_Reduce_scatter_block(const void* sendbuf, void* recvbuf, int recvcount,
+                                     MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD PMPI_Reduce_scatter(const void* sendbuf, void* recvbuf, const int recvcounts[],
+                               MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD PMPI_Iallreduce(const void* sendbuf, void* recvbuf, int count,
+                           MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                           MPI_Request* request);
+MPI_METHOD PMPI_Op_create(MPI_User_function* user_fn, int commute, MPI_Op* op);
+MPI_METHOD PMPI_Op_free(MPI_Op* op);
+MPI_METHOD PMPI_Op_commutative(MPI_Op op, int* commute);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSX_MPI_H_INCLUDED */

@@ -1,0 +1,84 @@
+/*
+ * msx.h — device-side C ABI of the MI355X MS-MPI reduction path.
+ *
+ * Plain C, no HIP/torch types: streams are passed as `void*` (a hipStream_t,
+ * NULL = the library's internal stream for the current device).
+ *
+ * Each entry point names the reference interface it replaces:
+ *
+ *   msx_reduce_local_dev  <- MPID_Uop_call(op, in, inout, &len, &dt)
+ *                            (src/mpi/msmpi/include/op.h:171-174) reaching
+ *                            MPIR_Op_<op>(void*, void*, int*, MPI_Datatype*)
+ *                            (src/mpi/msmpi/mpid/op.cpp:703-1795), with the
+ *                            MPI_Reduce_local argument checks
+ *                            (src/mpi/msmpi/api/mpi_reduce.cpp:304-385);
+ *                            64-bit count, stream-ordered, device pointers.
+ *   msx_op_check          <- MPIR_Op_check_dtype_table[op%16-1](dt)
+ *                            (op.cpp:653-672, api/mpi_api.h:765)
+ *   msx_reduce_tree_dev   <- the per-step MPID_Uop_call chain of the
+ *                            recursive-halving/doubling schedules
+ *                            (src/mpi/msmpi/mpid/reduce.cpp:3899-3989,
+ *                            1088-1175) fused into one pass over p inputs.
+ *
+ * All functions return an MPI error class (MPI_SUCCESS = 0).  Extensions do
+ * not invoke the MPI error handler; msx_last_error() describes the failure.
+ */
+#ifndef MSX_H_INCLUDED
+#define MSX_H_INCLUDED
+
+#include <stdint.h>
+#include "mpi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* library identity */
+const char* msx_version(void);
+/* number of visible GPUs (0 on a host without one); never aborts */
+int msx_device_count(void);
+/* text of the last error raised on the calling thread ("" if none) */
+const char* msx_last_error(void);
+
+/* (op, datatype) legality exactly as the reference's check tables */
+int msx_op_check(MPI_Op op, MPI_Datatype datatype);
+/* element size in bytes of a predefined datatype (-1 if unknown) */
+int msx_type_size(MPI_Datatype datatype);
+
+/* inout[i] = inout[i] (op) in[i], i in [0,count); device pointers,
+ * stream-ordered (returns after the launch, not after completion). */
+int msx_reduce_local_dev(const void* in, void* inout, int64_t count,
+                         MPI_Datatype datatype, MPI_Op op, void* stream);
+
+/* out[i] = tree(srcs[0][i], ..., srcs[p-1][i]) with the balanced binary tree
+ * ((s0 op s1) op (s2 op s3)) op ((s4 op s5) op (s6 op s7)), the left operand
+ * of each combine in the reference's `inout` role.  p in {1,2,4,8,16};
+ * srcs is a HOST array of device pointers; out may alias srcs[0]. */
+int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count,
+                        MPI_Datatype datatype, MPI_Op op, void* stream);
+
+/* benchmark knobs for the fp32 SUM hot path: variant index (0 = default) and
+ * a cap on workgroups (0 = one tile per workgroup). */
+int msx_tune_set(int variant, int grid_cap);
+int msx_tune_variant_count(void);
+const char* msx_tune_variant_name(int variant);
+
+/* host staging chunk size (bytes) for MPI_Reduce_local on host buffers */
+int msx_set_staging_chunk(int64_t bytes);
+
+/* schedule introspection for host-side tests of the collective engine
+ * (mpid/reduce.cpp:3884-4066, 917-1334 restated as expression trees):
+ * which = 0 allreduce tree of newrank n, 1 reduce_scatter tree of newrank n,
+ * 2 pairwise chain of real rank n.  src32[i] = real rank in kernel slot i. */
+int msx_schedule_tree(int which, int p, int n, int* src32, int* P, unsigned* pairmask,
+                      int* chain);
+/* which = 0 allreduce, 1 reduce_scatter: 0 recursive doubling, 1 Rabenseifner,
+ * 2 recursive halving, 3 pairwise */
+int msx_schedule_algo(int which, int p, int64_t count, int type_size);
+int msx_schedule_newrank(int rank, int p);
+int msx_schedule_block(int p, int64_t count, int n, int64_t* start, int64_t* len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,783 @@
+// msx_api.cpp — MPI-2.2 C entry points of the reduction path.
+//
+// Each function keeps the reference's argument-validation ORDER, because the
+// first failing check decides which error class a caller sees:
+//   MPI_Reduce_local           api/mpi_reduce.cpp:304-385
+//   MPI_Reduce                 api/mpi_reduce.cpp:46-273
+//   MPI_Allreduce              api/mpi_reduce.cpp:1246-1410
+//   MPI_Reduce_scatter(_block) api/mpi_reduce.cpp:422-997
+//   MPI_Iallreduce / I*        api/mpi_reduce.cpp:1445-1591, 617-790
+//   MPI_Scan / MPI_Exscan      api/mpi_reduce.cpp:1626-1900
+//   MPI_Op_create/free/commutative  api/mpi_op.cpp:48-260
+//   validators MpiaOpValidate / MpiaDatatypeValidate  api/mpi_api.h:113-212, 707-775
+//   error return               mpid/error.cpp:85-134 (ERRORS_ARE_FATAL default)
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/msx.h"
+#include "msx_comm.h"
+#include "msx_kernels.h"
+#include "msx_runtime.h"
+#include "msx_types.h"
+
+using namespace msx;
+
+#define MSX_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// user ops: MPID_Op pool for HANDLE_TYPE_DIRECT op handles (include/op.h:82-134)
+// ---------------------------------------------------------------------------
+struct UserOp {
+    MPI_User_function* fn = nullptr;
+    bool commute = true;
+    bool live = false;
+};
+std::mutex g_op_mu;
+std::vector<UserOp> g_user_ops;
+constexpr int kUserOpBase = (int)0x98000000;   // type DIRECT (2) | kind MPID_OP (6)
+
+const char* class_string(int cls)
+{
+    switch (cls) {
+    case MPI_SUCCESS: return "No MPI error";
+    case MPI_ERR_BUFFER: return "Invalid buffer pointer";
+    case MPI_ERR_COUNT: return "Invalid count argument";
+    case MPI_ERR_TYPE: return "Invalid datatype argument";
+    case MPI_ERR_TAG: return "Invalid tag argument";
+    case MPI_ERR_COMM: return "Invalid communicator";
+    case MPI_ERR_RANK: return "Invalid rank";
+    case MPI_ERR_ROOT: return "Invalid root";
+    case MPI_ERR_GROUP: return "Invalid group";
+    case MPI_ERR_OP: return "Invalid MPI_Op";
+    case MPI_ERR_ARG: return "Invalid argument";
+    case MPI_ERR_UNKNOWN: return "Unknown error";
+    case MPI_ERR_TRUNCATE: return "Message truncated";
+    case MPI_ERR_OTHER: return "Other MPI error";
+    case MPI_ERR_INTERN: return "Internal MPI error";
+    case MPI_ERR_REQUEST: return "Invalid MPI_Request";
+    case MPI_ERR_NO_MEM: return "Out of memory";
+    default: return "Unknown error class";
+    }
+}
+
+void not_initialized_exit(const char* fn)
+{
+    // MpiaIsInitializedOrExit -> MPIR_Err_preOrPostInit (api/mpi_api.h:27)
+    fprintf(stderr,
+            "Fatal error in %s: Attempting to use an MPI routine %s MPI_Init\n", fn,
+            is_finalized() ? "after finalizing" : "before initializing");
+    fflush(stderr);
+    exit(1);
+}
+
+#define MSX_REQUIRE_INIT(fn)                                                  \
+    do {                                                                      \
+        if (!is_initialized() || is_finalized()) not_initialized_exit(fn);    \
+    } while (0)
+
+// MPIR_Err_return_comm (mpid/error.cpp:85-134): default handler is the one on
+// MPI_COMM_WORLD; ERRORS_ARE_FATAL aborts the job.
+int err_return(Comm* c, const char* fn, int code)
+{
+    if (code == MPI_SUCCESS) return code;
+    if (c == nullptr) c = world();
+    MPI_Errhandler h = c ? c->errhandler : MPI_ERRORS_ARE_FATAL;
+    if (h == MPI_ERRORS_ARE_FATAL) {
+        const char* detail = last_error();
+        fprintf(stderr, "Fatal error in %s: %s, error stack:\n%s  %s\n", fn, class_string(code),
+                fn, (detail && *detail) ? detail : "");
+        fflush(stderr);
+        exit(code);
+    }
+    return code;
+}
+
+// MpiaCommValidateHandle
+int v_comm(MPI_Comm c, Comm** out)
+{
+    *out = nullptr;
+    if (c == MPI_COMM_NULL) { set_error("null communicator"); return MPI_ERR_COMM; }
+    Comm* p = lookup_comm(c);
+    if (!p) { set_error("invalid communicator 0x%x", c); return MPI_ERR_COMM; }
+    *out = p;
+    return MPI_SUCCESS;
+}
+
+bool dtype_known(MPI_Datatype dt) { return type_size(dt) >= 0; }
+
+// MpiaDatatypeValidate (mpi_api.h:113-169), predefined datatypes only.
+int v_dtype(const void* buf, long long count, MPI_Datatype dt)
+{
+    if (count == 0) return MPI_SUCCESS;
+    if (count < 0) { set_error("negative count %lld", count); return MPI_ERR_COUNT; }
+    if (dt == MPI_DATATYPE_NULL) { set_error("null datatype"); return MPI_ERR_TYPE; }
+    if (!dtype_known(dt)) { set_error("invalid datatype 0x%x", dt); return MPI_ERR_TYPE; }
+    if (buf == nullptr) { set_error("null buffer"); return MPI_ERR_BUFFER; }
+    return MPI_SUCCESS;
+}
+
+// MpiaDatatypeValidateBuffer (mpi_api.h:190-212)
+int v_buffer(MPI_Datatype dt, const void* buf, long long count)
+{
+    if (buf == nullptr && count > 0 && type_size(dt) > 0) {
+        set_error("null buffer");
+        return MPI_ERR_BUFFER;
+    }
+    return MPI_SUCCESS;
+}
+
+// MpiaOpValidateHandle (mpi_api.h:707-728)
+int v_op_handle(MPI_Op op, OpRef* out)
+{
+    if (handle_kind(op) != OBJ_OP || handle_type(op) == HT_INVALID) {
+        set_error("invalid MPI_Op 0x%x", op);
+        return MPI_ERR_OP;
+    }
+    if (handle_type(op) == HT_BUILTIN) {
+        int idx = op & 0xff;
+        if (idx < O_MAX || idx > O_NOOP || (op & 0x03ffff00)) {
+            set_error("invalid builtin MPI_Op 0x%x", op);
+            return MPI_ERR_OP;
+        }
+        out->opidx = idx;
+        out->user_fn = nullptr;
+        out->commutative = (idx != O_REPLACE && idx != O_NOOP);
+        return MPI_SUCCESS;
+    }
+    std::lock_guard<std::mutex> g(g_op_mu);
+    size_t idx = (size_t)(op & 0x03ffffff);
+    if (handle_type(op) != HT_DIRECT || idx >= g_user_ops.size() || !g_user_ops[idx].live) {
+        set_error("MPI_Op 0x%x does not name a live operation", op);
+        return MPI_ERR_OP;
+    }
+    out->opidx = O_NULL;
+    out->user_fn = g_user_ops[idx].fn;
+    out->commutative = g_user_ops[idx].commute;
+    return MPI_SUCCESS;
+}
+
+// MpiaOpValidate (mpi_api.h:731-775), rmaOp = false
+int v_op(MPI_Op op, MPI_Datatype dt, OpRef* out)
+{
+    int rc = v_op_handle(op, out);
+    if (rc != MPI_SUCCESS) return rc;
+    if (out->opidx == O_REPLACE) { set_error("MPI_REPLACE not allowed"); return MPI_ERR_OP; }
+    if (out->opidx == O_NOOP) { set_error("MPI_NO_OP not allowed"); return MPI_ERR_OP; }
+    if (out->opidx != O_NULL) {
+        rc = op_check_dtype(out->opidx, dt);
+        if (rc != MPI_SUCCESS) {
+            set_error("MPI_Op 0x%x is not defined for datatype 0x%x", op, dt);
+            return rc;
+        }
+    }
+    return MPI_SUCCESS;
+}
+
+}  // namespace
+
+// ===========================================================================
+// environment
+// ===========================================================================
+MSX_EXPORT int MPI_Init(int* argc, char*** argv)
+{
+    (void)argc; (void)argv;
+    if (is_initialized()) {
+        set_error("MPI_Init called twice");
+        return err_return(nullptr, "MPI_Init", MPI_ERR_OTHER);
+    }
+    int rc = world_init();
+    if (rc != MPI_SUCCESS) {
+        fprintf(stderr, "Fatal error in MPI_Init: %s\n", last_error());
+        exit(rc);
+    }
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Init_thread(int* argc, char*** argv, int required, int* provided)
+{
+    int rc = MPI_Init(argc, argv);
+    // Kernels are reentrant; the host staging path and bootstrap are locked
+    // (mid/env.cpp:1071-1078 grants up to MULTIPLE).
+    if (provided) *provided = required > MPI_THREAD_MULTIPLE ? MPI_THREAD_MULTIPLE : required;
+    return rc;
+}
+
+MSX_EXPORT int MPI_Finalize(void)
+{
+    MSX_REQUIRE_INIT("MPI_Finalize");
+    return world_finalize();
+}
+
+MSX_EXPORT int MPI_Initialized(int* flag)
+{
+    if (!flag) return MPI_ERR_ARG;
+    *flag = is_initialized() ? 1 : 0;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Finalized(int* flag)
+{
+    if (!flag) return MPI_ERR_ARG;
+    *flag = is_finalized() ? 1 : 0;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Abort(MPI_Comm comm, int errorcode)
+{
+    (void)comm;
+    fprintf(stderr, "MPI_Abort called with error code %d\n", errorcode);
+    fflush(stderr);
+    exit(errorcode);
+}
+
+MSX_EXPORT double MPI_Wtime(void)
+{
+    using namespace std::chrono;
+    return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+MSX_EXPORT int MPI_Comm_rank(MPI_Comm comm, int* rank)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_rank");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !rank) { set_error("null rank"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_rank", rc);
+    *rank = c->rank;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Comm_size(MPI_Comm comm, int* size)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_size");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !size) { set_error("null size"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_size", rc);
+    *size = c->size;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Barrier(MPI_Comm comm)
+{
+    MSX_REQUIRE_INIT("MPI_Barrier");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS) rc = coll_barrier(c);
+    return err_return(c, "MPI_Barrier", rc);
+}
+
+MSX_EXPORT int MPI_Comm_set_errhandler(MPI_Comm comm, MPI_Errhandler eh)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_set_errhandler");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && eh != MPI_ERRORS_ARE_FATAL && eh != MPI_ERRORS_RETURN) {
+        set_error("unsupported errhandler 0x%x", eh);
+        rc = MPI_ERR_ARG;
+    }
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_set_errhandler", rc);
+    c->errhandler = eh;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler* eh)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_get_errhandler");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !eh) rc = MPI_ERR_ARG;
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_get_errhandler", rc);
+    *eh = c->errhandler;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Error_class(int errorcode, int* errorclass)
+{
+    if (!errorclass) return MPI_ERR_ARG;
+    // This library returns error classes as codes.
+    *errorclass = errorcode & 0x7f;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Error_string(int errorcode, char* str, int* len)
+{
+    if (!str || !len) return MPI_ERR_ARG;
+    int n = snprintf(str, MPI_MAX_ERROR_STRING, "%s", class_string(errorcode & 0x7f));
+    *len = n < MPI_MAX_ERROR_STRING ? n : MPI_MAX_ERROR_STRING - 1;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Type_size(MPI_Datatype dt, int* size)
+{
+    MSX_REQUIRE_INIT("MPI_Type_size");
+    int rc = MPI_SUCCESS;
+    if (dt == MPI_DATATYPE_NULL || !dtype_known(dt)) { set_error("invalid datatype"); rc = MPI_ERR_TYPE; }
+    else if (!size) rc = MPI_ERR_ARG;
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Type_size", rc);
+    *size = type_size(dt);
+    return MPI_SUCCESS;
+}
+
+// ===========================================================================
+// operations (api/mpi_op.cpp:48-260)
+// ===========================================================================
+MSX_EXPORT int MPI_Op_create(MPI_User_function* user_fn, int commute, MPI_Op* op)
+{
+    MSX_REQUIRE_INIT("MPI_Op_create");
+    int rc = MPI_SUCCESS;
+    if (user_fn == nullptr) { set_error("null user_fn"); rc = MPI_ERR_ARG; }
+    else if (op == nullptr) { set_error("null op"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Op_create", rc);
+    std::lock_guard<std::mutex> g(g_op_mu);
+    size_t idx = 0;
+    while (idx < g_user_ops.size() && g_user_ops[idx].live) ++idx;
+    if (idx == g_user_ops.size()) g_user_ops.push_back(UserOp{});
+    g_user_ops[idx] = UserOp{user_fn, commute != 0, true};
+    *op = kUserOpBase | (int)idx;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Op_free(MPI_Op* op)
+{
+    MSX_REQUIRE_INIT("MPI_Op_free");
+    int rc = MPI_SUCCESS;
+    OpRef r;
+    if (op == nullptr) { set_error("null op"); rc = MPI_ERR_ARG; }
+    else rc = v_op_handle(*op, &r);
+    if (rc == MPI_SUCCESS && r.opidx != O_NULL) {
+        set_error("cannot free permanent MPI_Op");   // "**permop" mpi_op.cpp:169-173
+        rc = MPI_ERR_OP;
+    }
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Op_free", rc);
+    std::lock_guard<std::mutex> g(g_op_mu);
+    g_user_ops[(size_t)(*op & 0x03ffffff)].live = false;
+    *op = MPI_OP_NULL;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Op_commutative(MPI_Op op, int* commute)
+{
+    MSX_REQUIRE_INIT("MPI_Op_commutative");
+    OpRef r;
+    int rc = v_op_handle(op, &r);
+    if (rc == MPI_SUCCESS && commute == nullptr) { set_error("null commute"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Op_commutative", rc);
+    *commute = r.commutative ? 1 : 0;
+    return MPI_SUCCESS;
+}
+
+// ===========================================================================
+// MPI_Reduce_local (api/mpi_reduce.cpp:304-385)
+// ===========================================================================
+MSX_EXPORT int MPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
+                                MPI_Datatype datatype, MPI_Op op)
+{
+    MSX_REQUIRE_INIT("MPI_Reduce_local");
+    if (count == 0) return MPI_SUCCESS;             // :319-322, before any check
+    OpRef r;
+    int rc = v_op(op, datatype, &r);                // :324
+    if (rc == MPI_SUCCESS && inbuf == MPI_IN_PLACE) { set_error("inbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+    if (rc == MPI_SUCCESS && inoutbuf == MPI_IN_PLACE) { set_error("inoutbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+    if (rc == MPI_SUCCESS) rc = v_dtype(inbuf, count, datatype);   // :343
+    if (rc == MPI_SUCCESS && inbuf == inoutbuf) { set_error("inbuf aliases inoutbuf"); rc = MPI_ERR_BUFFER; }
+    if (rc == MPI_SUCCESS) rc = local_combine(r, datatype, inbuf, inoutbuf, (size_t)count);
+    return err_return(nullptr, "MPI_Reduce_local", rc);
+}
+
+// ===========================================================================
+// reduction collectives
+// ===========================================================================
+MSX_EXPORT int MPI_Allreduce(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                             MPI_Op op, MPI_Comm comm)
+{
+    MSX_REQUIRE_INIT("MPI_Allreduce");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS) rc = v_dtype(recvbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
+    if (rc == MPI_SUCCESS && count > 0) {
+        if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+        else if (sendbuf != MPI_IN_PLACE) {
+            rc = v_buffer(datatype, sendbuf, count);
+            if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+        }
+    }
+    if (rc == MPI_SUCCESS && count > 0)
+        rc = coll_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r);
+    return err_return(c, "MPI_Allreduce", rc);
+}
+
+MSX_EXPORT int MPI_Reduce(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                          MPI_Op op, int root, MPI_Comm comm)
+{
+    MSX_REQUIRE_INIT("MPI_Reduce");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && (root < 0 || root >= c->size)) { set_error("invalid root %d", root); rc = MPI_ERR_ROOT; }
+    if (rc == MPI_SUCCESS) rc = v_dtype(sendbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
+    if (rc == MPI_SUCCESS) {
+        if (c->rank == root) {
+            if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+            else rc = v_buffer(datatype, recvbuf, count);
+            if (rc == MPI_SUCCESS && count > 0 && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+        } else if (count > 0 && sendbuf == MPI_IN_PLACE) {
+            set_error("sendbuf is MPI_IN_PLACE on a non-root rank");
+            rc = MPI_ERR_BUFFER;
+        }
+    }
+    if (rc == MPI_SUCCESS && count > 0)
+        rc = coll_reduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, root);
+    return err_return(c, "MPI_Reduce", rc);
+}
+
+namespace {
+
+int validate_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
+                            MPI_Datatype datatype, MPI_Op op, OpRef* r)
+{
+    if (!recvcounts) { set_error("null recvcounts"); return MPI_ERR_ARG; }
+    int sentinel = 0;
+    for (int i = 0; i < c->size; ++i) {
+        if (recvcounts[i] < 0) { set_error("negative recvcount %d", recvcounts[i]); return MPI_ERR_COUNT; }
+        sentinel |= recvcounts[i];   // the reference's OR trick (mpi_reduce.cpp:833-847)
+    }
+    int rc = v_dtype(sendbuf, sentinel, datatype);
+    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, r);
+    if (rc == MPI_SUCCESS && recvcounts[c->rank] > 0) {
+        if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+        else if (sendbuf != MPI_IN_PLACE) {
+            rc = v_buffer(datatype, recvbuf, recvcounts[c->rank]);
+            if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+        }
+    }
+    return rc;
+}
+
+}  // namespace
+
+MSX_EXPORT int MPI_Reduce_scatter(const void* sendbuf, void* recvbuf, const int recvcounts[],
+                                  MPI_Datatype datatype, MPI_Op op, MPI_Comm comm)
+{
+    MSX_REQUIRE_INIT("MPI_Reduce_scatter");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS) rc = validate_reduce_scatter(c, sendbuf, recvbuf, recvcounts, datatype, op, &r);
+    if (rc == MPI_SUCCESS) rc = coll_reduce_scatter(c, sendbuf, recvbuf, recvcounts, datatype, r);
+    return err_return(c, "MPI_Reduce_scatter", rc);
+}
+
+MSX_EXPORT int MPI_Reduce_scatter_block(const void* sendbuf, void* recvbuf, int recvcount,
+                                        MPI_Datatype datatype, MPI_Op op, MPI_Comm comm)
+{
+    MSX_REQUIRE_INIT("MPI_Reduce_scatter_block");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    std::vector<int> counts;
+    if (rc == MPI_SUCCESS && recvcount < 0) { set_error("negative recvcount"); rc = MPI_ERR_COUNT; }
+    if (rc == MPI_SUCCESS) {
+        counts.assign((size_t)c->size, recvcount);
+        rc = validate_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, op, &r);
+    }
+    if (rc == MPI_SUCCESS) rc = coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
+    return err_return(c, "MPI_Reduce_scatter_block", rc);
+}
+
+namespace {
+
+int scan_common(const char* fn, const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                MPI_Op op, MPI_Comm comm, bool exclusive)
+{
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS) rc = v_dtype(recvbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
+    if (rc == MPI_SUCCESS && count > 0) {
+        if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+        else if (sendbuf != MPI_IN_PLACE) {
+            rc = v_buffer(datatype, sendbuf, count);
+            if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+        }
+    }
+    if (rc == MPI_SUCCESS && count > 0)
+        rc = coll_scan(c, sendbuf, recvbuf, (size_t)count, datatype, r, exclusive);
+    return err_return(c, fn, rc);
+}
+
+}  // namespace
+
+MSX_EXPORT int MPI_Scan(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                        MPI_Op op, MPI_Comm comm)
+{
+    MSX_REQUIRE_INIT("MPI_Scan");
+    return scan_common("MPI_Scan", sendbuf, recvbuf, count, datatype, op, comm, false);
+}
+
+MSX_EXPORT int MPI_Exscan(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                          MPI_Op op, MPI_Comm comm)
+{
+    MSX_REQUIRE_INIT("MPI_Exscan");
+    return scan_common("MPI_Exscan", sendbuf, recvbuf, count, datatype, op, comm, true);
+}
+
+// ---- non-blocking variants: stream-ordered requests -----------------------
+MSX_EXPORT int MPI_Iallreduce(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                              MPI_Op op, MPI_Comm comm, MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Iallreduce");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
+    if (rc == MPI_SUCCESS) rc = v_dtype(recvbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
+    if (rc == MPI_SUCCESS && count > 0) {
+        if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+        else if (sendbuf != MPI_IN_PLACE) {
+            rc = v_buffer(datatype, sendbuf, count);
+            if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+        }
+    }
+    if (rc == MPI_SUCCESS)
+        rc = request_start_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, request);
+    return err_return(c, "MPI_Iallreduce", rc);
+}
+
+MSX_EXPORT int MPI_Ireduce(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                           MPI_Op op, int root, MPI_Comm comm, MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Ireduce");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
+    if (rc == MPI_SUCCESS && (root < 0 || root >= c->size)) { set_error("invalid root"); rc = MPI_ERR_ROOT; }
+    if (rc == MPI_SUCCESS) rc = v_dtype(sendbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
+    if (rc == MPI_SUCCESS) {
+        if (c->rank == root) {
+            if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
+            else rc = v_buffer(datatype, recvbuf, count);
+            if (rc == MPI_SUCCESS && count > 0 && sendbuf == recvbuf) { set_error("alias"); rc = MPI_ERR_BUFFER; }
+        } else if (count > 0 && sendbuf == MPI_IN_PLACE) {
+            set_error("sendbuf is MPI_IN_PLACE on a non-root rank");
+            rc = MPI_ERR_BUFFER;
+        }
+    }
+    if (rc == MPI_SUCCESS) {
+        const size_t n = (size_t)count;
+        rc = request_start_generic(c, [=] {
+            return n ? coll_reduce(c, sendbuf, recvbuf, n, datatype, r, root) : MPI_SUCCESS;
+        }, request);
+    }
+    return err_return(c, "MPI_Ireduce", rc);
+}
+
+MSX_EXPORT int MPI_Ireduce_scatter(const void* sendbuf, void* recvbuf, const int recvcounts[],
+                                   MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                                   MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Ireduce_scatter");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
+    if (rc == MPI_SUCCESS) rc = validate_reduce_scatter(c, sendbuf, recvbuf, recvcounts, datatype, op, &r);
+    if (rc == MPI_SUCCESS) {
+        std::vector<int> counts(recvcounts, recvcounts + c->size);
+        rc = request_start_generic(c, [=] {
+            return coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
+        }, request);
+    }
+    return err_return(c, "MPI_Ireduce_scatter", rc);
+}
+
+MSX_EXPORT int MPI_Ireduce_scatter_block(const void* sendbuf, void* recvbuf, int recvcount,
+                                         MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                                         MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Ireduce_scatter_block");
+    Comm* c;
+    OpRef r;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
+    if (rc == MPI_SUCCESS && recvcount < 0) { set_error("negative recvcount"); rc = MPI_ERR_COUNT; }
+    std::vector<int> counts;
+    if (rc == MPI_SUCCESS) {
+        counts.assign((size_t)c->size, recvcount);
+        rc = validate_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, op, &r);
+    }
+    if (rc == MPI_SUCCESS) {
+        rc = request_start_generic(c, [=] {
+            return coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
+        }, request);
+    }
+    return err_return(c, "MPI_Ireduce_scatter_block", rc);
+}
+
+MSX_EXPORT int MPI_Wait(MPI_Request* request, MPI_Status* status)
+{
+    MSX_REQUIRE_INIT("MPI_Wait");
+    if (!request) { set_error("null request"); return err_return(nullptr, "MPI_Wait", MPI_ERR_ARG); }
+    return err_return(nullptr, "MPI_Wait", request_wait(request, status));
+}
+
+MSX_EXPORT int MPI_Test(MPI_Request* request, int* flag, MPI_Status* status)
+{
+    MSX_REQUIRE_INIT("MPI_Test");
+    if (!request || !flag) { set_error("null argument"); return err_return(nullptr, "MPI_Test", MPI_ERR_ARG); }
+    return err_return(nullptr, "MPI_Test", request_test(request, flag, status));
+}
+
+MSX_EXPORT int MPI_Waitall(int count, MPI_Request reqs[], MPI_Status statuses[])
+{
+    MSX_REQUIRE_INIT("MPI_Waitall");
+    int rc = MPI_SUCCESS;
+    for (int i = 0; i < count; ++i) {
+        MPI_Status* st = (statuses == MPI_STATUSES_IGNORE) ? MPI_STATUS_IGNORE : &statuses[i];
+        int r = request_wait(&reqs[i], st);
+        if (r != MPI_SUCCESS && rc == MPI_SUCCESS) rc = r;
+    }
+    return err_return(nullptr, "MPI_Waitall", rc);
+}
+
+// ---- PMPI_ profiling aliases (dll/msmpi.def) --------------------------------
+#define MSX_ALIAS(name) extern "C" __attribute__((visibility("default"), alias(#name)))
+MSX_ALIAS(MPI_Reduce_local) int PMPI_Reduce_local(const void*, void*, int, MPI_Datatype, MPI_Op);
+MSX_ALIAS(MPI_Reduce) int PMPI_Reduce(const void*, void*, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
+MSX_ALIAS(MPI_Allreduce) int PMPI_Allreduce(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);
+MSX_ALIAS(MPI_Reduce_scatter_block) int PMPI_Reduce_scatter_block(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);
+MSX_ALIAS(MPI_Reduce_scatter) int PMPI_Reduce_scatter(const void*, void*, const int[], MPI_Datatype, MPI_Op, MPI_Comm);
+MSX_ALIAS(MPI_Iallreduce) int PMPI_Iallreduce(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm, MPI_Request*);
+MSX_ALIAS(MPI_Op_create) int PMPI_Op_create(MPI_User_function*, int, MPI_Op*);
+MSX_ALIAS(MPI_Op_free) int PMPI_Op_free(MPI_Op*);
+MSX_ALIAS(MPI_Op_commutative) int PMPI_Op_commutative(MPI_Op, int*);
+
+// ===========================================================================
+// device-side extension ABI (include/msx.h)
+// ===========================================================================
+MSX_EXPORT const char* msx_version(void) { return "msmpi-mi355x 0.1 (gfx950)"; }
+MSX_EXPORT int msx_device_count(void) { return device_count_noinit(); }
+MSX_EXPORT const char* msx_last_error(void) { return last_error(); }
+
+MSX_EXPORT int msx_op_check(MPI_Op op, MPI_Datatype dt)
+{
+    OpRef r;
+    return v_op(op, dt, &r);
+}
+
+MSX_EXPORT int msx_type_size(MPI_Datatype dt) { return type_size(dt); }
+
+MSX_EXPORT int msx_reduce_local_dev(const void* in, void* inout, int64_t count, MPI_Datatype dt,
+                                    MPI_Op op, void* stream)
+{
+    if (count == 0) return MPI_SUCCESS;
+    OpRef r;
+    int rc = v_op(op, dt, &r);
+    if (rc != MPI_SUCCESS) return rc;
+    if (r.opidx == O_NULL) { set_error("device entry point takes builtin ops only"); return MPI_ERR_OP; }
+    if (count < 0) { set_error("negative count"); return MPI_ERR_COUNT; }
+    if (!in || !inout) { set_error("null buffer"); return MPI_ERR_BUFFER; }
+    if (in == inout) { set_error("inbuf aliases inoutbuf"); return MPI_ERR_BUFFER; }
+    rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : internal_stream();
+    return reduce_local_device(r.opidx, type_info(dt)->kind, in, inout, (size_t)count, s);
+}
+
+MSX_EXPORT int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count,
+                                   MPI_Datatype dt, MPI_Op op, void* stream)
+{
+    if (count == 0) return MPI_SUCCESS;
+    OpRef r;
+    int rc = v_op(op, dt, &r);
+    if (rc != MPI_SUCCESS) return rc;
+    if (r.opidx == O_NULL) { set_error("device entry point takes builtin ops only"); return MPI_ERR_OP; }
+    if (count < 0) { set_error("negative count"); return MPI_ERR_COUNT; }
+    if (!srcs || !out || !(p == 1 || p == 2 || p == 4 || p == 8 || p == 16)) {
+        set_error("bad tree arguments (p=%d)", p);
+        return MPI_ERR_ARG;
+    }
+    rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : internal_stream();
+    hipError_t e = launch_tree(r.opidx, type_info(dt)->kind, srcs, p, out, (size_t)count, s);
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "tree kernel launch");
+}
+
+MSX_EXPORT int msx_tune_set(int variant, int grid_cap)
+{
+    if (variant < 0 || variant >= combine_variant_count() || grid_cap < 0) return MPI_ERR_ARG;
+    launch_cfg().variant = variant;
+    launch_cfg().grid_cap = grid_cap;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int msx_tune_variant_count(void) { return combine_variant_count(); }
+MSX_EXPORT const char* msx_tune_variant_name(int v) { return combine_variant_name(v); }
+
+MSX_EXPORT int msx_set_staging_chunk(int64_t bytes)
+{
+    if (bytes <= 0) return MPI_ERR_ARG;
+    set_staging_chunk((size_t)bytes);
+    return MPI_SUCCESS;
+}
+
+// ---- schedule introspection (host-side tests of the collective engine) ------
+#include "msx_transport.h"
+
+// which: 0 = allreduce tree of newrank n, 1 = reduce_scatter (recursive
+// halving) tree of newrank n, 2 = pairwise chain of real rank n.
+// src32 receives real ranks per kernel slot (-1 = unused).
+MSX_EXPORT int msx_schedule_tree(int which, int p, int n, int* src32, int* P, unsigned* pairmask,
+                                 int* chain)
+{
+    if (p < 1 || p > 16 || !src32 || !P || !pairmask || !chain) return MPI_ERR_ARG;
+    RankTree t;
+    if (which == 0) t = tree_allreduce(p, n);
+    else if (which == 1) t = tree_reduce_scatter(p, n);
+    else if (which == 2) t = tree_pairwise(p, n);
+    else return MPI_ERR_ARG;
+    for (int i = 0; i < 32; ++i) src32[i] = t.src[i];
+    *P = t.P;
+    *pairmask = t.pairmask;
+    *chain = t.chain ? 1 : 0;
+    return MPI_SUCCESS;
+}
+
+// which: 0 = allreduce algorithm, 1 = reduce_scatter algorithm (Algo enum)
+MSX_EXPORT int msx_schedule_algo(int which, int p, int64_t count, int type_size)
+{
+    if (which == 0) return allreduce_algo(p, (size_t)count, type_size, true);
+    return reduce_scatter_algo(p, (size_t)count, type_size, true);
+}
+
+// newrank of `rank`, and the allreduce block owned by newrank n
+MSX_EXPORT int msx_schedule_newrank(int rank, int p) { return newrank_of(rank, p); }
+MSX_EXPORT int msx_schedule_block(int p, int64_t count, int n, int64_t* start, int64_t* len)
+{
+    size_t s, l;
+    allreduce_block(p, (size_t)count, allreduce_block_of_newrank(p, n), &s, &l);
+    *start = (int64_t)s;
+    *len = (int64_t)l;
+    return MPI_SUCCESS;
+}

@@ -1,0 +1,314 @@
+// msx_comm.cpp — process state, communicators, local combine, requests.
+//
+// Reference anchors:
+//   MPI_Init -> MpiProcess::Initialize (mpid/env.cpp:1062-1175)
+//   MPID_Uop_call / MPIR_Op_c_proxy (include/op.h:171-174, mpid/op.cpp:542-545)
+//   NBC requests progressed in MPI_Test/Wait (mpid/request.cpp:780-886)
+#include "msx_comm.h"
+
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <future>
+#include <mutex>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "msx_runtime.h"
+#include "msx_transport.h"
+
+namespace msx {
+
+namespace {
+
+std::atomic<bool> g_init{false};
+std::atomic<bool> g_fini{false};
+Comm g_world;
+Comm g_self;
+
+}  // namespace
+
+bool is_initialized() { return g_init.load(); }
+bool is_finalized() { return g_fini.load(); }
+Comm* world() { return g_init.load() ? &g_world : nullptr; }
+
+Comm* lookup_comm(MPI_Comm c)
+{
+    if (c == MPI_COMM_WORLD) return &g_world;
+    if (c == MPI_COMM_SELF) return &g_self;
+    return nullptr;
+}
+
+static int env_int(const char* a, const char* b, int dflt)
+{
+    const char* v = getenv(a);
+    if (!v && b) v = getenv(b);
+    return v ? atoi(v) : dflt;
+}
+
+int world_init()
+{
+    g_world = Comm{};
+    g_world.handle = MPI_COMM_WORLD;
+    g_self = Comm{};
+    g_self.handle = MPI_COMM_SELF;
+    // One process per GPU, launched by torchrun-style env (RANK, WORLD_SIZE,
+    // LOCAL_RANK, MASTER_ADDR, MASTER_PORT) or MSX_RANK / MSX_SIZE.
+    const int size = env_int("MSX_SIZE", "WORLD_SIZE", 1);
+    const int rank = env_int("MSX_RANK", "RANK", 0);
+    if (size < 1 || rank < 0 || rank >= size) {
+        set_error("bad rank/size from environment (rank=%d size=%d)", rank, size);
+        return MPI_ERR_OTHER;
+    }
+    // A host without a GPU still initialises (argument checking works); every
+    // compute call then fails loudly with MPI_ERR_OTHER.
+    (void)ensure_device();
+    g_world.rank = rank;
+    g_world.size = size;
+    if (size > 1) {
+        int rc = transport_create(rank, size, &g_world.tp);
+        if (rc != MPI_SUCCESS) return rc;
+    }
+    g_init.store(true);
+    return MPI_SUCCESS;
+}
+
+int world_finalize()
+{
+    int rc = MPI_SUCCESS;
+    if (g_world.tp) {
+        rc = g_world.tp->barrier();
+        transport_destroy(g_world.tp);
+        g_world.tp = nullptr;
+    }
+    if (ensure_device() == MPI_SUCCESS) (void)hipDeviceSynchronize();
+    g_fini.store(true);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// copies and the local combine
+// ---------------------------------------------------------------------------
+int copy_any(void* dst, const void* src, size_t bytes)
+{
+    if (bytes == 0 || dst == src) return MPI_SUCCESS;
+    BufInfo bd = classify(dst), bs = classify(src);
+    if (bd.place == Place::Host && bs.place == Place::Host) {
+        memcpy(dst, src, bytes);   // MPIR_Localcopy memcpy (mpid/pt2pt.cpp:812)
+        return MPI_SUCCESS;
+    }
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, internal_stream());
+    if (e == hipSuccess) e = hipStreamSynchronize(internal_stream());
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy");
+}
+
+int local_combine(const OpRef& op, MPI_Datatype dt, const void* in, void* inout, size_t count)
+{
+    if (count == 0) return MPI_SUCCESS;
+    if (op.opidx != O_NULL) {
+        const TypeInfo* t = type_info(dt);
+        if (!t) { set_error("datatype 0x%x has no reduction kernel", dt); return MPI_ERR_OP; }
+        return reduce_local_any(op.opidx, t->kind, in, inout, count);
+    }
+    // User-defined op: MPI_User_function is host code (mpi.h:2258-2265), called
+    // through the C proxy with int-sized chunks.  Device operands are staged
+    // to host memory around the call.
+    const int esz = type_size(dt);
+    if (esz <= 0) { set_error("datatype 0x%x not supported with user ops", dt); return MPI_ERR_TYPE; }
+    const size_t bytes = count * (size_t)esz;
+    BufInfo bi = classify(in), bo = classify(inout);
+    std::vector<char> hin, hio;
+    const char* pin = static_cast<const char*>(in);
+    char* pio = static_cast<char*>(inout);
+    int rc = MPI_SUCCESS;
+    if (bi.place == Place::Device) {
+        hin.resize(bytes);
+        if ((rc = copy_any(hin.data(), in, bytes)) != MPI_SUCCESS) return rc;
+        pin = hin.data();
+    }
+    if (bo.place == Place::Device) {
+        hio.resize(bytes);
+        if ((rc = copy_any(hio.data(), inout, bytes)) != MPI_SUCCESS) return rc;
+        pio = hio.data();
+    }
+    size_t off = 0;
+    while (off < count) {
+        size_t n = count - off;
+        if (n > 0x7fffffff) n = 0x7fffffff;
+        int len = (int)n;
+        MPI_Datatype d = dt;
+        op.user_fn(const_cast<char*>(pin) + off * esz, pio + off * esz, &len, &d);
+        off += n;
+    }
+    if (bo.place == Place::Device) rc = copy_any(inout, hio.data(), bytes);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// collectives: single-rank forms here, multi-rank forms in the transport engine
+// ---------------------------------------------------------------------------
+int coll_barrier(Comm* c)
+{
+    if (c->size == 1 || !c->tp) return MPI_SUCCESS;
+    return c->tp->barrier();
+}
+
+int coll_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                   const OpRef& op)
+{
+    if (c->size == 1) {
+        if (sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
+        return copy_any(recvbuf, sendbuf, count * (size_t)type_size(dt));
+    }
+    return engine_allreduce(c, sendbuf, recvbuf, count, dt, op);
+}
+
+int coll_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                const OpRef& op, int root)
+{
+    if (c->size == 1) {
+        if (sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
+        return copy_any(recvbuf, sendbuf, count * (size_t)type_size(dt));
+    }
+    return engine_reduce(c, sendbuf, recvbuf, count, dt, op, root);
+}
+
+int coll_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
+                        MPI_Datatype dt, const OpRef& op)
+{
+    if (c->size == 1) {
+        if (sendbuf == MPI_IN_PLACE || recvcounts[0] == 0) return MPI_SUCCESS;
+        return copy_any(recvbuf, sendbuf, (size_t)recvcounts[0] * (size_t)type_size(dt));
+    }
+    return engine_reduce_scatter(c, sendbuf, recvbuf, recvcounts, dt, op);
+}
+
+int coll_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+              const OpRef& op, bool exclusive)
+{
+    if (c->size == 1) {
+        // Exscan leaves rank 0's recvbuf undefined (unchanged here).
+        if (exclusive || sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
+        return copy_any(recvbuf, sendbuf, count * (size_t)type_size(dt));
+    }
+    return engine_scan(c, sendbuf, recvbuf, count, dt, op, exclusive);
+}
+
+// ---------------------------------------------------------------------------
+// requests: MPI_Request = 0xAC000000 | slot (type DIRECT, kind MPID_REQUEST)
+// ---------------------------------------------------------------------------
+struct Request {
+    bool live = false;
+    bool done = false;
+    int rc = MPI_SUCCESS;
+    bool has_fut = false;
+    std::shared_future<int> fut;   // collective running on the engine worker
+};
+
+namespace {
+std::mutex g_req_mu;
+std::vector<Request> g_reqs;
+constexpr int kReqBase = (int)0xAC000000;
+
+int req_alloc(MPI_Request* out, Request** r)
+{
+    std::lock_guard<std::mutex> g(g_req_mu);
+    size_t i = 0;
+    while (i < g_reqs.size() && g_reqs[i].live) ++i;
+    if (i == g_reqs.size()) g_reqs.emplace_back();
+    g_reqs[i] = Request{};
+    g_reqs[i].live = true;
+    *out = kReqBase | (int)i;
+    *r = &g_reqs[i];
+    return MPI_SUCCESS;
+}
+
+Request* req_lookup(MPI_Request h)
+{
+    std::lock_guard<std::mutex> g(g_req_mu);
+    size_t i = (size_t)(h & 0x03ffffff);
+    if ((h & (int)0xfc000000) != kReqBase || i >= g_reqs.size() || !g_reqs[i].live) return nullptr;
+    return &g_reqs[i];
+}
+
+void fill_status(MPI_Status* st, int rc)
+{
+    if (st == MPI_STATUS_IGNORE || st == nullptr) return;
+    st->MPI_SOURCE = MPI_UNDEFINED;
+    st->MPI_TAG = MPI_UNDEFINED;
+    st->MPI_ERROR = rc;
+    st->internal[0] = st->internal[1] = 0;
+}
+
+}  // namespace
+
+int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req)
+{
+    Request* r;
+    if (c->size > 1) {
+        // The engine worker runs it behind every earlier collective; the
+        // caller overlaps host work until MPI_Test/MPI_Wait.
+        std::shared_future<int> f = engine_async(std::move(body));
+        req_alloc(req, &r);
+        r->fut = f;
+        r->has_fut = true;
+        return MPI_SUCCESS;
+    }
+    int rc = body();
+    req_alloc(req, &r);
+    r->done = true;
+    r->rc = rc;
+    return MPI_SUCCESS;
+}
+
+int request_start_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count,
+                            MPI_Datatype dt, const OpRef& op, MPI_Request* req)
+{
+    return request_start_generic(
+        c, [=] { return count ? coll_allreduce(c, sendbuf, recvbuf, count, dt, op) : MPI_SUCCESS; },
+        req);
+}
+
+int request_test(MPI_Request* req, int* flag, MPI_Status* st)
+{
+    if (*req == MPI_REQUEST_NULL) { *flag = 1; fill_status(st, MPI_SUCCESS); return MPI_SUCCESS; }
+    Request* r = req_lookup(*req);
+    if (!r) { set_error("invalid request"); return MPI_ERR_REQUEST; }
+    if (!r->done && r->has_fut) {
+        if (r->fut.wait_for(std::chrono::seconds(0)) != std::future_status::ready) {
+            *flag = 0;
+            return MPI_SUCCESS;
+        }
+        r->done = true;
+        r->rc = r->fut.get();
+    }
+    *flag = 1;
+    int rc = r->rc;
+    r->fut = std::shared_future<int>();
+    {
+        std::lock_guard<std::mutex> g(g_req_mu);
+        r->live = false;
+    }
+    *req = MPI_REQUEST_NULL;
+    fill_status(st, rc);
+    return rc;
+}
+
+int request_wait(MPI_Request* req, MPI_Status* st)
+{
+    if (*req == MPI_REQUEST_NULL) { fill_status(st, MPI_SUCCESS); return MPI_SUCCESS; }
+    Request* r = req_lookup(*req);
+    if (!r) { set_error("invalid request"); return MPI_ERR_REQUEST; }
+    if (!r->done && r->has_fut) {
+        r->rc = r->fut.get();
+        r->done = true;
+    }
+    int flag;
+    return request_test(req, &flag, st);
+}
+
+}  // namespace msx

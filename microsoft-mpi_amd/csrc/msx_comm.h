@@ -1,0 +1,69 @@
+// msx_comm.h — communicators, user ops and the collective engine interface.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <functional>
+#include <vector>
+
+#include "msx_types.h"
+
+namespace msx {
+
+class Transport;   // msx_transport.h
+
+struct Comm {
+    MPI_Comm handle = MPI_COMM_NULL;
+    int rank = 0;
+    int size = 1;
+    MPI_Errhandler errhandler = MPI_ERRORS_ARE_FATAL;
+    Transport* tp = nullptr;   // null when size == 1
+};
+
+// MPI_COMM_WORLD / MPI_COMM_SELF; nullptr for anything else.
+Comm* lookup_comm(MPI_Comm c);
+
+// Resolved op (builtin kernel or user function), MPID_Op (include/op.h:82-134).
+struct OpRef {
+    int opidx = O_NULL;                 // builtin index, or O_NULL for user ops
+    MPI_User_function* user_fn = nullptr;
+    bool commutative = true;
+};
+
+// Process state (init/finalize, world bootstrap).
+bool is_initialized();
+bool is_finalized();
+int world_init();          // MPI_Init body: device + (multi-rank) bootstrap
+int world_finalize();
+Comm* world();
+
+// Reduction collectives over `comm` (arguments already validated).
+// `kind` is the element class of `dt` (K_NONE for user ops on non-reducible types).
+int coll_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                   const OpRef& op);
+int coll_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                const OpRef& op, int root);
+int coll_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
+                        MPI_Datatype dt, const OpRef& op);
+int coll_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+              const OpRef& op, bool exclusive);
+int coll_barrier(Comm* c);
+
+// Local combine with any op (builtin -> GPU kernel; user fn -> host call).
+int local_combine(const OpRef& op, MPI_Datatype dt, const void* in, void* inout, size_t count);
+
+// Copy `bytes` between any two buffers (host or device), blocking.
+int copy_any(void* dst, const void* src, size_t bytes);
+
+// Non-blocking requests (stream/event backed).
+struct Request;
+int request_start_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count,
+                            MPI_Datatype dt, const OpRef& op, MPI_Request* req);
+// Start `body` as a request: on the engine worker when c->size > 1 (true
+// overlap with the caller), inline otherwise.
+int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req);
+int request_wait(MPI_Request* req, MPI_Status* st);
+int request_test(MPI_Request* req, int* flag, MPI_Status* st);
+
+}  // namespace msx

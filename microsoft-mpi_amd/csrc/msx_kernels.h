@@ -1,0 +1,55 @@
+// msx_kernels.h — host-side launch interface of the gfx950 combine kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include "msx_types.h"
+
+namespace msx {
+
+// Launch geometry of the streaming combine.
+struct LaunchCfg {
+    int variant = 0;      // fp32-SUM tuning variant (0 = default); other pairs ignore it
+    int grid_cap = 0;     // 0 = one tile per workgroup (no grid-stride), else max workgroups
+};
+
+// inout[i] = op(inout[i], in[i]) for i in [0, count), stream-ordered on `s`.
+// in / inout must be device-accessible from the current device.
+// Returns hipSuccess, or hipErrorInvalidValue for a pair with no kernel.
+hipError_t launch_combine(int opidx, Kind k, const void* in, void* inout, size_t count,
+                          hipStream_t s, const LaunchCfg& cfg);
+
+// Reference-order tree combine over p inputs (p = 1..8):
+//   out[i] = T(srcs[0][i], ..., srcs[p-1][i]) where T is the balanced binary
+//   tree of the reference's recursive-halving/doubling schedules with the
+//   left operand as `inout`:  ((s0 op s1) op (s2 op s3)) op ((s4 op s5) op ...)
+// `srcs` is a device-visible array of p pointers (may be peer pointers).
+// `out` may alias srcs[0].
+hipError_t launch_tree(int opidx, Kind k, const void* const* srcs_dev, int p, void* out,
+                       size_t count, hipStream_t s);
+
+// General schedule-faithful combine (see k_tree in msx_kernels.hip):
+//   chain == false: P (power of two <= 16) leaves; leaf i = src[2i] if bit i of
+//     pairmask is clear, else src[2i] op src[2i+1] (the non-power-of-two fold);
+//     then the balanced tree over the leaves, left operand = inout.
+//   chain == true: ((src[0] op src[1]) op src[2]) ... op src[P-1], P <= 16.
+struct TreeSpec {
+    const void* src[32] = {};
+    int P = 1;
+    unsigned pairmask = 0;
+    bool chain = false;
+    bool sys = false;   // sources/output shared with peers: system acquire/release
+};
+hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t count,
+                            hipStream_t s);
+
+// Copy nseg independent byte ranges in one launch (one grid row per segment),
+// used to pull allgather blocks from every peer concurrently.
+hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size_t* nbytes,
+                            int nseg, bool sys, hipStream_t s);
+
+// Number of tuning variants compiled for the fp32 SUM hot path.
+int combine_variant_count();
+const char* combine_variant_name(int v);
+
+}  // namespace msx

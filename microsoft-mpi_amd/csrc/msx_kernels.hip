@@ -1,0 +1,628 @@
+// msx_kernels.hip — gfx950 (CDNA4) element-wise MPI_Op combine kernels.
+//
+// What the reference does (src/mpi/msmpi/mpid/op.cpp:14-160): a scalar loop
+// `inout[i] = inout[i] (op) in[i]` per (op, C type).  What this file does:
+// the same element semantics as a memory-bound stream on MI355X:
+//   * 16-byte (dwordx4) coalesced loads/stores per lane; a 64-lane wave moves
+//     1 KiB per instruction per operand;
+//   * UNROLL independent vectors per lane per operand in flight before the
+//     first use, so each CU keeps enough HBM requests outstanding
+//     (MI355X_MICROARCH.md: ~10 B/cyc/CU HBM-bound dwordx4);
+//   * one tile of BLOCK*UNROLL vectors per workgroup: >> 256 CUs x 8 XCDs for
+//     the benchmark sizes; full tiles run with no bounds checks;
+//   * head/tail elements (unaligned start, ragged end) are handled by the same
+//     launch with scalar element loads, so every (pointer, count) is legal;
+//   * no MFMA: arithmetic intensity is 1 op per 3 x sizeof(T) bytes.
+// Numerics: compiled with -ffp-contract=off and IEEE denormals so every
+// float result is the single correctly-rounded IEEE op the reference performs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <type_traits>
+
+#include "msx_kernels.h"
+
+namespace msx {
+namespace dev {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ---- element types (layouts of op.cpp:280-340, padding made explicit so a
+// struct assignment copies every byte like the reference's `*this = rhs`) ----
+struct c32 { float re, im; };
+struct c64 { double re, im; };
+struct loc_ii { int32_t v; int32_t l; };
+struct loc_fi { float v; int32_t l; };
+struct loc_si { int16_t v; int16_t pad; int32_t l; };
+struct loc_di { double v; int32_t l; int32_t pad; };
+struct loc_ff { float v; float l; };
+struct loc_dd { double v; double l; };
+static_assert(sizeof(loc_si) == 8 && sizeof(loc_di) == 16, "loc layout");
+
+// ---- integer arithmetic with two's-complement wrap (MSVC semantics) -------
+template <class T> struct Wrap {
+    using U = typename std::make_unsigned<T>::type;
+    using W = typename std::conditional<(sizeof(T) < 4), uint32_t, U>::type;
+    __device__ static T add(T a, T b) { return (T)(U)((W)(U)a + (W)(U)b); }
+    __device__ static T mul(T a, T b) { return (T)(U)((W)(U)a * (W)(U)b); }
+};
+
+// ---- op functors: apply(inout, in) -> new inout ---------------------------
+template <int OP> struct Fn;
+
+// Op<T>::Max/Min (op.cpp:18-40): minwindef.h max(inout,in) = inout>in?inout:in
+template <> struct Fn<O_MAX> {
+    template <class T> __device__ static T apply(T io, T in) { return io > in ? io : in; }
+};
+template <> struct Fn<O_MIN> {
+    template <class T> __device__ static T apply(T io, T in) { return io < in ? io : in; }
+};
+
+// Op<T>::Sum (op.cpp:42-52) and complex += (op.cpp:287-292)
+template <> struct Fn<O_SUM> {
+    template <class T>
+    __device__ static typename std::enable_if<std::is_integral<T>::value, T>::type apply(T io, T in)
+    { return Wrap<T>::add(io, in); }
+    __device__ static float apply(float io, float in) { return io + in; }
+    __device__ static double apply(double io, double in) { return io + in; }
+    __device__ static c32 apply(c32 io, c32 in) { return c32{io.re + in.re, io.im + in.im}; }
+    __device__ static c64 apply(c64 io, c64 in) { return c64{io.re + in.re, io.im + in.im}; }
+};
+
+// Op<T>::Prod (op.cpp:54-64) and complex *= (op.cpp:294-303): 4 mul + 2 add,
+// each rounded (no FMA contraction).
+template <class C> __device__ inline C cmul(C io, C in)
+{
+#pragma clang fp contract(off)
+    auto r = (io.re * in.re) - (io.im * in.im);
+    auto i = (io.re * in.im) + (in.re * io.im);
+    return C{r, i};
+}
+template <> struct Fn<O_PROD> {
+    template <class T>
+    __device__ static typename std::enable_if<std::is_integral<T>::value, T>::type apply(T io, T in)
+    { return Wrap<T>::mul(io, in); }
+    __device__ static float apply(float io, float in) { return io * in; }
+    __device__ static double apply(double io, double in) { return io * in; }
+    __device__ static c32 apply(c32 io, c32 in) { return cmul(io, in); }
+    __device__ static c64 apply(c64 io, c64 in) { return cmul(io, in); }
+};
+
+// Op<T>::LogicalAnd/Or/Xor (op.cpp:66-124): C truthiness, stored as T(0/1).
+template <> struct Fn<O_LAND> {
+    template <class T> __device__ static T apply(T io, T in)
+    { return (T)((io != (T)0) && (in != (T)0)); }
+};
+template <> struct Fn<O_LOR> {
+    template <class T> __device__ static T apply(T io, T in)
+    { return (T)((io != (T)0) || (in != (T)0)); }
+};
+template <> struct Fn<O_LXOR> {
+    template <class T> __device__ static T apply(T io, T in)
+    {
+        bool a = io != (T)0, b = in != (T)0;
+        return (T)((a && !b) || (!a && b));
+    }
+};
+
+// Op<T>::Bitwise* (op.cpp:78-136): byte-independent, so they run on raw words.
+template <> struct Fn<O_BAND> {
+    template <class T> __device__ static T apply(T io, T in) { return (T)(io & in); }
+};
+template <> struct Fn<O_BOR> {
+    template <class T> __device__ static T apply(T io, T in) { return (T)(io | in); }
+};
+template <> struct Fn<O_BXOR> {
+    template <class T> __device__ static T apply(T io, T in) { return (T)(io ^ in); }
+};
+
+// loctype<V,L>::MaxLoc/MinLoc (op.cpp:315-339)
+template <> struct Fn<O_MAXLOC> {
+    template <class T> __device__ static T apply(T io, T in)
+    {
+        if (io.v == in.v) { io.l = io.l < in.l ? io.l : in.l; return io; }
+        return (io.v < in.v) ? in : io;
+    }
+};
+template <> struct Fn<O_MINLOC> {
+    template <class T> __device__ static T apply(T io, T in)
+    {
+        if (io.v == in.v) { io.l = io.l < in.l ? io.l : in.l; return io; }
+        return (io.v > in.v) ? in : io;
+    }
+};
+
+// ---- 16-byte vector apply ------------------------------------------------------
+template <int OP, class VT>
+__device__ __forceinline__ u32x4 apply_vec(u32x4 io, u32x4 in)
+{
+    constexpr int N = 16 / (int)sizeof(VT);
+    VT a[N], b[N];
+    __builtin_memcpy(a, &io, 16);
+    __builtin_memcpy(b, &in, 16);
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = Fn<OP>::apply(a[j], b[j]);
+    u32x4 r;
+    __builtin_memcpy(&r, a, 16);
+    return r;
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4* p, u32x4 v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// ---- the streaming combine -------------------------------------------------------
+// Elements [0, head) and [head + nvec*EPV, head + nvec*EPV + tail) are scalar;
+// the vector body starts at element `head`, 16-byte aligned for both operands.
+// T  = element type used for scalar elements;
+// VT = lane type used inside a 16-byte vector (== T except bitwise ops, which
+//      run on 32-bit words regardless of the MPI element type).
+template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
+__global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* __restrict__ io,
+                                                   size_t head, size_t nvec, size_t tail)
+{
+    constexpr size_t EPV = 16 / sizeof(T);
+    constexpr size_t TILE = (size_t)BLOCK * UNROLL;
+    const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in + head);
+    u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
+
+    for (size_t t0 = (size_t)blockIdx.x * TILE; t0 < nvec; t0 += (size_t)gridDim.x * TILE) {
+        const size_t i0 = t0 + threadIdx.x;
+        if (t0 + TILE <= nvec) {
+            u32x4 a[UNROLL], b[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                a[u] = ld<NTLD>(vin + i0 + (size_t)u * BLOCK);
+                b[u] = ld<NTLD>(vio + i0 + (size_t)u * BLOCK);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+                st<NTST>(vio + i0 + (size_t)u * BLOCK, apply_vec<OP, VT>(b[u], a[u]));
+        } else {
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const size_t i = i0 + (size_t)u * BLOCK;
+                if (i < nvec) vio[i] = apply_vec<OP, VT>(vio[i], vin[i]);
+            }
+        }
+    }
+
+    const size_t nscalar = head + tail;
+    if (nscalar) {
+        const size_t body_end = head + nvec * EPV;
+        for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nscalar;
+             s += (size_t)gridDim.x * BLOCK) {
+            const size_t e = s < head ? s : body_end + (s - head);
+            io[e] = Fn<OP>::apply(io[e], in[e]);
+        }
+    }
+}
+
+// ---- reference-order multi-input combine ----------------------------------------
+// One pass over up to 2*kMaxLeaves inputs that reproduces the association AND
+// the inout/in roles of the reference's multi-step schedules:
+//   tree  (chain == 0): leaf_k = pair_k ? f(s[2k], s[2k+1]) : s[2k], k < P (pow2),
+//         then the balanced tree ((l0 op l1) op (l2 op l3)) op ... with the left
+//         operand always in the `inout` role (recursive doubling / halving,
+//         reduce.cpp:3890-4009, 1088-1175; the non-power-of-two fold is the
+//         leaf pair, reduce.cpp:3835-3871);
+//   chain (chain == 1): ((s0 op s1) op s2) op ... op s[P-1] (pairwise exchange,
+//         reduce.cpp:1258-1318).
+constexpr int kMaxLeaves = 16;
+struct TreeArgs {
+    const void* s[2 * kMaxLeaves];
+    int P;
+    unsigned pairmask;
+    int chain;
+    int sys;   // sources/outputs shared with other GPUs: system-coherent access
+};
+
+// Start-of-kernel system acquire: invalidate this CU's L1 and the XCD's L2
+// lines for memory other GPUs may have written since (peer HBM over xGMI).
+__device__ __forceinline__ void acquire_system()
+{
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __syncthreads();
+}
+
+// End-of-kernel system release: write this XCD's dirty L2 lines back so peers
+// reading over xGMI see them (one fence per workgroup).
+__device__ __forceinline__ void release_system()
+{
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+template <class F, class V, class LD>
+__device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
+{
+    if (a.chain) {
+        V v = load(0);
+        for (int k = 1; k < a.P; ++k) v = F::apply(v, load(k));
+        return v;
+    }
+    V v[kMaxLeaves];
+#pragma unroll
+    for (int k = 0; k < kMaxLeaves; ++k) {
+        if (k < a.P) {
+            v[k] = load(2 * k);
+            if ((a.pairmask >> k) & 1u) v[k] = F::apply(v[k], load(2 * k + 1));
+        }
+    }
+#pragma unroll
+    for (int w = 1; w < kMaxLeaves; w *= 2) {
+#pragma unroll
+        for (int k = 0; k + w < kMaxLeaves; k += 2 * w)
+            if (k + w < a.P) v[k] = F::apply(v[k], v[k + w]);
+    }
+    return v[0];
+}
+
+template <int OP, class VT> struct VecFn {
+    __device__ static u32x4 apply(u32x4 io, u32x4 in) { return apply_vec<OP, VT>(io, in); }
+};
+
+template <int OP, class T, class VT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out, size_t nvec,
+                                                size_t tail, int vec_ok)
+{
+    constexpr size_t EPV = 16 / sizeof(T);
+    const size_t stride = (size_t)gridDim.x * BLOCK;
+    if (a.sys) acquire_system();
+    if (vec_ok) {
+        for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < nvec; i += stride) {
+            auto load = [&](int k) { return reinterpret_cast<const u32x4*>(a.s[k])[i]; };
+            reinterpret_cast<u32x4*>(out)[i] = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
+        }
+    }
+    const size_t first = vec_ok ? nvec * EPV : 0;
+    const size_t nsc = vec_ok ? tail : tail + nvec * EPV;
+    for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nsc; s += stride) {
+        auto load = [&](int k) { return reinterpret_cast<const T*>(a.s[k])[first + s]; };
+        out[first + s] = tree_eval<Fn<OP>, T>(a, load);
+    }
+    if (a.sys) release_system();
+}
+
+// ---- multi-segment copy (allgather phase: blocks pulled from peers) -------------
+constexpr int kMaxSegs = 32;
+struct CopySegs {
+    const void* src[kMaxSegs];
+    void* dst[kMaxSegs];
+    size_t nbytes[kMaxSegs];
+    int n;
+    int sys;
+};
+
+__global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
+{
+    // blockIdx.y selects the segment so every source link is busy at once.
+    const int sg = blockIdx.y;
+    if (c.sys) acquire_system();
+    const char* src = static_cast<const char*>(c.src[sg]);
+    char* dst = static_cast<char*>(c.dst[sg]);
+    const size_t nb = c.nbytes[sg];
+    const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t done = 0;
+    if (vec) {
+        const size_t nv = nb / 16;
+        const u32x4* s = reinterpret_cast<const u32x4*>(src);
+        u32x4* d = reinterpret_cast<u32x4*>(dst);
+        size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+        for (; i + 3 * stride < nv; i += 4 * stride) {
+            u32x4 a0 = s[i], a1 = s[i + stride], a2 = s[i + 2 * stride], a3 = s[i + 3 * stride];
+            d[i] = a0; d[i + stride] = a1; d[i + 2 * stride] = a2; d[i + 3 * stride] = a3;
+        }
+        for (; i < nv; i += stride) d[i] = s[i];
+        done = nv * 16;
+    }
+    for (size_t i = done + (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
+    if (c.sys) release_system();
+}
+
+}  // namespace dev
+
+// =====================================================================================
+// host-side dispatch
+// =====================================================================================
+namespace {
+
+using namespace dev;
+
+constexpr int kBlock = 256;
+constexpr int kUnroll = 4;
+
+template <class T>
+inline void split(const void* in, const void* io, size_t count, size_t& head, size_t& nvec,
+                  size_t& tail)
+{
+    constexpr size_t ES = sizeof(T);
+    const uintptr_t a = (uintptr_t)in, b = (uintptr_t)io;
+    if ((a & 15) != (b & 15) || (a % ES) != 0 || (b % ES) != 0 || (ES == 16 && (a & 15))) {
+        head = count; nvec = 0; tail = 0;   // alignments disagree: all-scalar
+        return;
+    }
+    size_t h = ((16 - (a & 15)) & 15) / ES;
+    if (h > count) h = count;
+    const size_t rest = count - h;
+    const size_t epv = 16 / ES;
+    head = h; nvec = rest / epv; tail = rest - nvec * epv;
+}
+
+template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
+hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
+{
+    size_t head, nvec, tail;
+    split<T>(in, io, count, head, nvec, tail);
+    const size_t tile = (size_t)BLOCK * UNROLL;
+    size_t grid = (nvec + tile - 1) / tile;
+    const size_t sc = (head + tail + BLOCK - 1) / BLOCK;
+    if (grid < sc) grid = sc;
+    if (grid == 0) return hipSuccess;
+    if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
+    if (grid > 0x7fffffffu) grid = 0x7fffffffu;
+    hipLaunchKernelGGL((k_combine<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
+                       dim3(BLOCK), 0, s, static_cast<const T*>(in), static_cast<T*>(io), head,
+                       nvec, tail);
+    return hipGetLastError();
+}
+
+template <int OP, class T>
+hipError_t run_default(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
+{
+    return run_combine<OP, T, T, kUnroll, kBlock, false, false>(in, io, count, s, cfg);
+}
+
+// Bitwise ops: byte-granular scalars, 32-bit lanes inside vectors.
+template <int OP>
+hipError_t run_bitwise(const void* in, void* io, size_t nbytes, hipStream_t s, const LaunchCfg& cfg)
+{
+    return run_combine<OP, uint8_t, uint32_t, kUnroll, kBlock, false, false>(in, io, nbytes, s, cfg);
+}
+
+// fp32 SUM tuning variants (the benchmark's hot path).
+struct Variant {
+    const char* name;
+    hipError_t (*fn)(const void*, void*, size_t, hipStream_t, const LaunchCfg&);
+};
+const Variant kF32SumVariants[] = {
+    {"u4_b256", run_combine<O_SUM, float, float, 4, 256, false, false>},
+    {"u4_b256_ntld", run_combine<O_SUM, float, float, 4, 256, true, false>},
+    {"u4_b256_ntall", run_combine<O_SUM, float, float, 4, 256, true, true>},
+    {"u8_b256", run_combine<O_SUM, float, float, 8, 256, false, false>},
+    {"u8_b256_ntld", run_combine<O_SUM, float, float, 8, 256, true, false>},
+    {"u2_b256", run_combine<O_SUM, float, float, 2, 256, false, false>},
+    {"u1_b256", run_combine<O_SUM, float, float, 1, 256, false, false>},
+    {"u4_b512", run_combine<O_SUM, float, float, 4, 512, false, false>},
+    {"u2_b512", run_combine<O_SUM, float, float, 2, 512, false, false>},
+    {"u8_b128", run_combine<O_SUM, float, float, 8, 128, false, false>},
+    {"u16_b256_ntld", run_combine<O_SUM, float, float, 16, 256, true, false>},
+};
+constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
+
+template <int OP>
+hipError_t dispatch_arith(Kind k, const void* in, void* io, size_t n, hipStream_t s,
+                          const LaunchCfg& c)
+{
+    switch (k) {
+    case K_I8:  return run_default<OP, int8_t>(in, io, n, s, c);
+    case K_U8:  return run_default<OP, uint8_t>(in, io, n, s, c);
+    case K_I16: return run_default<OP, int16_t>(in, io, n, s, c);
+    case K_U16: return run_default<OP, uint16_t>(in, io, n, s, c);
+    case K_I32: return run_default<OP, int32_t>(in, io, n, s, c);
+    case K_U32: return run_default<OP, uint32_t>(in, io, n, s, c);
+    case K_I64: return run_default<OP, int64_t>(in, io, n, s, c);
+    case K_U64: return run_default<OP, uint64_t>(in, io, n, s, c);
+    case K_F32: return run_default<OP, float>(in, io, n, s, c);
+    case K_F64: return run_default<OP, double>(in, io, n, s, c);
+    default: break;
+    }
+    if constexpr (OP == O_SUM || OP == O_PROD) {
+        if (k == K_C32) return run_default<OP, c32>(in, io, n, s, c);
+        if (k == K_C64) return run_default<OP, c64>(in, io, n, s, c);
+    }
+    if constexpr (OP == O_LAND || OP == O_LOR || OP == O_LXOR) {
+        if (k == K_BOOL) return run_default<OP, uint8_t>(in, io, n, s, c);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int OP>
+hipError_t dispatch_loc(Kind k, const void* in, void* io, size_t n, hipStream_t s,
+                        const LaunchCfg& c)
+{
+    switch (k) {
+    case K_LOC_II: return run_default<OP, loc_ii>(in, io, n, s, c);
+    case K_LOC_FI: return run_default<OP, loc_fi>(in, io, n, s, c);
+    case K_LOC_SI: return run_default<OP, loc_si>(in, io, n, s, c);
+    case K_LOC_DI: return run_default<OP, loc_di>(in, io, n, s, c);
+    case K_LOC_FF: return run_default<OP, loc_ff>(in, io, n, s, c);
+    case K_LOC_DD: return run_default<OP, loc_dd>(in, io, n, s, c);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// ---- tree dispatch ----
+template <int OP, class T, class VT>
+hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
+{
+    bool ok = ((uintptr_t)out & 15) == 0;
+    for (int k = 0; k < nsrc; ++k) ok = ok && a.s[k] && (((uintptr_t)a.s[k] & 15) == 0);
+    constexpr size_t ES = sizeof(T);
+    const size_t epv = 16 / ES;
+    const size_t nvec = count / epv, tail = count - nvec * epv;
+    const size_t work = ok ? nvec + tail : count;
+    size_t grid = (work + kBlock - 1) / kBlock;
+    if (grid > 4096) grid = 4096;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_tree<OP, T, VT, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, s, a,
+                       static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
+    return hipGetLastError();
+}
+
+template <int OP>
+hipError_t tree_arith(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
+{
+    switch (k) {
+    case K_I8:  return run_tree<OP, int8_t, int8_t>(a, ns, out, n, s);
+    case K_U8:  return run_tree<OP, uint8_t, uint8_t>(a, ns, out, n, s);
+    case K_I16: return run_tree<OP, int16_t, int16_t>(a, ns, out, n, s);
+    case K_U16: return run_tree<OP, uint16_t, uint16_t>(a, ns, out, n, s);
+    case K_I32: return run_tree<OP, int32_t, int32_t>(a, ns, out, n, s);
+    case K_U32: return run_tree<OP, uint32_t, uint32_t>(a, ns, out, n, s);
+    case K_I64: return run_tree<OP, int64_t, int64_t>(a, ns, out, n, s);
+    case K_U64: return run_tree<OP, uint64_t, uint64_t>(a, ns, out, n, s);
+    case K_F32: return run_tree<OP, float, float>(a, ns, out, n, s);
+    case K_F64: return run_tree<OP, double, double>(a, ns, out, n, s);
+    default: break;
+    }
+    if constexpr (OP == O_SUM || OP == O_PROD) {
+        if (k == K_C32) return run_tree<OP, c32, c32>(a, ns, out, n, s);
+        if (k == K_C64) return run_tree<OP, c64, c64>(a, ns, out, n, s);
+    }
+    if constexpr (OP == O_LAND || OP == O_LOR || OP == O_LXOR) {
+        if (k == K_BOOL) return run_tree<OP, uint8_t, uint8_t>(a, ns, out, n, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int OP>
+hipError_t tree_loc(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
+{
+    switch (k) {
+    case K_LOC_II: return run_tree<OP, loc_ii, loc_ii>(a, ns, out, n, s);
+    case K_LOC_FI: return run_tree<OP, loc_fi, loc_fi>(a, ns, out, n, s);
+    case K_LOC_SI: return run_tree<OP, loc_si, loc_si>(a, ns, out, n, s);
+    case K_LOC_DI: return run_tree<OP, loc_di, loc_di>(a, ns, out, n, s);
+    case K_LOC_FF: return run_tree<OP, loc_ff, loc_ff>(a, ns, out, n, s);
+    case K_LOC_DD: return run_tree<OP, loc_dd, loc_dd>(a, ns, out, n, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+int combine_variant_count() { return kNumVariants; }
+const char* combine_variant_name(int v)
+{
+    return (v >= 0 && v < kNumVariants) ? kF32SumVariants[v].name : nullptr;
+}
+
+hipError_t launch_combine(int opidx, Kind k, const void* in, void* io, size_t n, hipStream_t s,
+                          const LaunchCfg& c)
+{
+    if (n == 0) return hipSuccess;
+    switch (opidx) {
+    case O_SUM:
+        if (k == K_F32 && c.variant > 0 && c.variant < kNumVariants)
+            return kF32SumVariants[c.variant].fn(in, io, n, s, c);
+        return dispatch_arith<O_SUM>(k, in, io, n, s, c);
+    case O_MAX:  return dispatch_arith<O_MAX>(k, in, io, n, s, c);
+    case O_MIN:  return dispatch_arith<O_MIN>(k, in, io, n, s, c);
+    case O_PROD: return dispatch_arith<O_PROD>(k, in, io, n, s, c);
+    case O_LAND: return dispatch_arith<O_LAND>(k, in, io, n, s, c);
+    case O_LOR:  return dispatch_arith<O_LOR>(k, in, io, n, s, c);
+    case O_LXOR: return dispatch_arith<O_LXOR>(k, in, io, n, s, c);
+    case O_BAND: return run_bitwise<O_BAND>(in, io, n * kind_size(k), s, c);
+    case O_BOR:  return run_bitwise<O_BOR>(in, io, n * kind_size(k), s, c);
+    case O_BXOR: return run_bitwise<O_BXOR>(in, io, n * kind_size(k), s, c);
+    case O_MAXLOC: return dispatch_loc<O_MAXLOC>(k, in, io, n, s, c);
+    case O_MINLOC: return dispatch_loc<O_MINLOC>(k, in, io, n, s, c);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_tree(int opidx, Kind k, const void* const* srcs, int p, void* out, size_t n,
+                       hipStream_t s)
+{
+    // Plain balanced tree over p (power of two) inputs, no pairs.
+    if (p < 1 || p > kMaxLeaves || (p & (p - 1))) return hipErrorInvalidValue;
+    TreeSpec t;
+    t.P = p;
+    t.pairmask = 0;
+    t.chain = false;
+    for (int i = 0; i < p; ++i) t.src[2 * i] = srcs[i];
+    return launch_tree_spec(opidx, k, t, out, n, s);
+}
+
+hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    if (t.P < 1 || t.P > kMaxLeaves) return hipErrorInvalidValue;
+    TreeArgs a{};
+    int ns;
+    if (t.chain) {
+        for (int i = 0; i < t.P; ++i) a.s[i] = t.src[i];
+        ns = t.P;
+    } else {
+        if (t.P & (t.P - 1)) return hipErrorInvalidValue;
+        for (int i = 0; i < 2 * t.P; ++i) a.s[i] = t.src[i];
+        ns = 0;
+        for (int i = 0; i < t.P; ++i) {
+            if (!t.src[2 * i]) return hipErrorInvalidValue;
+            if ((t.pairmask >> i) & 1u) { if (!t.src[2 * i + 1]) return hipErrorInvalidValue; }
+            else a.s[2 * i + 1] = t.src[2 * i];   // keep alignment check simple
+        }
+        ns = 2 * t.P;
+    }
+    a.P = t.P;
+    a.pairmask = t.pairmask;
+    a.chain = t.chain ? 1 : 0;
+    a.sys = t.sys ? 1 : 0;
+    if (!t.chain && t.P == 1 && t.pairmask == 0) {
+        if (t.src[0] == out) return hipSuccess;
+        return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
+    }
+    switch (opidx) {
+    case O_SUM:  return tree_arith<O_SUM>(k, a, ns, out, n, s);
+    case O_MAX:  return tree_arith<O_MAX>(k, a, ns, out, n, s);
+    case O_MIN:  return tree_arith<O_MIN>(k, a, ns, out, n, s);
+    case O_PROD: return tree_arith<O_PROD>(k, a, ns, out, n, s);
+    case O_LAND: return tree_arith<O_LAND>(k, a, ns, out, n, s);
+    case O_LOR:  return tree_arith<O_LOR>(k, a, ns, out, n, s);
+    case O_LXOR: return tree_arith<O_LXOR>(k, a, ns, out, n, s);
+    case O_BAND: return run_tree<O_BAND, uint8_t, uint32_t>(a, ns, out, n * kind_size(k), s);
+    case O_BOR:  return run_tree<O_BOR, uint8_t, uint32_t>(a, ns, out, n * kind_size(k), s);
+    case O_BXOR: return run_tree<O_BXOR, uint8_t, uint32_t>(a, ns, out, n * kind_size(k), s);
+    case O_MAXLOC: return tree_loc<O_MAXLOC>(k, a, ns, out, n, s);
+    case O_MINLOC: return tree_loc<O_MINLOC>(k, a, ns, out, n, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
+                            bool sys, hipStream_t s)
+{
+    for (int base = 0; base < nseg; base += kMaxSegs) {
+        CopySegs c{};
+        c.sys = sys ? 1 : 0;
+        c.n = (nseg - base < kMaxSegs) ? nseg - base : kMaxSegs;
+        size_t maxb = 0;
+        for (int i = 0; i < c.n; ++i) {
+            c.src[i] = src[base + i];
+            c.dst[i] = dst[base + i];
+            c.nbytes[i] = nbytes[base + i];
+            if (c.nbytes[i] > maxb) maxb = c.nbytes[i];
+        }
+        if (maxb == 0) continue;
+        size_t gx = (maxb / 16 + 1023) / 1024;
+        if (gx < 1) gx = 1;
+        if (gx > 512) gx = 512;
+        hipLaunchKernelGGL(k_copy_segs, dim3((unsigned)gx, (unsigned)c.n), dim3(256), 0, s, c);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace msx

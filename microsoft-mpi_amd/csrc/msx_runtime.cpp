@@ -1,0 +1,236 @@
+// msx_runtime.cpp — device bring-up, buffer placement and the host-staged path.
+//
+// The reference combines in place on host memory (op.cpp:42-52).  On MI355X
+// the combine always runs on the GPU; host-resident MPI buffers are streamed
+// through HBM in chunks: H2D(in), H2D(inout) -> combine -> D2H(inout), with two
+// HIP streams so chunk i+1's copies overlap chunk i's combine and copy-back.
+// There is no CPU fallback: without a GPU the call fails with MPI_ERR_OTHER.
+#include "msx_runtime.h"
+
+#include <mutex>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+namespace msx {
+
+namespace {
+
+thread_local char g_err[512];
+
+struct DevState {
+    std::once_flag once;
+    int rc = MPI_ERR_OTHER;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    // host staging
+    std::mutex stage_mu;
+    size_t chunk = 64u << 20;       // bytes per staged chunk and operand
+    void* stage_in[2] = {nullptr, nullptr};
+    void* stage_io[2] = {nullptr, nullptr};
+    hipStream_t stage_s[2] = {nullptr, nullptr};
+    size_t stage_cap = 0;
+};
+
+DevState& ds()
+{
+    static DevState s;
+    return s;
+}
+
+LaunchCfg g_cfg;
+
+}  // namespace
+
+void set_error(const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+const char* last_error() { return g_err; }
+
+int hip_fail(hipError_t e, const char* what)
+{
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return MPI_ERR_OTHER;
+}
+
+LaunchCfg& launch_cfg() { return g_cfg; }
+
+int device_count_noinit()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ensure_device()
+{
+    DevState& s = ds();
+    std::call_once(s.once, [&s] {
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess || n == 0) {
+            s.rc = MPI_ERR_OTHER;
+            return;
+        }
+        // One rank per GPU: LOCAL_RANK (torchrun) or MSX_DEVICE picks the card.
+        int dev = 0;
+        if (const char* v = getenv("MSX_DEVICE")) dev = atoi(v);
+        else if (const char* v = getenv("LOCAL_RANK")) dev = atoi(v);
+        dev = ((dev % n) + n) % n;
+        if (hipSetDevice(dev) != hipSuccess) return;
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return;
+        s.device = dev;
+        s.rc = MPI_SUCCESS;
+    });
+    if (s.rc != MPI_SUCCESS) {
+        set_error("no usable MI355X (gfx950) device: the HIP reduction path cannot run "
+                  "(hipGetDeviceCount reports %d)", device_count_noinit());
+        return s.rc;
+    }
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != s.device) (void)hipSetDevice(s.device);
+    return MPI_SUCCESS;
+}
+
+int current_device() { return ds().device; }
+hipStream_t internal_stream() { return ds().stream; }
+
+void set_staging_chunk(size_t bytes)
+{
+    DevState& s = ds();
+    std::lock_guard<std::mutex> g(s.stage_mu);
+    if (bytes < (1u << 16)) bytes = 1u << 16;
+    s.chunk = bytes & ~(size_t)255;
+}
+
+BufInfo classify(const void* p)
+{
+    BufInfo b;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();   // pageable host memory is not an error
+        return b;
+    }
+    switch (a.type) {
+    case hipMemoryTypeDevice:
+    case hipMemoryTypeManaged:
+    case hipMemoryTypeArray:
+        b.place = Place::Device;
+        b.dev = a.devicePointer ? a.devicePointer : const_cast<void*>(p);
+        b.device = a.device;
+        break;
+    case hipMemoryTypeHost:
+        // pinned host memory: device-visible but PCIe-bound; stage it like any
+        // other host buffer so the combine itself streams from HBM.
+        b.place = Place::Host;
+        b.dev = a.devicePointer;
+        b.device = a.device;
+        break;
+    default:
+        b.place = Place::Host;
+        break;
+    }
+    return b;
+}
+
+int reduce_local_device(int opidx, Kind k, const void* in, void* inout, size_t count,
+                        hipStream_t s)
+{
+    hipError_t e = launch_combine(opidx, k, in, inout, count, s, g_cfg);
+    if (e != hipSuccess) return hip_fail(e, "combine kernel launch");
+    return MPI_SUCCESS;
+}
+
+namespace {
+
+int ensure_staging(DevState& s)
+{
+    if (s.stage_cap >= s.chunk && s.stage_in[0]) return MPI_SUCCESS;
+    for (int i = 0; i < 2; ++i) {
+        if (s.stage_in[i]) (void)hipFree(s.stage_in[i]);
+        if (s.stage_io[i]) (void)hipFree(s.stage_io[i]);
+        s.stage_in[i] = s.stage_io[i] = nullptr;
+    }
+    s.stage_cap = 0;
+    for (int i = 0; i < 2; ++i) {
+        hipError_t e = hipMalloc(&s.stage_in[i], s.chunk);
+        if (e == hipSuccess) e = hipMalloc(&s.stage_io[i], s.chunk);
+        if (e != hipSuccess) return hip_fail(e, "staging hipMalloc");
+        if (!s.stage_s[i]) {
+            e = hipStreamCreateWithFlags(&s.stage_s[i], hipStreamNonBlocking);
+            if (e != hipSuccess) return hip_fail(e, "staging stream");
+        }
+    }
+    s.stage_cap = s.chunk;
+    return MPI_SUCCESS;
+}
+
+}  // namespace
+
+int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t count)
+{
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    const BufInfo bi = classify(in), bo = classify(inout);
+    DevState& s = ds();
+
+    if (bi.place == Place::Device && bo.place == Place::Device) {
+        rc = reduce_local_device(opidx, k, bi.dev, bo.dev, count, s.stream);
+        if (rc != MPI_SUCCESS) return rc;
+        hipError_t e = hipStreamSynchronize(s.stream);
+        return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "combine kernel");
+    }
+
+    // At least one operand in host memory: chunked, double-buffered staging.
+    std::lock_guard<std::mutex> g(s.stage_mu);
+    rc = ensure_staging(s);
+    if (rc != MPI_SUCCESS) return rc;
+    const size_t esz = (size_t)kind_size(k);
+    const size_t per = (s.chunk / esz) > 0 ? (s.chunk / esz) : 1;   // elements per chunk
+    size_t off = 0;
+    int slot = 0;
+    hipError_t e = hipSuccess;
+    while (off < count && e == hipSuccess) {
+        const size_t n = (count - off < per) ? count - off : per;
+        const size_t bytes = n * esz;
+        hipStream_t st = s.stage_s[slot];
+        const char* src_in = static_cast<const char*>(in) + off * esz;
+        char* src_io = static_cast<char*>(inout) + off * esz;
+        const void* din;
+        void* dio;
+        if (bi.place == Place::Device) {
+            din = static_cast<const char*>(bi.dev) + off * esz;
+        } else {
+            e = hipMemcpyAsync(s.stage_in[slot], src_in, bytes, hipMemcpyHostToDevice, st);
+            din = s.stage_in[slot];
+        }
+        if (bo.place == Place::Device) {
+            dio = static_cast<char*>(bo.dev) + off * esz;
+        } else {
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(s.stage_io[slot], src_io, bytes, hipMemcpyHostToDevice, st);
+            dio = s.stage_io[slot];
+        }
+        if (e == hipSuccess) e = launch_combine(opidx, k, din, dio, n, st, g_cfg);
+        if (e == hipSuccess && bo.place == Place::Host)
+            e = hipMemcpyAsync(src_io, dio, bytes, hipMemcpyDeviceToHost, st);
+        off += n;
+        slot ^= 1;
+        // Before re-using the other slot's staging buffers, its previous chunk
+        // must have drained.
+        if (e == hipSuccess && off < count) e = hipStreamSynchronize(s.stage_s[slot]);
+    }
+    for (int i = 0; i < 2; ++i) {
+        hipError_t e2 = hipStreamSynchronize(s.stage_s[i]);
+        if (e == hipSuccess) e = e2;
+    }
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "host-staged combine");
+}
+
+}  // namespace msx

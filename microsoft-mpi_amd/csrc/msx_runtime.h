@@ -1,0 +1,50 @@
+// msx_runtime.h — process state, device/stream management, buffer placement.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <string>
+
+#include "msx_kernels.h"
+#include "msx_types.h"
+
+namespace msx {
+
+// Where a user buffer lives, as seen from the current device.
+enum class Place { Device, Host };
+
+struct BufInfo {
+    Place place = Place::Host;
+    void* dev = nullptr;     // device-accessible alias (device/managed/pinned), or nullptr
+    int device = -1;
+};
+
+// thread-local error text (msx_last_error)
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+// Device bring-up.  Returns MPI_SUCCESS or MPI_ERR_OTHER (no usable GPU).
+int ensure_device();
+int current_device();
+hipStream_t internal_stream();
+int device_count_noinit();
+
+BufInfo classify(const void* p);
+
+LaunchCfg& launch_cfg();
+void set_staging_chunk(size_t bytes);
+
+// inout = inout (op) in over `count` elements on any combination of host and
+// device buffers; blocking (returns after the result is in `inout`).
+// Returns an MPI error class.
+int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t count);
+
+// Same, stream-ordered, both operands device-accessible.
+int reduce_local_device(int opidx, Kind k, const void* in, void* inout, size_t count,
+                        hipStream_t s);
+
+// hipError_t -> MPI error class with the HIP error text recorded.
+int hip_fail(hipError_t e, const char* what);
+
+}  // namespace msx

@@ -1,0 +1,86 @@
+// msx_transport.h — multi-rank bootstrap, peer mapping and the collective engine.
+//
+// One process per GPU on one node.  Ranks find each other through a small TCP
+// hub (rank 0 listens on MASTER_ADDR:MSX_BOOTSTRAP_PORT), exchange HIP IPC
+// handles of the buffers a collective touches, and then every rank reads its
+// peers' HBM directly (xGMI on 8 x MI355X; same-HBM when several ranks share
+// one GPU).  The combine runs as one schedule-faithful multi-input kernel, so
+// each element sees exactly the association and inout/in roles of the
+// reference's recursive-halving / recursive-doubling / pairwise schedules.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <functional>
+#include <future>
+#include <vector>
+
+#include "msx_comm.h"
+
+namespace msx {
+
+class Transport {
+public:
+    virtual ~Transport() = default;
+    int rank = 0;
+    int size = 1;
+    // lock-step host collectives over the bootstrap hub (all ranks, same n)
+    virtual int allgather(const void* mine, size_t n, void* all) = 0;
+    virtual int barrier() = 0;
+    // Device pointers through which THIS process reads rank r's `ptr`
+    // (ptr must be device memory of the calling rank).  Collective.
+    virtual int map_peers(const void* ptr, std::vector<char*>& out) = 0;
+    // Per-rank device scratch, IPC-mapped once: out[r] = rank r's window.
+    virtual int window(size_t bytes, std::vector<char*>& out) = 0;
+    virtual hipStream_t stream() = 0;
+};
+
+int transport_create(int rank, int size, Transport** out);
+void transport_destroy(Transport* t);
+
+// ---- schedules (pure functions; exported for host-side tests) ----------------
+// Reference algorithm selected for an allreduce (reduce.cpp:3884-3888) and for a
+// reduce_scatter (reduce.cpp:1705-1750).
+enum Algo { A_RECURSIVE_DOUBLING = 0, A_RABENSEIFNER = 1, A_RS_HALVING = 2, A_RS_PAIRWISE = 3 };
+
+struct Leaf { int a = -1, b = -1; };   // real ranks: value = a, or a op b when b >= 0
+
+int pof2_floor(int p);
+int newrank_of(int rank, int p);                  // -1 for folded (even, < 2*rem) ranks
+int real_of_newrank(int n, int p);
+Leaf leaf_of(int n, int p);                       // leaf value of newrank n
+int allreduce_algo(int p, size_t count, int type_size, bool builtin);
+int reduce_scatter_algo(int p, size_t total_count, int type_size, bool commutative);
+// allreduce Rabenseifner blocks: block j = [start, start+len), computed at newrank owner
+void allreduce_block(int p, size_t count, int j, size_t* start, size_t* len);
+int allreduce_block_owner(int p, int j);           // newrank that owns block j
+int allreduce_block_of_newrank(int p, int n);
+// Tree spec (in real ranks) for the value newrank n computes:
+//   allreduce:      leaves y_k = leaf(n ^ k)
+//   reduce_scatter: leaves y_k = leaf(n ^ bitrev(k))   (recursive halving)
+//   pairwise:       chain x_r, x_{r-1}, ..., x_{r-p+1}
+struct RankTree {
+    int P = 1;
+    unsigned pairmask = 0;
+    bool chain = false;
+    int src[32];            // real ranks in kernel slot order
+};
+RankTree tree_allreduce(int p, int n);
+RankTree tree_reduce_scatter(int p, int n);
+RankTree tree_pairwise(int p, int r);
+
+// ---- engine entry points (msx_comm.cpp routes size > 1 here) ---------------
+int engine_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                     const OpRef& op);
+int engine_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                  const OpRef& op, int root);
+int engine_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
+                          MPI_Datatype dt, const OpRef& op);
+int engine_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                const OpRef& op, bool exclusive);
+// Run `fn` on the collective worker thread, after every collective issued
+// before it (MPI issue order); re-entrant calls from the worker run inline.
+std::shared_future<int> engine_async(std::function<int()> fn);
+
+}  // namespace msx

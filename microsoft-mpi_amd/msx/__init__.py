@@ -1,0 +1,162 @@
+"""msx — Python binding of libmsmpi_mi355x.so (the MI355X MS-MPI reduction path).
+
+Thin ctypes layer over the C ABI declared in include/mpi.h and include/msx.h,
+used by the tests, bench.py and __graft_entry__.py.  The library is the
+product; nothing here computes a reduction.  If the shared library is missing
+the import of `lib()` raises: there is no Python or CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from types import SimpleNamespace
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)                      # microsoft-mpi_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmsmpi_mi355x.so")
+INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
+
+_lib = None
+
+
+def _parse_header_constants(path):
+    """#define NAME value / ((T)0x...) from include/mpi.h -> dict (ints only)."""
+    out = {}
+    pat = re.compile(r"^#define\s+(MPI_\w+)\s+(.+?)\s*(?:/\*.*)?$")
+    with open(path) as f:
+        for line in f:
+            m = pat.match(line.strip())
+            if not m:
+                continue
+            name, val = m.group(1), m.group(2).strip()
+            val = re.sub(r"\(\((?:MPI_\w+|void\*|MPI_Status\*)\)(?:\(MPI_Aint\))?(.+?)\)$", r"\1", val)
+            val = val.strip("() ")
+            try:
+                out[name] = int(val, 0)
+            except ValueError:
+                if val in out:
+                    out[name] = out[val]
+    return out
+
+
+C = SimpleNamespace(**_parse_header_constants(os.path.join(INCLUDE_DIR, "mpi.h")))
+
+
+def _signed32(v):
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+# all handle values as C ints (MPI_Datatype / MPI_Op are `int`)
+for _k, _v in list(vars(C).items()):
+    setattr(C, _k, _signed32(_v))
+
+
+def lib():
+    """Load the HIP library (raises OSError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} missing: run `make -C microsoft-mpi_amd` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    i, p, i64 = ctypes.c_int, ctypes.c_void_p, ctypes.c_int64
+    sig = {
+        "MPI_Init": (i, [p, p]),
+        "MPI_Finalize": (i, []),
+        "MPI_Initialized": (i, [ctypes.POINTER(i)]),
+        "MPI_Finalized": (i, [ctypes.POINTER(i)]),
+        "MPI_Comm_rank": (i, [i, ctypes.POINTER(i)]),
+        "MPI_Comm_size": (i, [i, ctypes.POINTER(i)]),
+        "MPI_Barrier": (i, [i]),
+        "MPI_Comm_set_errhandler": (i, [i, i]),
+        "MPI_Error_class": (i, [i, ctypes.POINTER(i)]),
+        "MPI_Type_size": (i, [i, ctypes.POINTER(i)]),
+        "MPI_Op_create": (i, [p, i, ctypes.POINTER(i)]),
+        "MPI_Op_free": (i, [ctypes.POINTER(i)]),
+        "MPI_Op_commutative": (i, [i, ctypes.POINTER(i)]),
+        "MPI_Reduce_local": (i, [p, p, i, i, i]),
+        "MPI_Reduce": (i, [p, p, i, i, i, i, i]),
+        "MPI_Allreduce": (i, [p, p, i, i, i, i]),
+        "MPI_Reduce_scatter": (i, [p, p, p, i, i, i]),
+        "MPI_Reduce_scatter_block": (i, [p, p, i, i, i, i]),
+        "MPI_Iallreduce": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Ireduce": (i, [p, p, i, i, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Ireduce_scatter_block": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Wait": (i, [ctypes.POINTER(i), p]),
+        "MPI_Test": (i, [ctypes.POINTER(i), ctypes.POINTER(i), p]),
+        "MPI_Wtime": (ctypes.c_double, []),
+        "msx_version": (ctypes.c_char_p, []),
+        "msx_device_count": (i, []),
+        "msx_last_error": (ctypes.c_char_p, []),
+        "msx_op_check": (i, [i, i]),
+        "msx_type_size": (i, [i]),
+        "msx_reduce_local_dev": (i, [p, p, i64, i, i, p]),
+        "msx_reduce_tree_dev": (i, [ctypes.POINTER(p), i, p, i64, i, i, p]),
+        "msx_tune_set": (i, [i, i]),
+        "msx_tune_variant_count": (i, []),
+        "msx_tune_variant_name": (ctypes.c_char_p, [i]),
+        "msx_set_staging_chunk": (i, [i64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names the C headers declare (MPI_*/PMPI_*/msx_* prototypes)."""
+    names = set()
+    for h in ("mpi.h", "msx.h"):
+        with open(os.path.join(INCLUDE_DIR, h)) as f:
+            txt = f.read()
+        names.update(re.findall(
+            r"(?:MPI_METHOD|double MPIAPI|const char\*|int)\s+((?:P?MPI|msx)_\w+)\s*\(", txt))
+    return sorted(names)
+
+
+def ptr(x):
+    """Raw address of a torch tensor, numpy array, int or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    raise TypeError(type(x))
+
+
+def last_error():
+    return lib().msx_last_error().decode()
+
+
+def init(errors_return=True):
+    """MPI_Init once; by default switch COMM_WORLD to MPI_ERRORS_RETURN."""
+    L = lib()
+    flag = ctypes.c_int(0)
+    L.MPI_Initialized(ctypes.byref(flag))
+    if not flag.value:
+        rc = L.MPI_Init(None, None)
+        if rc:
+            raise RuntimeError(f"MPI_Init failed: {rc} {last_error()}")
+    if errors_return:
+        L.MPI_Comm_set_errhandler(C.MPI_COMM_WORLD, C.MPI_ERRORS_RETURN)
+    return L
+
+
+# element kinds per datatype, as the reference's CASE_MPI_* macros map them
+# (mpid/op.cpp:343-536, LLP64); numpy dtype strings for test data.
+LOC_DTYPES = {
+    "ii": [("v", "<i4"), ("l", "<i4")],
+    "fi": [("v", "<f4"), ("l", "<i4")],
+    "si": {"names": ["v", "l"], "formats": ["<i2", "<i4"], "offsets": [0, 4], "itemsize": 8},
+    "di": {"names": ["v", "l"], "formats": ["<f8", "<i4"], "offsets": [0, 8], "itemsize": 16},
+    "ff": [("v", "<f4"), ("l", "<f4")],
+    "dd": [("v", "<f8"), ("l", "<f8")],
+}

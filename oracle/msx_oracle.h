@@ -1,0 +1,67 @@
+/*
+ * msx_oracle.h — CPU restatement of MS-MPI's MPI_Op kernels (TEST INFRASTRUCTURE).
+ *
+ * ORACLE — test infrastructure only.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library.  The product path
+ * (libmsmpi_mi355x.so) never links or calls it.
+ *
+ * Parity pinning: the reference library cannot be built here (op.cpp pulls
+ * precomp.h -> mpiimpl.h -> windows.h/winsock2.h/SAL/ETW, which this image
+ * lacks and which must not be replaced by stand-ins), so oracle/_ref does not
+ * exist.  The restatement is pinned by the known-answer outputs recorded from
+ * the reference's compiled kernels in SURVEY.md §8(a) notes / Appendix A,
+ * committed as tests/golden/survey_kat.json.
+ */
+#ifndef MSX_ORACLE_H
+#define MSX_ORACLE_H
+
+#include <stdint.h>
+#include "../include/mpi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Element classes the reference's CASE_MPI_* macros map datatypes to
+ * (op.cpp:343-536; LLP64 widths per mpi.h:284-368). */
+enum oracle_kind {
+    ORK_NONE = 0,
+    ORK_I8, ORK_U8, ORK_I16, ORK_U16, ORK_I32, ORK_U32, ORK_I64, ORK_U64,
+    ORK_F32, ORK_F64, ORK_BOOL, ORK_C32, ORK_C64,
+    ORK_LOC_II, ORK_LOC_FI, ORK_LOC_SI, ORK_LOC_DI, ORK_LOC_FF, ORK_LOC_DD,
+    ORK_COUNT
+};
+
+/* datatype handle -> element class (ORK_NONE if not reducible) */
+int oracle_kind_of(MPI_Datatype dt);
+/* bytes per element of a kind (sizeof the C struct, padding included) */
+int oracle_kind_size(int kind);
+/* MPIR_Op_<op>_check_dtype (op.cpp:739-1883): MPI_SUCCESS or MPI_ERR_OP */
+int oracle_op_check(MPI_Op op, MPI_Datatype dt);
+/* MPIR_Op_<op>(in, inout, &len, &dt) (op.cpp:703-1795) with a 64-bit count.
+ * Returns the value the reference leaves in op_errno: MPI_SUCCESS, or
+ * MPI_ERR_OP for an unsupported (op, type) pair (inout untouched). */
+int oracle_reduce_local(MPI_Op op, MPI_Datatype dt, const void* in, void* inout,
+                        int64_t count);
+
+/* CPU baseline helper: sharded over nthreads pthreads (1 = one MS-MPI rank). */
+int oracle_reduce_local_mt(MPI_Op op, MPI_Datatype dt, const void* in, void* inout,
+                           int64_t count, int nthreads);
+
+/* Reference-order multi-rank schedules (restated from mpid/reduce.cpp), used as
+ * the expected result of the collectives for p ranks.  sendbufs[r] is rank r's
+ * contribution (count elements each); results are written per rank.
+ * Returns MPI_SUCCESS / MPI_ERR_OP / MPI_ERR_ARG. */
+int oracle_allreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
+                     const void* const* sendbufs, void* const* recvbufs);
+int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcounts,
+                          const void* const* sendbufs, void* const* recvbufs);
+int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
+                  const void* const* sendbufs, void* recvbuf_root);
+int oracle_scan(MPI_Op op, MPI_Datatype dt, int p, int64_t count, int exclusive,
+                const void* const* sendbufs, void* const* recvbufs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

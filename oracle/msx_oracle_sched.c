@@ -1,0 +1,286 @@
+/*
+ * msx_oracle_sched.c — step-by-step simulation of MS-MPI's reduction schedules.
+ *
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  p ranks are simulated in lock step in one
+ * process: every MPIC_Sendrecv of a step is a memcpy of the sender's region as
+ * it stood at the start of the step, and every MPID_Uop_call is
+ * oracle_reduce_local(op, dt, in=<received>, inout=<local>), with exactly the
+ * buffers and index arithmetic of the reference:
+ *   MPIR_Allreduce_intra_flat               reduce.cpp:3768-4104
+ *   MPIR_Reduce_scatter_intra_impl          reduce.cpp:1636-1770 (32-bit nbytes gate)
+ *   MPIR_Reduce_scatter_commutative_short   reduce.cpp:917-1219
+ *   MPIR_Reduce_scatter_commutative_long    reduce.cpp:1225-1334
+ * (the HA / node-aware variants, reduce.cpp:4180-4292, are not simulated: the
+ * flat algorithm is the reference order, as with MSMPI_HA_COLLECTIVE=OFF, and
+ * the one the reference takes for every message >= 256 KiB.)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "msx_oracle.h"
+
+static int pof2_floor(int p)
+{
+    int v = 1;
+    while (v * 2 <= p) v *= 2;
+    return v;
+}
+
+typedef struct { char* buf; } rbuf;
+
+static int combine(MPI_Op op, MPI_Datatype dt, const void* in, void* inout, int64_t n)
+{
+    return n > 0 ? oracle_reduce_local(op, dt, in, inout, n) : 0;
+}
+
+int oracle_allreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
+                     const void* const* sendbufs, void* const* recvbufs)
+{
+    if (oracle_op_check(op, dt) != MPI_SUCCESS) return MPI_ERR_OP;
+    if (p < 1) return MPI_ERR_ARG;
+    if (count == 0) return MPI_SUCCESS;
+    const int64_t esz = oracle_kind_size(oracle_kind_of(dt));
+    const int64_t bytes = count * esz;
+    char** rb = (char**)recvbufs;
+    char** tmp = (char**)calloc((size_t)p, sizeof(char*));
+    char** snap = (char**)calloc((size_t)p, sizeof(char*));
+    int* newrank = (int*)calloc((size_t)p, sizeof(int));
+    int rc = MPI_SUCCESS;
+    for (int r = 0; r < p; ++r) {
+        if (sendbufs[r] != MPI_IN_PLACE) memcpy(rb[r], sendbufs[r], (size_t)bytes);  /* :3814-3819 */
+        tmp[r] = (char*)malloc((size_t)bytes);
+        snap[r] = (char*)malloc((size_t)bytes);
+    }
+    const int pof2 = pof2_floor(p), rem = p - pof2;
+
+    /* fold (:3835-3871): even r < 2*rem sends to r+1, which combines tmp -> recvbuf */
+    for (int r = 0; r < p; ++r) {
+        if (r < 2 * rem) {
+            if ((r & 1) == 0) {
+                newrank[r] = -1;
+            } else {
+                memcpy(tmp[r], rb[r - 1], (size_t)bytes);
+                rc |= combine(op, dt, tmp[r], rb[r], count);
+                newrank[r] = r / 2;
+            }
+        } else {
+            newrank[r] = r - rem;
+        }
+    }
+    int* real = (int*)calloc((size_t)pof2, sizeof(int));
+    for (int r = 0; r < p; ++r) if (newrank[r] >= 0) real[newrank[r]] = r;
+
+    const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)esz);   /* :3884 */
+    if (nbytes <= 262144u || count < pof2) {
+        /* recursive doubling (:3890-3926): commutative builtin -> Uop(tmp, recvbuf) */
+        for (int mask = 1; mask < pof2; mask <<= 1) {
+            for (int n = 0; n < pof2; ++n) memcpy(snap[real[n]], rb[real[n]], (size_t)bytes);
+            for (int n = 0; n < pof2; ++n) {
+                const int r = real[n], dst = real[n ^ mask];
+                memcpy(tmp[r], snap[dst], (size_t)bytes);
+                rc |= combine(op, dt, tmp[r], rb[r], count);
+            }
+        }
+    } else {
+        /* reduce-scatter + allgather (:3927-4066) */
+        const int64_t reduceSize = count / pof2, endSize = count % pof2;
+        int *send_idx = calloc((size_t)pof2, sizeof(int)), *recv_idx = calloc((size_t)pof2, sizeof(int));
+        int *last_idx = calloc((size_t)pof2, sizeof(int)), *idx_shift = calloc((size_t)pof2, sizeof(int));
+        int64_t *scnt = calloc((size_t)pof2, sizeof(int64_t)), *rcnt = calloc((size_t)pof2, sizeof(int64_t));
+        for (int n = 0; n < pof2; ++n) { last_idx[n] = pof2; idx_shift[n] = pof2 >> 1; }
+        int mask = 1;
+        while (mask < pof2) {
+            for (int n = 0; n < pof2; ++n) {
+                const int nd = n ^ mask;
+                if (n < nd) {
+                    send_idx[n] = recv_idx[n] + idx_shift[n];
+                    rcnt[n] = (int64_t)(send_idx[n] - recv_idx[n]) * reduceSize;
+                    scnt[n] = (int64_t)(last_idx[n] - send_idx[n]) * reduceSize;
+                    if (last_idx[n] == pof2) scnt[n] += endSize;
+                } else {
+                    recv_idx[n] = send_idx[n] + idx_shift[n];
+                    scnt[n] = (int64_t)(recv_idx[n] - send_idx[n]) * reduceSize;
+                    rcnt[n] = (int64_t)(last_idx[n] - recv_idx[n]) * reduceSize;
+                    if (last_idx[n] == pof2) rcnt[n] += endSize;
+                }
+            }
+            for (int n = 0; n < pof2; ++n) memcpy(snap[real[n]], rb[real[n]], (size_t)bytes);
+            for (int n = 0; n < pof2; ++n) {
+                const int r = real[n], d = n ^ mask;
+                const int64_t off = reduceSize * recv_idx[n] * esz;
+                /* what d sends: its send region, which is our recv region */
+                memcpy(tmp[r] + off, snap[real[d]] + reduceSize * send_idx[d] * esz, (size_t)(rcnt[n] * esz));
+                rc |= combine(op, dt, tmp[r] + off, rb[r] + off, rcnt[n]);
+            }
+            for (int n = 0; n < pof2; ++n) {
+                send_idx[n] = recv_idx[n];
+                if ((mask << 1) < pof2) {
+                    last_idx[n] = recv_idx[n] + idx_shift[n];
+                    idx_shift[n] >>= 1;
+                }
+            }
+            mask <<= 1;
+        }
+        mask >>= 1;
+        while (mask > 0) {
+            for (int n = 0; n < pof2; ++n) {
+                const int nd = n ^ mask;
+                if (n < nd) {
+                    if (mask != pof2 >> 1) last_idx[n] = last_idx[n] + idx_shift[n];
+                    recv_idx[n] = send_idx[n] + idx_shift[n];
+                    scnt[n] = (int64_t)(recv_idx[n] - send_idx[n]) * reduceSize;
+                    rcnt[n] = (int64_t)(last_idx[n] - recv_idx[n]) * reduceSize;
+                    if (last_idx[n] == pof2) rcnt[n] += endSize;
+                } else {
+                    recv_idx[n] = send_idx[n] - idx_shift[n];
+                    rcnt[n] = (int64_t)(send_idx[n] - recv_idx[n]) * reduceSize;
+                    scnt[n] = (int64_t)(last_idx[n] - send_idx[n]) * reduceSize;
+                    if (last_idx[n] == pof2) scnt[n] += endSize;
+                }
+            }
+            for (int n = 0; n < pof2; ++n) memcpy(snap[real[n]], rb[real[n]], (size_t)bytes);
+            for (int n = 0; n < pof2; ++n) {
+                const int r = real[n], d = n ^ mask;
+                memcpy(rb[r] + reduceSize * recv_idx[n] * esz,
+                       snap[real[d]] + reduceSize * send_idx[d] * esz, (size_t)(rcnt[n] * esz));
+            }
+            for (int n = 0; n < pof2; ++n) {
+                if (n > (n ^ mask)) send_idx[n] = recv_idx[n];
+                idx_shift[n] <<= 1;
+            }
+            mask >>= 1;
+        }
+        free(send_idx); free(recv_idx); free(last_idx); free(idx_shift); free(scnt); free(rcnt);
+    }
+    /* unfold (:4071-4092) */
+    for (int r = 0; r < 2 * rem; r += 2) memcpy(rb[r], rb[r + 1], (size_t)bytes);
+
+    for (int r = 0; r < p; ++r) { free(tmp[r]); free(snap[r]); }
+    free(tmp); free(snap); free(newrank); free(real);
+    return rc ? MPI_ERR_OP : MPI_SUCCESS;
+}
+
+int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcounts,
+                          const void* const* sendbufs, void* const* recvbufs)
+{
+    if (oracle_op_check(op, dt) != MPI_SUCCESS) return MPI_ERR_OP;
+    const int64_t esz = oracle_kind_size(oracle_kind_of(dt));
+    int64_t* disps = (int64_t*)calloc((size_t)p + 1, sizeof(int64_t));
+    for (int i = 0; i < p; ++i) disps[i + 1] = disps[i] + recvcounts[i];
+    const int64_t total = disps[p];
+    int rc = MPI_SUCCESS;
+    if (total == 0) { free(disps); return MPI_SUCCESS; }
+    const int64_t bytes = total * esz;
+    const uint32_t nbytes = (uint32_t)((uint64_t)total * (uint64_t)esz);   /* :1705 */
+    char** res = (char**)calloc((size_t)p, sizeof(char*));
+    char** tmp = (char**)calloc((size_t)p, sizeof(char*));
+    char** snap = (char**)calloc((size_t)p, sizeof(char*));
+    for (int r = 0; r < p; ++r) {
+        res[r] = (char*)malloc((size_t)bytes);
+        tmp[r] = (char*)malloc((size_t)bytes);
+        snap[r] = (char*)malloc((size_t)bytes);
+        const void* src = sendbufs[r] != MPI_IN_PLACE ? sendbufs[r] : recvbufs[r];
+        memcpy(res[r], src, (size_t)bytes);
+    }
+    if (nbytes < 524288u) {
+        /* recursive halving (:917-1219) */
+        const int pof2 = pof2_floor(p), rem = p - pof2;
+        int* newrank = (int*)calloc((size_t)p, sizeof(int));
+        int* real = (int*)calloc((size_t)pof2, sizeof(int));
+        for (int r = 0; r < p; ++r) {
+            if (r < 2 * rem) {
+                if ((r & 1) == 0) newrank[r] = -1;
+                else {
+                    memcpy(tmp[r], res[r - 1], (size_t)bytes);
+                    rc |= combine(op, dt, tmp[r], res[r], total);
+                    newrank[r] = r / 2;
+                }
+            } else newrank[r] = r - rem;
+            if (newrank[r] >= 0) real[newrank[r]] = r;
+        }
+        int64_t* newcnts = (int64_t*)calloc((size_t)pof2, sizeof(int64_t));
+        int64_t* newdisps = (int64_t*)calloc((size_t)pof2 + 1, sizeof(int64_t));
+        {
+            int i = 0, old_i = 0;
+            for (i = 0; i < rem; i++) {
+                newcnts[i] = recvcounts[old_i] + recvcounts[old_i + 1];
+                old_i += 2;
+                newdisps[i + 1] = newdisps[i] + newcnts[i];
+            }
+            for (; old_i < p; ++old_i, ++i) {
+                newcnts[i] = recvcounts[old_i];
+                newdisps[i + 1] = newdisps[i] + newcnts[i];
+            }
+        }
+        int *send_idx = calloc((size_t)pof2, sizeof(int)), *recv_idx = calloc((size_t)pof2, sizeof(int));
+        int *last_idx = calloc((size_t)pof2, sizeof(int));
+        int64_t* rcnt = calloc((size_t)pof2, sizeof(int64_t));
+        for (int n = 0; n < pof2; ++n) last_idx[n] = pof2;
+        for (int mask = pof2 >> 1; mask > 0; mask >>= 1) {
+            for (int n = 0; n < pof2; ++n) {
+                const int nd = n ^ mask;
+                rcnt[n] = 0;
+                if (n < nd) {
+                    send_idx[n] = recv_idx[n] + mask;
+                    for (int i = recv_idx[n]; i < send_idx[n]; i++) rcnt[n] += newcnts[i];
+                } else {
+                    recv_idx[n] = send_idx[n] + mask;
+                    for (int i = recv_idx[n]; i < last_idx[n]; i++) rcnt[n] += newcnts[i];
+                }
+            }
+            for (int n = 0; n < pof2; ++n) memcpy(snap[real[n]], res[real[n]], (size_t)bytes);
+            for (int n = 0; n < pof2; ++n) {
+                const int r = real[n], d = n ^ mask;
+                if (rcnt[n]) {
+                    const int64_t off = newdisps[recv_idx[n]] * esz;
+                    memcpy(tmp[r] + off, snap[real[d]] + newdisps[send_idx[d]] * esz, (size_t)(rcnt[n] * esz));
+                    rc |= combine(op, dt, tmp[r] + off, res[r] + off, rcnt[n]);
+                }
+            }
+            for (int n = 0; n < pof2; ++n) {
+                send_idx[n] = recv_idx[n];
+                last_idx[n] = recv_idx[n] + mask;
+            }
+        }
+        for (int r = 0; r < p; ++r) {
+            if (newrank[r] >= 0 && recvcounts[r])
+                memcpy(recvbufs[r], res[r] + disps[r] * esz, (size_t)recvcounts[r] * esz);
+        }
+        for (int r = 0; r < 2 * rem; r += 2)   /* odd sends the even rank's block */
+            if (recvcounts[r]) memcpy(recvbufs[r], res[r + 1] + disps[r] * esz, (size_t)recvcounts[r] * esz);
+        free(newrank); free(real); free(newcnts); free(newdisps);
+        free(send_idx); free(recv_idx); free(last_idx); free(rcnt);
+    } else {
+        /* pairwise exchange (:1225-1334): recvbuf = own block, then p-1 combines */
+        for (int r = 0; r < p; ++r) {
+            const int64_t n = recvcounts[r];
+            char* acc = (char*)malloc((size_t)(n * esz) + 1);
+            memcpy(acc, res[r] + disps[r] * esz, (size_t)(n * esz));
+            int src = r;
+            for (int i = p - 1; i > 0; i--) {
+                if (--src < 0) src += p;
+                rc |= combine(op, dt, res[src] + disps[r] * esz, acc, n);
+            }
+            if (n) memcpy(recvbufs[r], acc, (size_t)(n * esz));
+            free(acc);
+        }
+    }
+    for (int r = 0; r < p; ++r) { free(res[r]); free(tmp[r]); free(snap[r]); }
+    free(res); free(tmp); free(snap); free(disps);
+    return rc ? MPI_ERR_OP : MPI_SUCCESS;
+}
+
+int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
+                  const void* const* sendbufs, void* recvbuf_root)
+{
+    (void)op; (void)dt; (void)p; (void)root; (void)count; (void)sendbufs; (void)recvbuf_root;
+    return MPI_ERR_INTERN;   /* rooted schedules: see DESIGN.md §Next */
+}
+
+int oracle_scan(MPI_Op op, MPI_Datatype dt, int p, int64_t count, int exclusive,
+                const void* const* sendbufs, void* const* recvbufs)
+{
+    (void)op; (void)dt; (void)p; (void)count; (void)exclusive; (void)sendbufs; (void)recvbufs;
+    return MPI_ERR_INTERN;
+}

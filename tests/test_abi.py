@@ -1,0 +1,154 @@
+"""CPU: the C-ABI library loads, exports every symbol the headers declare, keeps
+MS-MPI's handle values, and reproduces MPI_Reduce_local's argument checks in
+the reference's order (api/mpi_reduce.cpp:304-385, api/mpi_api.h:113-212,
+707-775).  No compute call here needs a GPU."""
+import ctypes
+import os
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+import msx
+import oracle
+from _cases import KIND, NON_REDUCIBLE, OPS, h
+
+C = msx.C
+
+
+def test_library_exports_every_declared_symbol():
+    L = msx.lib()
+    missing = [s for s in msx.exported_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+    assert len(msx.exported_symbols()) >= 50
+
+
+def test_handle_values_match_msmpi_abi():
+    # src/include/mpi.h:192-250, 281-368, 410-426, 441-463, 1956
+    assert (C.MPI_SUCCESS, C.MPI_ERR_BUFFER, C.MPI_ERR_COUNT, C.MPI_ERR_TYPE, C.MPI_ERR_OP,
+            C.MPI_ERR_ARG, C.MPI_ERR_OTHER) == (0, 1, 2, 3, 9, 12, 15)
+    u = lambda v: v & 0xFFFFFFFF
+    assert u(C.MPI_SUM) == 0x58000003 and u(C.MPI_MAXLOC) == 0x5800000C and u(C.MPI_OP_NULL) == 0x18000000
+    assert u(C.MPI_FLOAT) == 0x4C00040A and u(C.MPI_LONG) == 0x4C000407 and u(C.MPI_UINT64_T) == 0x4C00083A
+    assert u(C.MPI_LONG_DOUBLE) == 0x4C00080C and u(C.MPI_AINT) == 0x4C00083B
+    assert u(C.MPI_FLOAT_INT) == 0x8C000000 and u(C.MPI_LONG_DOUBLE_INT) == 0x8C000004
+    assert u(C.MPI_COMM_WORLD) == 0x44000000 and u(C.MPI_ERRORS_RETURN) == 0x54000001
+    assert C.MPI_IN_PLACE == -1 and C.MPI_REAL2 == C.MPI_DATATYPE_NULL
+    # element size lives in byte 1 of the handle (include/datatype.h:36)
+    L = msx.lib()
+    for name, kind in KIND.items():
+        hv = u(h(name))
+        if hv >> 24 == 0x4C:
+            assert L.msx_type_size(h(name)) == (hv >> 8) & 0xFF, name
+
+
+def test_type_sizes_llp64():
+    L = msx.lib()
+    assert L.msx_type_size(C.MPI_LONG) == 4 and L.msx_type_size(C.MPI_UNSIGNED_LONG) == 4
+    assert L.msx_type_size(C.MPI_LONG_DOUBLE) == 8
+    assert L.msx_type_size(C.MPI_SHORT_INT) == 8 and L.msx_type_size(C.MPI_DOUBLE_INT) == 16
+
+
+def test_op_check_matches_oracle_everywhere():
+    L = msx.lib()
+    for op in OPS:
+        for dt in list(KIND) + NON_REDUCIBLE + ["MPI_DATATYPE_NULL"]:
+            assert L.msx_op_check(h(op), h(dt)) == oracle.op_check(h(op), h(dt)), (op, dt)
+    for bad in (C.MPI_REPLACE, C.MPI_NO_OP, C.MPI_OP_NULL, 0x12345678, C.MPI_FLOAT):
+        assert L.msx_op_check(bad, C.MPI_INT) == C.MPI_ERR_OP
+
+
+def test_reduce_local_validation_order(msxlib):
+    L = msxlib
+    a = np.arange(8, dtype=np.int32)
+    b = np.ones(8, dtype=np.int32)
+    pa, pb = a.ctypes.data, b.ctypes.data
+    IN_PLACE = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value
+    # count == 0 returns success before any check (:319-322), even with bad op/type
+    assert L.MPI_Reduce_local(None, None, 0, 0x1234, 0x42) == 0
+    # op checked first (:324)
+    assert L.MPI_Reduce_local(None, None, 5, C.MPI_INT, C.MPI_OP_NULL) == C.MPI_ERR_OP
+    assert L.MPI_Reduce_local(pa, pb, 5, C.MPI_BYTE, C.MPI_SUM) == C.MPI_ERR_OP
+    assert L.MPI_Reduce_local(pa, pb, -1, C.MPI_BYTE, C.MPI_SUM) == C.MPI_ERR_OP
+    assert L.MPI_Reduce_local(pa, pb, 5, C.MPI_INT, C.MPI_REPLACE) == C.MPI_ERR_OP
+    assert L.MPI_Reduce_local(pa, pb, 5, C.MPI_INT, C.MPI_NO_OP) == C.MPI_ERR_OP
+    assert L.MPI_Reduce_local(pa, pb, 5, C.MPI_DATATYPE_NULL, C.MPI_SUM) == C.MPI_ERR_OP
+    # then IN_PLACE on either side (:331-341)
+    assert L.MPI_Reduce_local(IN_PLACE, pb, 5, C.MPI_INT, C.MPI_SUM) == C.MPI_ERR_BUFFER
+    assert L.MPI_Reduce_local(pa, IN_PLACE, 5, C.MPI_INT, C.MPI_SUM) == C.MPI_ERR_BUFFER
+    # then count / null buffer (:343, mpi_api.h:113-169)
+    assert L.MPI_Reduce_local(pa, pb, -3, C.MPI_INT, C.MPI_SUM) == C.MPI_ERR_COUNT
+    assert L.MPI_Reduce_local(None, pb, 5, C.MPI_INT, C.MPI_SUM) == C.MPI_ERR_BUFFER
+    # then aliasing (:349-358)
+    assert L.MPI_Reduce_local(pb, pb, 5, C.MPI_INT, C.MPI_SUM) == C.MPI_ERR_BUFFER
+    assert (b == 1).all()
+
+
+def test_user_ops_and_commutativity(msxlib):
+    L = msxlib
+    c = ctypes.c_int(-1)
+    for op in OPS:
+        assert L.MPI_Op_commutative(h(op), ctypes.byref(c)) == 0 and c.value == 1
+    assert L.MPI_Op_commutative(C.MPI_REPLACE, ctypes.byref(c)) == 0 and c.value == 0
+    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+
+    def sub(invec, inoutvec, n, dt):      # inout = in - inout (non-commutative)
+        x = np.ctypeslib.as_array((ctypes.c_int * n[0]).from_address(invec))
+        y = np.ctypeslib.as_array((ctypes.c_int * n[0]).from_address(inoutvec))
+        y[:] = x - y
+
+    fn = UF(sub)
+    op = ctypes.c_int(0)
+    assert L.MPI_Op_create(fn, 0, ctypes.byref(op)) == 0
+    assert L.MPI_Op_commutative(op.value, ctypes.byref(c)) == 0 and c.value == 0
+    a = np.arange(6, dtype=np.int32)
+    b = np.full(6, 10, dtype=np.int32)
+    # user functions are host code: host buffers call it directly, no GPU needed
+    assert L.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, 6, C.MPI_INT, op.value) == 0
+    assert b.tolist() == [-10, -9, -8, -7, -6, -5]
+    # freeing a builtin is an error ("**permop", mpi_op.cpp:169-173)
+    perm = ctypes.c_int(C.MPI_SUM)
+    assert L.MPI_Op_free(ctypes.byref(perm)) == C.MPI_ERR_OP
+    assert L.MPI_Op_free(ctypes.byref(op)) == 0 and op.value == C.MPI_OP_NULL
+    assert L.MPI_Op_free(ctypes.byref(op)) == C.MPI_ERR_OP
+
+
+def test_no_gpu_fails_loudly_not_silently(msxlib):
+    if msxlib.msx_device_count() > 0:
+        pytest.skip("GPU present")
+    a = np.arange(8, dtype=np.float32)
+    b = np.ones(8, dtype=np.float32)
+    rc = msxlib.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, 8, C.MPI_FLOAT, C.MPI_SUM)
+    assert rc == C.MPI_ERR_OTHER and "no usable MI355X" in msx.last_error()
+    assert (b == 1).all()    # nothing computed on the CPU
+    assert msxlib.msx_reduce_local_dev(a.ctypes.data, b.ctypes.data, 8, C.MPI_FLOAT, C.MPI_SUM,
+                                       None) == C.MPI_ERR_OTHER
+
+
+def _run_py(code, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    pre = f"import sys; sys.path.insert(0, {os.path.join(msx.REPO_ROOT, 'microsoft-mpi_amd')!r})\n"
+    return subprocess.run([sys.executable, "-c", pre + textwrap.dedent(code)], capture_output=True,
+                          text=True, env=e, timeout=120)
+
+
+def test_errors_are_fatal_by_default_and_require_init():
+    r = _run_py("""
+        import msx
+        L = msx.lib()
+        L.MPI_Init(None, None)
+        L.MPI_Reduce_local(None, None, 4, msx.C.MPI_BYTE, msx.C.MPI_SUM)
+        print("not reached")
+    """)
+    assert r.returncode == C.MPI_ERR_OP and "not reached" not in r.stdout
+    assert "Fatal error in MPI_Reduce_local" in r.stderr
+    r = _run_py("""
+        import msx
+        msx.lib().MPI_Reduce_local(None, None, 4, msx.C.MPI_INT, msx.C.MPI_SUM)
+        print("not reached")
+    """)
+    assert r.returncode != 0 and "before initializing" in r.stderr

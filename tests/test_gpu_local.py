@@ -1,0 +1,266 @@
+"""GPU parity: the HIP combine kernels vs the oracle, through the C ABI.
+
+Every legal (op, datatype) pair of the reference (op.cpp:739-1883) runs on the
+MI355X on seeded inputs with edge values (wrap, NaN, +-0, inf, denormals,
+ties, zeros) and must match the oracle BIT-EXACTLY: each element is one IEEE
+operation or one integer/logical/bitwise operation, exactly as in op.cpp, so
+no tolerance applies (not even for floating point).  Also covered: ragged
+sizes, unaligned and mutually misaligned pointers, host (pageable / pinned)
+buffers through MPI_Reduce_local's staged path, the reference's known-answer
+vectors, and a size-independent check at the benchmark size (256 MiB fp32).
+"""
+import ctypes
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import msx
+import oracle
+from _cases import KIND, OPS, gen, h, itemsize, legal_pairs, np_dtype
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+C = msx.C
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lib = msx.init(errors_return=True)
+    assert lib.msx_device_count() > 0
+    return lib
+
+
+def _dev(a, offset=0):
+    """Copy numpy array bytes into a fresh device buffer at byte `offset`."""
+    raw = np.frombuffer(a.tobytes(), np.uint8)
+    t = torch.zeros(raw.size + offset + 64, dtype=torch.uint8, device="cuda")
+    if raw.size:
+        t[offset:offset + raw.size] = torch.from_numpy(raw.copy()).cuda()
+    return t, t.data_ptr() + offset
+
+
+def _host(t, offset, like):
+    raw = t[offset:offset + like.nbytes].cpu().numpy()
+    return np.frombuffer(raw.tobytes(), dtype=like.dtype).copy()
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check_dev(L, op, dt, a, b, off_in=0, off_io=0):
+    exp = b.copy()
+    rc_o = oracle.reduce_local(h(op), h(dt), a, exp)
+    assert rc_o == 0
+    ta, pa = _dev(a, off_in)
+    tb, pb = _dev(b, off_io)
+    rc = L.msx_reduce_local_dev(pa, pb, a.size, h(dt), h(op), _stream())
+    assert rc == 0, msx.last_error()
+    torch.cuda.synchronize()
+    got = _host(tb, off_io, b)
+    ok = np.array_equal(np.frombuffer(got.tobytes(), np.uint8), np.frombuffer(exp.tobytes(), np.uint8))
+    if not ok:
+        bad = np.nonzero(np.frombuffer(got.tobytes(), np.uint8) != np.frombuffer(exp.tobytes(), np.uint8))[0]
+        i = bad[0] // got.dtype.itemsize
+        pytest.fail(f"{op} {dt} n={a.size} off=({off_in},{off_io}): elem {i}: "
+                    f"in={a[i]!r} inout={b[i]!r} got={got[i]!r} exp={exp[i]!r} ({len(bad)} bad bytes)")
+
+
+_PAIRS = None
+
+
+def _pairs():
+    global _PAIRS
+    if _PAIRS is None:
+        _PAIRS = legal_pairs(oracle)
+    return _PAIRS
+
+
+@pytest.mark.parametrize("pair", _pairs(), ids=lambda p: f"{p[0]}-{p[1]}")
+def test_every_legal_pair_bit_exact(L, pair):
+    op, dt = pair
+    kind = KIND[dt]
+    rng = np.random.default_rng(zlib.crc32(f"{op}/{dt}".encode()))
+    for n in (1, 3, 17, 1000, 65537):
+        a, b = gen(kind, op, n, rng), gen(kind, op, n, rng)
+        _check_dev(L, op, dt, a, b)
+
+
+@pytest.mark.parametrize("dt", ["MPI_FLOAT", "MPI_INT8_T", "MPI_SHORT", "MPI_DOUBLE", "MPI_DOUBLE_INT",
+                                "MPI_C_DOUBLE_COMPLEX", "MPI_SHORT_INT"])
+def test_unaligned_and_misaligned_pointers(L, dt):
+    kind = KIND[dt]
+    esz = itemsize(kind)
+    op = "MPI_MAXLOC" if kind in msx.LOC_DTYPES else "MPI_SUM"
+    rng = np.random.default_rng(7)
+    for n in (5, 4099):
+        a, b = gen(kind, op, n, rng), gen(kind, op, n, rng)
+        for off_in, off_io in ((esz, esz), (0, esz), (esz * 3, 0), (8, 8)):
+            if off_in % min(esz, 8) or off_io % min(esz, 8):
+                continue
+            _check_dev(L, op, dt, a, b, off_in, off_io)
+
+
+def test_loc_whole_struct_copy_includes_padding(L):
+    # loctype `*this = rhs` (op.cpp:327) copies the whole struct
+    rng = np.random.default_rng(9)
+    for dt, kind in (("MPI_DOUBLE_INT", "di"), ("MPI_SHORT_INT", "si")):
+        n = 4096
+        a, b = gen(kind, "MPI_MAXLOC", n, rng), gen(kind, "MPI_MAXLOC", n, rng)
+        ab = np.frombuffer(a.tobytes(), np.uint8).copy()
+        bb = np.frombuffer(b.tobytes(), np.uint8).copy()
+        isz = a.dtype.itemsize
+        pad = [i for i in range(isz) if i not in set(range(0, a.dtype["v"].itemsize)) | set(
+            range(a.dtype.fields["l"][1], a.dtype.fields["l"][1] + 4))]
+        for pbyte in pad:
+            ab[pbyte::isz] = rng.integers(0, 256, n, dtype=np.uint8)
+            bb[pbyte::isz] = rng.integers(0, 256, n, dtype=np.uint8)
+        a2 = np.frombuffer(ab.tobytes(), a.dtype).copy()
+        b2 = np.frombuffer(bb.tobytes(), a.dtype).copy()
+        _check_dev(L, "MPI_MAXLOC", dt, a2, b2)
+        _check_dev(L, "MPI_MINLOC", dt, a2, b2)
+
+
+def test_known_answer_vectors_on_gpu(L):
+    with open(os.path.join(os.path.dirname(__file__), "golden", "survey_kat.json")) as f:
+        kat = json.load(f)
+    case = next(c for c in kat["cases"] if c["id"] == "int_sum_wrap_1MiB")
+    i = np.arange(case["n"], dtype=np.int64)
+    a = (7 * i - 3).astype(np.int32)
+    b = (0x7FFFFFFF - i).astype(np.int32)
+    ta, pa = _dev(a)
+    tb, pb = _dev(b)
+    assert L.msx_reduce_local_dev(pa, pb, a.size, C.MPI_INT, C.MPI_SUM, _stream()) == 0
+    torch.cuda.synchronize()
+    got = _host(tb, 0, b)
+    assert got[0] == case["expect_first"] and got[-1] == case["expect_last"]
+    case = next(c for c in kat["cases"] if c["id"] == "f32_max_nan_zero")
+    to_f = lambda hx: np.array([int(x, 16) for x in hx], np.uint32).view(np.float32)
+    a, b = to_f(case["in_f32_hex"]), to_f(case["inout_f32_hex"])
+    ta, pa = _dev(a)
+    tb, pb = _dev(b)
+    assert L.msx_reduce_local_dev(pa, pb, 4, C.MPI_FLOAT, C.MPI_MAX, _stream()) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(_host(tb, 0, b).view(np.uint32), to_f(case["expect_f32_hex"]).view(np.uint32))
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_mpi_reduce_local_host_buffers_staged(L, pinned):
+    # the MPI path starts and ends in host memory: staged through HBM in chunks
+    assert L.msx_set_staging_chunk(1 << 20) == 0      # force many chunks
+    rng = np.random.default_rng(11)
+    for dt, op in (("MPI_FLOAT", "MPI_SUM"), ("MPI_UINT64_T", "MPI_BAND"), ("MPI_2INT", "MPI_MINLOC")):
+        kind = KIND[dt]
+        n = (3 << 20) // itemsize(kind) + 13
+        a, b = gen(kind, op, n, rng), gen(kind, op, n, rng)
+        exp = b.copy()
+        oracle.reduce_local(h(op), h(dt), a, exp)
+        if pinned:
+            ta = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory()
+            tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
+            rc = L.MPI_Reduce_local(ta.data_ptr(), tb.data_ptr(), n, h(dt), h(op))
+            got = np.frombuffer(tb.numpy().tobytes(), a.dtype)
+        else:
+            bb = b.copy()
+            rc = L.MPI_Reduce_local(a.ctypes.data, bb.ctypes.data, n, h(dt), h(op))
+            got = bb
+        assert rc == 0, msx.last_error()
+        assert got.tobytes() == exp.tobytes()
+    assert L.msx_set_staging_chunk(64 << 20) == 0
+
+
+def test_mpi_reduce_local_device_and_mixed(L):
+    rng = np.random.default_rng(12)
+    n = 100003
+    a = gen("f8", "MPI_PROD", n, rng)
+    b = gen("f8", "MPI_PROD", n, rng)
+    exp = b.copy()
+    oracle.reduce_local(C.MPI_PROD, C.MPI_DOUBLE, a, exp)
+    ta, pa = _dev(a)
+    tb, pb = _dev(b)
+    assert L.MPI_Reduce_local(pa, pb, n, C.MPI_DOUBLE, C.MPI_PROD) == 0
+    assert _host(tb, 0, b).tobytes() == exp.tobytes()
+    # host in, device inout
+    tb, pb = _dev(b)
+    assert L.MPI_Reduce_local(a.ctypes.data, pb, n, C.MPI_DOUBLE, C.MPI_PROD) == 0
+    assert _host(tb, 0, b).tobytes() == exp.tobytes()
+    # device in, host inout
+    bb = b.copy()
+    assert L.MPI_Reduce_local(pa, bb.ctypes.data, n, C.MPI_DOUBLE, C.MPI_PROD) == 0
+    assert bb.tobytes() == exp.tobytes()
+
+
+def test_user_op_on_device_buffers(L):
+    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+
+    def absmax(invec, inoutvec, n, dt):
+        x = np.ctypeslib.as_array((ctypes.c_float * n[0]).from_address(invec))
+        y = np.ctypeslib.as_array((ctypes.c_float * n[0]).from_address(inoutvec))
+        y[:] = np.maximum(np.abs(x), np.abs(y))
+
+    fn = UF(absmax)
+    op = ctypes.c_int()
+    assert L.MPI_Op_create(fn, 1, ctypes.byref(op)) == 0
+    a = np.linspace(-5, 5, 1001).astype(np.float32)
+    b = np.linspace(3, -3, 1001).astype(np.float32)
+    ta, pa = _dev(a)
+    tb, pb = _dev(b)
+    assert L.MPI_Reduce_local(pa, pb, a.size, C.MPI_FLOAT, op.value) == 0
+    assert np.array_equal(_host(tb, 0, b), np.maximum(np.abs(a), np.abs(b)))
+    assert L.MPI_Op_free(ctypes.byref(op)) == 0
+
+
+def test_tree_combine_reference_association(L):
+    # msx_reduce_tree_dev: ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)), left = inout
+    rng = np.random.default_rng(13)
+    n = 70001
+    xs = [(rng.standard_normal(n) * 10.0 ** rng.integers(-7, 7, n)).astype(np.float32) for _ in range(8)]
+    devs = [_dev(x) for x in xs]
+    out = torch.zeros(n, dtype=torch.float32, device="cuda")
+    for p in (2, 4, 8):
+        arr = (ctypes.c_void_p * p)(*[d[1] for d in devs[:p]])
+        assert L.msx_reduce_tree_dev(arr, p, out.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
+        torch.cuda.synchronize()
+        lv = list(xs[:p])
+        while len(lv) > 1:
+            lv = [lv[i] + lv[i + 1] for i in range(0, len(lv), 2)]
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), lv[0].view(np.uint32))
+    # MAX with NaNs: the role of each operand matters (op.cpp:26)
+    ys = [gen("f4", "MPI_MAX", n, rng) for _ in range(4)]
+    dv = [_dev(y) for y in ys]
+    arr = (ctypes.c_void_p * 4)(*[d[1] for d in dv])
+    assert L.msx_reduce_tree_dev(arr, 4, out.data_ptr(), n, C.MPI_FLOAT, C.MPI_MAX, _stream()) == 0
+    torch.cuda.synchronize()
+    l0, l1 = ys[0].copy(), ys[2].copy()
+    oracle.reduce_local(C.MPI_MAX, C.MPI_FLOAT, ys[1], l0)
+    oracle.reduce_local(C.MPI_MAX, C.MPI_FLOAT, ys[3], l1)
+    oracle.reduce_local(C.MPI_MAX, C.MPI_FLOAT, l1, l0)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), l0.view(np.uint32))
+
+
+def test_benchmark_size_fp32_sum_bit_exact(L):
+    # config 2 (BASELINE.json): 256 MiB fp32 per operand, device resident.
+    n = 64 << 20
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    a = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    b = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    exp = (a + b)       # one IEEE fp32 add per element (torch fp32 reference)
+    assert L.msx_reduce_local_dev(a.data_ptr(), b.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(b.view(torch.int32), exp.view(torch.int32))
+    # and for every tuning variant
+    ref = b.clone()
+    for v in range(L.msx_tune_variant_count()):
+        assert L.msx_tune_set(v, 0) == 0
+        c = b.clone()
+        assert L.msx_reduce_local_dev(a.data_ptr(), c.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(c.view(torch.int32), (ref + a).view(torch.int32)), L.msx_tune_variant_name(v)
+    assert L.msx_tune_set(0, 0) == 0
