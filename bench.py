@@ -128,7 +128,8 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
     src = torch.rand(n, device=dev, generator=g) * 2 - 1
     acc = torch.rand(n, device=dev, generator=g) * 2 - 1
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)          # the launch stream of every timed kernel
+    torch.cuda.set_stream(stream)
     sp = ctypes.c_void_p(stream.cuda_stream)
 
     def step():
@@ -146,20 +147,26 @@ def main():
 
     sweep = {}
     if args.sweep and rank == 0:
-        for v in range(L.msx_tune_variant_count()):
-            L.msx_tune_set(v, 0)
-            for _ in range(5):
-                step()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(20):
-                step()
-            e1.record(stream)
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / 20
-            sweep[L.msx_tune_variant_name(v).decode()] = round(n * BYTES_PER_ELEM / ms / 1e6, 1)
-            print(f"variant {v} {L.msx_tune_variant_name(v).decode()}: {ms * 1e3:.1f} us "
-                  f"{n * BYTES_PER_ELEM / ms / 1e6:.0f} GB/s", file=sys.stderr)
+        # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
+        configs = [(v, cap) for v in range(L.msx_tune_variant_count()) for cap in (0, 2048, 4096, 8192)]
+        times = {c: [] for c in configs}
+        for _ in range(3):
+            for (v, cap) in configs:
+                L.msx_tune_set(v, cap)
+                for _ in range(3):
+                    step()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(10):
+                    step()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times[(v, cap)].append(e0.elapsed_time(e1) / 10)
+        for (v, cap), ts in times.items():
+            ms = sorted(ts)[len(ts) // 2]
+            key = f"{L.msx_tune_variant_name(v).decode()}/cap{cap}"
+            sweep[key] = round(n * BYTES_PER_ELEM / ms / 1e6, 1)
+            print(f"{key}: {ms * 1e3:.1f} us {sweep[key]:.0f} GB/s", file=sys.stderr)
         L.msx_tune_set(max(args.variant, 0), 0)
 
     for _ in range(args.warmup):

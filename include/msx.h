@@ -2,7 +2,7 @@
  * msx.h — device-side C ABI of the MI355X MS-MPI reduction path.
  *
  * Plain C, no HIP/torch types: streams are passed as `void*` (a hipStream_t,
- * NULL = the library's internal stream for the current device).
+ * NULL = the HIP null stream, as with any HIP API).
  *
  * Each entry point names the reference interface it replaces:
  *

@@ -700,7 +700,7 @@ MSX_EXPORT int msx_reduce_local_dev(const void* in, void* inout, int64_t count, 
     if (in == inout) { set_error("inbuf aliases inoutbuf"); return MPI_ERR_BUFFER; }
     rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : internal_stream();
+    hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the HIP null stream
     return reduce_local_device(r.opidx, type_info(dt)->kind, in, inout, (size_t)count, s);
 }
 
@@ -719,7 +719,7 @@ MSX_EXPORT int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, in
     }
     rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : internal_stream();
+    hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the HIP null stream
     hipError_t e = launch_tree(r.opidx, type_info(dt)->kind, srcs, p, out, (size_t)count, s);
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "tree kernel launch");
 }

@@ -407,6 +407,11 @@ const Variant kF32SumVariants[] = {
     {"u2_b512", run_combine<O_SUM, float, float, 2, 512, false, false>},
     {"u8_b128", run_combine<O_SUM, float, float, 8, 128, false, false>},
     {"u16_b256_ntld", run_combine<O_SUM, float, float, 16, 256, true, false>},
+    {"u4_b256_ntst", run_combine<O_SUM, float, float, 4, 256, false, true>},
+    {"u2_b1024", run_combine<O_SUM, float, float, 2, 1024, false, false>},
+    {"u4_b128", run_combine<O_SUM, float, float, 4, 128, false, false>},
+    {"u2_b256_ntst", run_combine<O_SUM, float, float, 2, 256, false, true>},
+    {"u1_b512", run_combine<O_SUM, float, float, 1, 512, false, false>},
 };
 constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
 

@@ -47,7 +47,13 @@ def _dev(a, offset=0):
 
 def _host(t, offset, like):
     raw = t[offset:offset + like.nbytes].cpu().numpy()
-    return np.frombuffer(raw.tobytes(), dtype=like.dtype).copy()
+    return _raw(raw, like.dtype)
+
+
+def _raw(a, dtype=None):
+    """Writable array over a private byte copy of `a` (padding bytes kept:
+    numpy's copy() of structured arrays does not preserve them)."""
+    return np.frombuffer(bytearray(a.tobytes()), dtype=dtype if dtype is not None else a.dtype)
 
 
 def _stream():
@@ -55,7 +61,8 @@ def _stream():
 
 
 def _check_dev(L, op, dt, a, b, off_in=0, off_io=0):
-    exp = b.copy()
+    a, b = _raw(a), _raw(b)
+    exp = _raw(b)
     rc_o = oracle.reduce_local(h(op), h(dt), a, exp)
     assert rc_o == 0
     ta, pa = _dev(a, off_in)
@@ -121,8 +128,8 @@ def test_loc_whole_struct_copy_includes_padding(L):
         for pbyte in pad:
             ab[pbyte::isz] = rng.integers(0, 256, n, dtype=np.uint8)
             bb[pbyte::isz] = rng.integers(0, 256, n, dtype=np.uint8)
-        a2 = np.frombuffer(ab.tobytes(), a.dtype).copy()
-        b2 = np.frombuffer(bb.tobytes(), a.dtype).copy()
+        a2 = _raw(ab, a.dtype)
+        b2 = _raw(bb, a.dtype)
         _check_dev(L, "MPI_MAXLOC", dt, a2, b2)
         _check_dev(L, "MPI_MINLOC", dt, a2, b2)
 
