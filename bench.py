@@ -50,31 +50,31 @@ def parse():
     return ap.parse_args()
 
 
-def traffic_from_profiles(kernel_substr="k_combineILi3EffLi4ELi256ELb0ELb0"):
-    """Per-launch HBM bytes from the newest committed PMC counter collection."""
+def traffic_from_profiles(kernel_substr="k_combineILi3EffLi4ELi256ELb1ELb0"):
+    """Per-launch HBM bytes of the default fp32 SUM kernel from the newest
+    committed rocprofv3 PMC collection (profiles/<round>/pmc_*counter_collection.csv,
+    FETCH_SIZE and WRITE_SIZE in separate passes)."""
+    dirs = sorted({os.path.dirname(p) for p in
+                   glob.glob(os.path.join(REPO, "profiles", "*", "pmc_*counter_collection.csv"))})
     best = None
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_*counter_collection.csv"))):
-        fetch, write, n = {}, {}, 0
-        with open(path) as f:
-            hdr = f.readline().strip().split(",")
-            idx = {k.strip('"'): i for i, k in enumerate(hdr)}
-            for line in f:
-                cols = line.rstrip("\n").split(",")
-                if len(cols) < len(hdr):
-                    continue
-                name = cols[idx["Kernel_Name"]]
-                if kernel_substr not in name:
-                    continue
-                disp = cols[idx["Dispatch_Id"]]
-                cn, val = cols[idx["Counter_Name"]].strip('"'), float(cols[idx["Counter_Value"]])
-                if cn == "FETCH_SIZE":
-                    fetch[disp] = val
-                elif cn == "WRITE_SIZE":
-                    write[disp] = val
-        if fetch and write:
-            f_kb = sum(fetch.values()) / len(fetch)
-            w_kb = sum(write.values()) / len(write)
-            # gfx950: FETCH_SIZE reads 1/2 of a 16-B/lane streaming read; KiB units
+    for d in dirs:
+        vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+        for path in glob.glob(os.path.join(d, "pmc_*counter_collection.csv")):
+            with open(path) as f:
+                hdr = [k.strip('"') for k in f.readline().strip().split(",")]
+                idx = {k: i for i, k in enumerate(hdr)}
+                for line in f:
+                    cols = line.rstrip("\n").split(",")
+                    if len(cols) < len(hdr) or kernel_substr not in ",".join(cols[idx["Kernel_Name"]:]):
+                        continue
+                    cn = cols[-2 if "Counter_Value" not in idx else idx["Counter_Name"]].strip('"')
+                    if cn in vals:
+                        vals[cn].append(float(cols[idx["Counter_Value"]]))
+        if vals["FETCH_SIZE"] and vals["WRITE_SIZE"]:
+            f_kb = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
+            w_kb = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
+            # gfx950: FETCH_SIZE reports 1/2 of a 16-B/lane streaming read
+            # (MI355X_MICROARCH.md §HBM); both counters are in KiB
             best = (2.0 * f_kb + w_kb) * 1024.0
     return best
 
