@@ -50,26 +50,21 @@ def parse():
     return ap.parse_args()
 
 
-def traffic_from_profiles(kernel_substr="k_combineILi3EffLi4ELi256ELb1ELb0"):
+def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 4, 256, true, false>"):
     """Per-launch HBM bytes of the default fp32 SUM kernel from the newest
     committed rocprofv3 PMC collection (profiles/<round>/pmc_*counter_collection.csv,
-    FETCH_SIZE and WRITE_SIZE in separate passes)."""
+    FETCH_SIZE and WRITE_SIZE collected in separate passes)."""
+    import csv
     dirs = sorted({os.path.dirname(p) for p in
                    glob.glob(os.path.join(REPO, "profiles", "*", "pmc_*counter_collection.csv"))})
     best = None
     for d in dirs:
         vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
         for path in glob.glob(os.path.join(d, "pmc_*counter_collection.csv")):
-            with open(path) as f:
-                hdr = [k.strip('"') for k in f.readline().strip().split(",")]
-                idx = {k: i for i, k in enumerate(hdr)}
-                for line in f:
-                    cols = line.rstrip("\n").split(",")
-                    if len(cols) < len(hdr) or kernel_substr not in ",".join(cols[idx["Kernel_Name"]:]):
-                        continue
-                    cn = cols[-2 if "Counter_Value" not in idx else idx["Counter_Name"]].strip('"')
-                    if cn in vals:
-                        vals[cn].append(float(cols[idx["Counter_Value"]]))
+            with open(path, newline="") as f:
+                for row in csv.DictReader(f):
+                    if kernel_substr in row["Kernel_Name"] and row["Counter_Name"] in vals:
+                        vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
         if vals["FETCH_SIZE"] and vals["WRITE_SIZE"]:
             f_kb = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
             w_kb = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])

@@ -580,9 +580,10 @@ int host_user_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t coun
 int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                  const OpRef& op)
 {
+    // user functions are host code: no GPU needed on this path
+    if (op.opidx == O_NULL) return host_user_allreduce(c, sendbuf, recvbuf, count, dt, op);
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
-    if (op.opidx == O_NULL) return host_user_allreduce(c, sendbuf, recvbuf, count, dt, op);
 
     Transport* tp = c->tp;
     const int p = c->size, me = c->rank;

@@ -1,0 +1,282 @@
+"""CPU: the multi-rank path without a GPU.
+
+1. The collective engine's schedules (expression trees per rank/block,
+   msx_schedule_*) evaluated with the oracle's combine reproduce, bit for bit,
+   the oracle's step-by-step simulation of the reference schedules
+   (reduce.cpp:3768-4104, 917-1334) for p = 1..9, including the
+   non-power-of-two fold and order-sensitive data (fp32 SUM over a wide
+   dynamic range, MAX with NaN and +-0).
+2. world_size-2 gloo: two processes exchange their contributions with
+   torch.distributed (gloo) and each evaluates its own schedule; results match
+   the simulator.
+3. The library's own bootstrap (TCP hub): two MPI processes initialise, agree
+   on rank/size, barrier, run a user-op MPI_Allreduce on host buffers (host
+   code, no GPU), and fail loudly (MPI_ERR_OTHER) for builtin-op collectives
+   on a GPU-less host instead of computing on the CPU.
+"""
+import ctypes
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+import msx
+import oracle
+
+C = msx.C
+REPO = msx.REPO_ROOT
+
+
+def schedule_tree(which, p, n):
+    L = msx.lib()
+    src = (ctypes.c_int * 32)()
+    P, pm, ch = ctypes.c_int(), ctypes.c_uint(), ctypes.c_int()
+    L.msx_schedule_tree.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 4
+    assert L.msx_schedule_tree(which, p, n, src, ctypes.byref(P), ctypes.byref(pm), ctypes.byref(ch)) == 0
+    return list(src), P.value, pm.value, bool(ch.value)
+
+
+def schedule_block(p, count, n):
+    L = msx.lib()
+    s, ln = ctypes.c_int64(), ctypes.c_int64()
+    L.msx_schedule_block.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.msx_schedule_block(p, count, n, ctypes.byref(s), ctypes.byref(ln))
+    return s.value, ln.value
+
+
+def algo(which, p, count, tsize):
+    L = msx.lib()
+    L.msx_schedule_algo.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int]
+    return L.msx_schedule_algo(which, p, count, tsize)
+
+
+def newrank(r, p):
+    return msx.lib().msx_schedule_newrank(r, p)
+
+
+def eval_tree(tree, xs, op, dt, lo, hi):
+    """Evaluate a schedule tree with the oracle's combine (left = inout)."""
+    src, P, pm, chain = tree
+    if chain:
+        v = xs[src[0]][lo:hi].copy()
+        for k in range(1, P):
+            oracle.reduce_local(op, dt, xs[src[k]][lo:hi].copy(), v)
+        return v
+    leaves = []
+    for k in range(P):
+        v = xs[src[2 * k]][lo:hi].copy()
+        if (pm >> k) & 1:
+            oracle.reduce_local(op, dt, xs[src[2 * k + 1]][lo:hi].copy(), v)
+        leaves.append(v)
+    w = 1
+    while w < P:
+        for k in range(0, P, 2 * w):
+            oracle.reduce_local(op, dt, leaves[k + w], leaves[k])
+        w *= 2
+    return leaves[0]
+
+
+def engine_allreduce_result(xs, op, dt, rank):
+    """What the engine computes for `rank` (recvbuf) from its schedules."""
+    p, count = len(xs), xs[0].size
+    esz = xs[0].dtype.itemsize
+    n = newrank(rank, p)
+    if algo(0, p, count, esz) == 0:        # recursive doubling: own lineage, whole vector
+        nn = n if n >= 0 else newrank(rank + 1, p)
+        return eval_tree(schedule_tree(0, p, nn), xs, op, dt, 0, count)
+    out = np.empty_like(xs[0])
+    pof2 = 1 << (p.bit_length() - 1)
+    for m in range(pof2):                   # every block, computed by its owner m
+        lo, ln = schedule_block(p, count, m)
+        out[lo:lo + ln] = eval_tree(schedule_tree(0, p, m), xs, op, dt, lo, lo + ln)
+    return out
+
+
+def engine_reduce_scatter_result(xs, counts, op, dt, rank):
+    p = len(xs)
+    total = sum(counts)
+    esz = xs[0].dtype.itemsize
+    disp = np.concatenate([[0], np.cumsum(counts)]).astype(int)
+    if algo(1, p, total, esz) == 3:
+        t = schedule_tree(2, p, rank)
+    else:
+        n = newrank(rank, p)
+        t = schedule_tree(1, p, n if n >= 0 else newrank(rank + 1, p))
+    return eval_tree(t, xs, op, dt, disp[rank], disp[rank + 1])
+
+
+def _data(p, count, op, seed):
+    rng = np.random.default_rng(seed)
+    xs = []
+    for _ in range(p):
+        if op == C.MPI_SUM:
+            x = (rng.standard_normal(count) * 10.0 ** rng.integers(-6, 7, count)).astype(np.float32)
+        else:
+            x = rng.integers(-3, 4, count).astype(np.float32)
+            x[rng.random(count) < 0.1] = np.nan
+            x[rng.random(count) < 0.1] = -0.0
+        xs.append(x)
+    return xs
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("count", [13, 70001])      # recursive doubling / Rabenseifner
+@pytest.mark.parametrize("opname", ["MPI_SUM", "MPI_MAX"])
+def test_engine_allreduce_schedule_matches_reference_simulation(p, count, opname):
+    op = getattr(C, opname)
+    xs = _data(p, count, op, 100 * p + count % 97)
+    rb = [np.zeros(count, np.float32) for _ in range(p)]
+    assert oracle.allreduce(op, C.MPI_FLOAT, xs, rb) == 0
+    for r in range(p):
+        got = engine_allreduce_result(xs, op, C.MPI_FLOAT, r)
+        assert np.array_equal(got.view(np.uint32), rb[r].view(np.uint32)), (p, count, r)
+
+
+@pytest.mark.parametrize("p", [2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize("per", [5, 9000])          # recursive halving / pairwise
+@pytest.mark.parametrize("opname", ["MPI_SUM", "MPI_MAX"])
+def test_engine_reduce_scatter_schedule_matches_reference_simulation(p, per, opname):
+    op = getattr(C, opname)
+    counts = [per + (i % 3) for i in range(p)]
+    xs = _data(p, sum(counts), op, 7 * p + per)
+    rb = [np.zeros(c, np.float32) for c in counts]
+    assert oracle.reduce_scatter(op, C.MPI_FLOAT, counts, xs, rb) == 0
+    for r in range(p):
+        got = engine_reduce_scatter_result(xs, counts, op, C.MPI_FLOAT, r)
+        assert np.array_equal(got.view(np.uint32), rb[r].view(np.uint32)), (p, per, r)
+
+
+def test_algorithm_gates_follow_reference_32bit_arithmetic():
+    # allreduce: RD iff (unsigned)(count*size) <= 256 KiB or count < pof2 (reduce.cpp:3884)
+    assert algo(0, 8, 65536, 4) == 0 and algo(0, 8, 65537, 4) == 1
+    assert algo(0, 8, 7, 4) == 0
+    assert algo(0, 8, 1 << 30, 4) == 0     # 4 GiB wraps to 0 bytes: recursive doubling
+    # reduce_scatter: c4 (536870912 doubles = 2^32 B) wraps to 0 -> recursive halving
+    assert algo(1, 8, 536870912, 8) == 2
+    assert algo(1, 8, 65536, 8) == 3 and algo(1, 8, 65535, 8) == 2
+
+
+# ---------------------------------------------------------------------------
+# world_size 2 over gloo
+# ---------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+GLOO_WORKER = r'''
+import os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd")); sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np, torch, torch.distributed as dist
+import msx, oracle
+from test_collectives_cpu import engine_allreduce_result, engine_reduce_scatter_result, _data
+C = msx.C
+dist.init_process_group("gloo", init_method="env://")
+rank, p = dist.get_rank(), dist.get_world_size()
+ok = True
+for count in (33, 90001):
+    for op in (C.MPI_SUM, C.MPI_MAX):
+        mine = _data(p, count, op, 5 + count)[rank]
+        bufs = [torch.zeros(count, dtype=torch.float32) for _ in range(p)]
+        dist.all_gather(bufs, torch.from_numpy(mine))        # the exchange step over gloo
+        xs = [b.numpy() for b in bufs]
+        got = engine_allreduce_result(xs, op, C.MPI_FLOAT, rank)
+        rb = [np.zeros(count, np.float32) for _ in range(p)]
+        oracle.allreduce(op, C.MPI_FLOAT, xs, rb)
+        ok &= np.array_equal(got.view(np.uint32), rb[rank].view(np.uint32))
+        counts = [count // p] * p
+        got = engine_reduce_scatter_result(xs, counts, op, C.MPI_FLOAT, rank)
+        rs = [np.zeros(c, np.float32) for c in counts]
+        oracle.reduce_scatter(op, C.MPI_FLOAT, counts, xs, rs)
+        ok &= np.array_equal(got.view(np.uint32), rs[rank].view(np.uint32))
+flag = torch.tensor([1 if ok else 0])
+dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+print("RESULT", rank, int(flag.item()))
+dist.destroy_process_group()
+'''
+
+
+def _spawn(code, ranks, extra_env):
+    procs = []
+    for r in range(ranks):
+        env = dict(os.environ)
+        env.update(extra_env(r))
+        procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(code)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    outs = []
+    for pr in procs:
+        try:
+            o, e = pr.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            pr.kill()
+            o, e = pr.communicate()
+        outs.append((pr.returncode, o, e))
+    return outs
+
+
+def test_gloo_world_size_2_engine_schedule():
+    port = _free_port()
+    outs = _spawn(GLOO_WORKER, 2, lambda r: {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                                             "RANK": str(r), "WORLD_SIZE": "2"})
+    for rc, o, e in outs:
+        assert rc == 0, e[-2000:]
+        assert "RESULT" in o and o.strip().split()[-1] == "1", o + e[-2000:]
+
+
+MPI_WORKER = r'''
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
+import numpy as np
+import msx
+C = msx.C
+L = msx.init(errors_return=True)
+r, s = ctypes.c_int(), ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r)); L.MPI_Comm_size(C.MPI_COMM_WORLD, ctypes.byref(s))
+assert L.MPI_Barrier(C.MPI_COMM_WORLD) == 0
+UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+def sub(a, b, n, dt):   # non-commutative: inout = in - inout
+    x = np.ctypeslib.as_array((ctypes.c_double * n[0]).from_address(a))
+    y = np.ctypeslib.as_array((ctypes.c_double * n[0]).from_address(b))
+    y[:] = x - y
+fn = UF(sub)
+op = ctypes.c_int()
+assert L.MPI_Op_create(fn, 0, ctypes.byref(op)) == 0
+send = np.array([10.0 * (r.value + 1), 1.0 + r.value], dtype=np.float64)
+recv = np.zeros(2, np.float64)
+rc = L.MPI_Allreduce(send.ctypes.data, recv.ctypes.data, 2, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD)
+assert rc == 0, msx.last_error()
+b = np.zeros(4, np.float32)
+rc2 = L.MPI_Allreduce(b.ctypes.data, np.zeros(4, np.float32).ctypes.data, 4, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+gpu = L.msx_device_count() > 0
+print("OUT", r.value, s.value, recv.tolist(), rc2, int(gpu))
+assert L.MPI_Finalize() == 0
+'''
+
+
+def test_two_mpi_processes_bootstrap_and_user_op_allreduce():
+    port = _free_port()
+    outs = _spawn(MPI_WORKER, 2, lambda r: {"MSX_SIZE": "2", "MSX_RANK": str(r),
+                                            "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1"})
+    res = {}
+    for rc, o, e in outs:
+        assert rc == 0, e[-3000:]
+        line = [l for l in o.splitlines() if l.startswith("OUT")][0].split(" ", 1)[1]
+        rk, sz, rest = line.split(" ", 2)
+        res[int(rk)] = (int(sz), rest)
+    assert set(res) == {0, 1} and all(v[0] == 2 for v in res.values())
+    # p = 2, recursive doubling with a non-commutative op: both ranks get
+    # x0 op x1 = in(x0) - inout(x1) with the lower rank's data as `in`
+    # (reduce.cpp:3909-3924): [10-20, 1-2] = [-10, -1]
+    for rk in (0, 1):
+        assert res[rk][1].startswith("[-10.0, -1.0]"), res
+        gpu = res[rk][1].rstrip().endswith("1")
+        rc2 = int(res[rk][1].split()[-2])
+        assert rc2 == (0 if gpu else C.MPI_ERR_OTHER)

@@ -1,0 +1,181 @@
+"""GPU: the multi-rank collectives end to end, several MPI processes per GPU.
+
+One MI355X box has one GPU, so p = 2, 3, 4 ranks share it: the engine's IPC
+peer mapping, bootstrap hub, schedule-faithful combine kernels and allgather
+copies all run for real (peer HBM is the same HBM here).  Each rank derives
+every rank's input from a shared seed and compares its result with the
+oracle's step-by-step simulation of the reference schedule, bit for bit.
+"""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+import msx
+
+pytestmark = pytest.mark.gpu
+REPO = msx.REPO_ROOT
+
+WORKER = r'''
+import ctypes, os, sys, time
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd")); sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np, torch
+import msx, oracle
+from _cases import gen, KIND
+C = msx.C
+L = msx.init(errors_return=True)
+r_, s_ = ctypes.c_int(), ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r_)); L.MPI_Comm_size(C.MPI_COMM_WORLD, ctypes.byref(s_))
+rank, p = r_.value, s_.value
+fails = []
+
+def raw(a):
+    return np.frombuffer(bytearray(a.tobytes()), dtype=a.dtype)
+
+def todev(a):
+    t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
+    if a.nbytes:
+        t.copy_(torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()))
+    return t
+
+def fromdev(t, like, n=None):
+    n = like.size if n is None else n
+    return np.frombuffer(bytearray(t[: n * like.dtype.itemsize].cpu().numpy().tobytes()), like.dtype)
+
+def check(tag, got, exp):
+    if got.tobytes() != exp.tobytes():
+        fails.append(tag)
+
+def inputs(op, dt, count, seed):
+    rng = np.random.default_rng(seed)
+    return [raw(gen(KIND[dt], op, count, rng)) for _ in range(p)]
+
+ALLREDUCE = [("MPI_SUM", "MPI_FLOAT", 1000), ("MPI_SUM", "MPI_FLOAT", 100003),
+             ("MPI_MAX", "MPI_FLOAT", 70001), ("MPI_MAX", "MPI_DOUBLE", 50),
+             ("MPI_BAND", "MPI_UINT64_T", 65536), ("MPI_SUM", "MPI_INT8_T", 300001),
+             ("MPI_MAXLOC", "MPI_DOUBLE_INT", 40000), ("MPI_PROD", "MPI_C_FLOAT_COMPLEX", 33333),
+             ("MPI_LXOR", "MPI_C_BOOL", 777)]
+for i, (opn, dtn, count) in enumerate(ALLREDUCE):
+    op, dt = getattr(C, opn), getattr(C, dtn)
+    xs = inputs(opn, dtn, count, 1000 + i)
+    exp = [raw(x.copy()) for x in xs]
+    assert oracle.allreduce(op, dt, xs, exp) == 0
+    for mode in ("dev", "inplace", "host"):
+        if mode == "dev":
+            sb, rb = todev(xs[rank]), torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+            rc = L.MPI_Allreduce(sb.data_ptr(), rb.data_ptr(), count, dt, op, C.MPI_COMM_WORLD)
+            got = fromdev(rb, xs[rank])
+        elif mode == "inplace":
+            rb = todev(xs[rank])
+            rc = L.MPI_Allreduce(ctypes.c_void_p(-1 & 0xffffffffffffffff), rb.data_ptr(), count, dt, op,
+                                 C.MPI_COMM_WORLD)
+            got = fromdev(rb, xs[rank])
+        else:
+            hb = raw(np.zeros_like(xs[rank]))
+            rc = L.MPI_Allreduce(xs[rank].ctypes.data, hb.ctypes.data, count, dt, op, C.MPI_COMM_WORLD)
+            got = hb
+        if rc != 0:
+            fails.append(f"allreduce {opn} {dtn} {count} {mode} rc={rc} {msx.last_error()}")
+            continue
+        check(f"allreduce {opn} {dtn} {count} {mode}", got, exp[rank])
+
+RS = [("MPI_MAX", "MPI_DOUBLE", 1000), ("MPI_SUM", "MPI_FLOAT", 40000), ("MPI_SUM", "MPI_FLOAT", 7),
+      ("MPI_BXOR", "MPI_INT", 20000)]
+for i, (opn, dtn, per) in enumerate(RS):
+    op, dt = getattr(C, opn), getattr(C, dtn)
+    counts = [per + (k % 2) * 3 for k in range(p)]
+    tot = sum(counts)
+    xs = inputs(opn, dtn, tot, 2000 + i)
+    exp = [raw(np.zeros(c, dtype=xs[0].dtype)) for c in counts]
+    assert oracle.reduce_scatter(op, dt, counts, xs, exp) == 0
+    cnt = (ctypes.c_int * p)(*counts)
+    for mode in ("dev", "inplace"):
+        if mode == "dev":
+            sb = todev(xs[rank])
+            rb = torch.zeros(max(counts[rank] * xs[0].dtype.itemsize, 1), dtype=torch.uint8, device="cuda")
+            rc = L.MPI_Reduce_scatter(sb.data_ptr(), rb.data_ptr(), cnt, dt, op, C.MPI_COMM_WORLD)
+        else:
+            rb = todev(xs[rank])
+            rc = L.MPI_Reduce_scatter(ctypes.c_void_p(-1 & 0xffffffffffffffff), rb.data_ptr(), cnt, dt, op,
+                                      C.MPI_COMM_WORLD)
+        if rc != 0:
+            fails.append(f"reduce_scatter {opn} {dtn} {per} {mode} rc={rc} {msx.last_error()}")
+            continue
+        check(f"reduce_scatter {opn} {dtn} {per} {mode}", fromdev(rb, exp[rank], counts[rank]), exp[rank])
+
+# MPI_Reduce (integer: order-independent) at two roots
+xs = inputs("MPI_SUM", "MPI_INT", 5000, 3000)
+exp = np.sum(np.stack(xs).astype(np.int64), axis=0).astype(np.int32)
+for root in (0, p - 1):
+    sb = todev(xs[rank])
+    rb = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+    rc = L.MPI_Reduce(sb.data_ptr(), rb.data_ptr(), 5000, C.MPI_INT, C.MPI_SUM, root, C.MPI_COMM_WORLD)
+    if rc != 0:
+        fails.append(f"reduce root={root} rc={rc} {msx.last_error()}")
+    elif rank == root:
+        check(f"reduce root={root}", fromdev(rb, xs[rank]), exp)
+
+# MPI_Iallreduce BAND u64 (config 5 op/type) overlapped with host compute
+xs = inputs("MPI_BAND", "MPI_UINT64_T", 1 << 18, 4000)
+exp = [raw(x.copy()) for x in xs]
+oracle.allreduce(C.MPI_BAND, C.MPI_UINT64_T, xs, exp)
+sb, rb = todev(xs[rank]), torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+req = ctypes.c_int()
+rc = L.MPI_Iallreduce(sb.data_ptr(), rb.data_ptr(), 1 << 18, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD,
+                      ctypes.byref(req))
+host = np.random.default_rng(1).random(1 << 20)
+flag, polls = ctypes.c_int(0), 0
+while rc == 0 and not flag.value:
+    host = 1.0001 * host + 0.5           # host work between tests
+    rc = L.MPI_Test(ctypes.byref(req), ctypes.byref(flag), None)
+    polls += 1
+if rc != 0:
+    fails.append(f"iallreduce rc={rc} {msx.last_error()}")
+else:
+    check("iallreduce band u64", fromdev(rb, xs[rank]), exp[rank])
+assert req.value == C.MPI_REQUEST_NULL
+
+print("RESULT", rank, p, len(fails), fails[:5], flush=True)
+L.MPI_Finalize()
+'''
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("p", [2, 3, 4])
+def test_collectives_p_ranks_on_one_gpu(p):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = _free_port()
+    procs = []
+    for r in range(p):
+        env = dict(os.environ)
+        env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
+                    "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
+                    "MSX_BOOTSTRAP_TIMEOUT": "180"})
+        procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    results = []
+    for pr in procs:
+        try:
+            o, e = pr.communicate(timeout=400)
+        except subprocess.TimeoutExpired:
+            pr.kill()
+            o, e = pr.communicate()
+        results.append((pr.returncode, o, e))
+    for rc, o, e in results:
+        assert rc == 0, (o + e)[-3000:]
+        line = [l for l in o.splitlines() if l.startswith("RESULT")]
+        assert line, (o + e)[-3000:]
+        assert line[0].split()[3] == "0", line[0]
