@@ -58,15 +58,38 @@ template <> struct Fn<O_MIN> {
     template <class T> __device__ static T apply(T io, T in) { return io < in ? io : in; }
 };
 
+// ---- floating-point arithmetic with the reference platform's NaN rule ------
+// IEEE 754 leaves a NaN result's payload open.  The reference runs on x86-64
+// SSE: `x op y` yields x's NaN (quieted) if x is a NaN, else y's (quieted),
+// else the x86 default NaN (sign set) for invalid operations such as inf-inf.
+// The kernels apply that rule explicitly with the operands in op.cpp's
+// textual order, so NaN results are bit-identical too (oracle: msx_oracle.c).
+// Non-NaN results are the plain IEEE op; the check is one compare + select.
+__device__ __forceinline__ float qnan(float x) { return __uint_as_float(__float_as_uint(x) | 0x00400000u); }
+__device__ __forceinline__ double qnan(double x)
+{
+    return __longlong_as_double(__double_as_longlong(x) | 0x0008000000000000ll);
+}
+__device__ __forceinline__ float dnan(float) { return __uint_as_float(0xFFC00000u); }
+__device__ __forceinline__ double dnan(double) { return __longlong_as_double((long long)0xFFF8000000000000ull); }
+template <class T> __device__ __forceinline__ T x86nan(T r, T x, T y)
+{
+    if (__builtin_expect(r == r, 1)) return r;
+    return (x != x) ? qnan(x) : ((y != y) ? qnan(y) : dnan(x));
+}
+template <class T> __device__ __forceinline__ T fadd(T x, T y) { return x86nan<T>(x + y, x, y); }
+template <class T> __device__ __forceinline__ T fsub(T x, T y) { return x86nan<T>(x - y, x, y); }
+template <class T> __device__ __forceinline__ T fmul(T x, T y) { return x86nan<T>(x * y, x, y); }
+
 // Op<T>::Sum (op.cpp:42-52) and complex += (op.cpp:287-292)
 template <> struct Fn<O_SUM> {
     template <class T>
     __device__ static typename std::enable_if<std::is_integral<T>::value, T>::type apply(T io, T in)
     { return Wrap<T>::add(io, in); }
-    __device__ static float apply(float io, float in) { return io + in; }
-    __device__ static double apply(double io, double in) { return io + in; }
-    __device__ static c32 apply(c32 io, c32 in) { return c32{io.re + in.re, io.im + in.im}; }
-    __device__ static c64 apply(c64 io, c64 in) { return c64{io.re + in.re, io.im + in.im}; }
+    __device__ static float apply(float io, float in) { return fadd(io, in); }
+    __device__ static double apply(double io, double in) { return fadd(io, in); }
+    __device__ static c32 apply(c32 io, c32 in) { return c32{fadd(io.re, in.re), fadd(io.im, in.im)}; }
+    __device__ static c64 apply(c64 io, c64 in) { return c64{fadd(io.re, in.re), fadd(io.im, in.im)}; }
 };
 
 // Op<T>::Prod (op.cpp:54-64) and complex *= (op.cpp:294-303): 4 mul + 2 add,
@@ -74,16 +97,16 @@ template <> struct Fn<O_SUM> {
 template <class C> __device__ inline C cmul(C io, C in)
 {
 #pragma clang fp contract(off)
-    auto r = (io.re * in.re) - (io.im * in.im);
-    auto i = (io.re * in.im) + (in.re * io.im);
+    auto r = fsub(fmul(io.re, in.re), fmul(io.im, in.im));
+    auto i = fadd(fmul(io.re, in.im), fmul(in.re, io.im));
     return C{r, i};
 }
 template <> struct Fn<O_PROD> {
     template <class T>
     __device__ static typename std::enable_if<std::is_integral<T>::value, T>::type apply(T io, T in)
     { return Wrap<T>::mul(io, in); }
-    __device__ static float apply(float io, float in) { return io * in; }
-    __device__ static double apply(double io, double in) { return io * in; }
+    __device__ static float apply(float io, float in) { return fmul(io, in); }
+    __device__ static double apply(double io, double in) { return fmul(io, in); }
     __device__ static c32 apply(c32 io, c32 in) { return cmul(io, in); }
     __device__ static c64 apply(c64 io, c64 in) { return cmul(io, in); }
 };

@@ -211,27 +211,55 @@ static int do_min(int k, const void* in, void* inout, int64_t count)
     }
 }
 
+/* Floating-point arithmetic with the reference platform's NaN rule.
+ * IEEE 754 leaves the payload of a NaN result open; the reference runs on
+ * x86-64 SSE, where `x op y` returns x's NaN (quieted) if x is a NaN, else
+ * y's NaN (quieted), and the "default NaN" (sign set: 0xFFC00000 /
+ * 0xFFF8000000000000) for an invalid operation on non-NaN operands (inf-inf,
+ * 0*inf).  The first operand is the one written first in op.cpp:
+ * `inout += in` / `inout *= in` (op.cpp:49, 61) and the complex expressions
+ * of op.cpp:289-300.  Every non-NaN result is the plain IEEE result. */
+static inline float qnan_f(float x) { uint32_t u; memcpy(&u, &x, 4); u |= 0x00400000u; memcpy(&x, &u, 4); return x; }
+static inline double qnan_d(double x) { uint64_t u; memcpy(&u, &x, 8); u |= 0x0008000000000000ull; memcpy(&x, &u, 8); return x; }
+static inline float dnan_f(void) { uint32_t u = 0xFFC00000u; float x; memcpy(&x, &u, 4); return x; }
+static inline double dnan_d(void) { uint64_t u = 0xFFF8000000000000ull; double x; memcpy(&x, &u, 8); return x; }
+#define X86_OP(NAME, T, OPER, Q, D)                                          \
+    static inline T NAME(T x, T y)                                           \
+    {                                                                        \
+        T r = x OPER y;                                                      \
+        if (r == r) return r;                                                \
+        if (x != x) return Q(x);                                             \
+        if (y != y) return Q(y);                                             \
+        return D();                                                          \
+    }
+X86_OP(addf, float, +, qnan_f, dnan_f)
+X86_OP(subf, float, -, qnan_f, dnan_f)
+X86_OP(mulf, float, *, qnan_f, dnan_f)
+X86_OP(addd, double, +, qnan_d, dnan_d)
+X86_OP(subd, double, -, qnan_d, dnan_d)
+X86_OP(muld, double, *, qnan_d, dnan_d)
+
 static int do_sum(int k, const void* in, void* inout, int64_t count)
 {
     switch (k) {
 #define X(K, T, UT) case K: IWRAP_ADD(T, UT); return 0;
     INT_KINDS(X)
 #undef X
-    case ORK_F32: LOOP(float, b[i] += a[i]); return 0;
-    case ORK_F64: LOOP(double, b[i] += a[i]); return 0;
+    case ORK_F32: LOOP(float, b[i] = addf(b[i], a[i])); return 0;
+    case ORK_F64: LOOP(double, b[i] = addd(b[i], a[i])); return 0;
     /* complex<T>::operator+= op.cpp:287-292 */
-    case ORK_C32: LOOP(cplx_f, b[i].re += a[i].re; b[i].im += a[i].im); return 0;
-    case ORK_C64: LOOP(cplx_d, b[i].re += a[i].re; b[i].im += a[i].im); return 0;
+    case ORK_C32: LOOP(cplx_f, b[i].re = addf(b[i].re, a[i].re); b[i].im = addf(b[i].im, a[i].im)); return 0;
+    case ORK_C64: LOOP(cplx_d, b[i].re = addd(b[i].re, a[i].re); b[i].im = addd(b[i].im, a[i].im)); return 0;
     default: return MPI_ERR_OP;
     }
 }
 
 /* complex<T>::operator*= op.cpp:294-303:
  *   r = (re * rhs.re) - (im * rhs.im);  i = (re * rhs.im) + (rhs.re * im); */
-#define CMUL(T)                                                              \
+#define CMUL(T, ADD, SUB, MUL)                                               \
     LOOP(T, {                                                                \
-        __typeof__(b[i].re) r = (b[i].re * a[i].re) - (b[i].im * a[i].im);  \
-        __typeof__(b[i].re) m = (b[i].re * a[i].im) + (a[i].re * b[i].im);  \
+        __typeof__(b[i].re) r = SUB(MUL(b[i].re, a[i].re), MUL(b[i].im, a[i].im)); \
+        __typeof__(b[i].re) m = ADD(MUL(b[i].re, a[i].im), MUL(a[i].re, b[i].im)); \
         b[i].re = r; b[i].im = m; })
 
 static int do_prod(int k, const void* in, void* inout, int64_t count)
@@ -240,10 +268,10 @@ static int do_prod(int k, const void* in, void* inout, int64_t count)
 #define X(K, T, UT) case K: IWRAP_MUL(T, UT); return 0;
     INT_KINDS(X)
 #undef X
-    case ORK_F32: LOOP(float, b[i] *= a[i]); return 0;
-    case ORK_F64: LOOP(double, b[i] *= a[i]); return 0;
-    case ORK_C32: CMUL(cplx_f); return 0;
-    case ORK_C64: CMUL(cplx_d); return 0;
+    case ORK_F32: LOOP(float, b[i] = mulf(b[i], a[i])); return 0;
+    case ORK_F64: LOOP(double, b[i] = muld(b[i], a[i])); return 0;
+    case ORK_C32: CMUL(cplx_f, addf, subf, mulf); return 0;
+    case ORK_C64: CMUL(cplx_d, addd, subd, muld); return 0;
     default: return MPI_ERR_OP;
     }
 }

@@ -271,3 +271,27 @@ def test_benchmark_size_fp32_sum_bit_exact(L):
         torch.cuda.synchronize()
         assert torch.equal(c.view(torch.int32), (ref + a).view(torch.int32)), L.msx_tune_variant_name(v)
     assert L.msx_tune_set(0, 0) == 0
+
+
+NAN_CASES_F32 = [0x7FC00001, 0xFFC00002, 0x7FA00003, 0xFF800000, 0x7F800000, 0x3F800000, 0x80000000, 0x00000001]
+
+
+@pytest.mark.parametrize("dt", ["MPI_FLOAT", "MPI_DOUBLE", "MPI_C_FLOAT_COMPLEX", "MPI_C_DOUBLE_COMPLEX"])
+@pytest.mark.parametrize("op", ["MPI_SUM", "MPI_PROD"])
+def test_nan_payload_propagation_matches_reference_cpu(L, dt, op):
+    """Two-NaN / inf-inf / signalling-NaN inputs: every NaN bit pattern must be
+    the one the reference's x86 `inout op= in` produces (inout's NaN first,
+    then in's, quieted; inf-inf = the x86 default NaN)."""
+    if dt in ("MPI_FLOAT", "MPI_C_FLOAT_COMPLEX"):
+        vals = np.array(NAN_CASES_F32, np.uint32).view(np.float32)
+    else:
+        vals = np.array([0x7FF8000000000001, 0xFFF8000000000002, 0x7FF4000000000003, 0xFFF0000000000000,
+                         0x7FF0000000000000, 0x3FF0000000000000, 0x8000000000000000, 1], np.uint64).view(np.float64)
+    a = np.repeat(vals, len(vals))
+    b = np.tile(vals, len(vals))
+    if "COMPLEX" in dt:
+        ct = np.complex64 if vals.dtype == np.float32 else np.complex128
+        ac = np.empty(a.size, ct); ac.real, ac.imag = a, b[::-1]
+        bc = np.empty(b.size, ct); bc.real, bc.imag = b, a[::-1]
+        a, b = ac, bc
+    _check_dev(L, op, dt, a, b)
