@@ -50,7 +50,7 @@ def parse():
     return ap.parse_args()
 
 
-def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 4, 256, true, false>"):
+def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 1, 256, true, false>"):
     """Per-launch HBM bytes of the default fp32 SUM kernel from the newest
     committed rocprofv3 PMC collection (profiles/<round>/pmc_*counter_collection.csv,
     FETCH_SIZE and WRITE_SIZE collected in separate passes)."""
@@ -183,10 +183,22 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
 
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+    # the same K steps without the per-launch event records (launch gaps only)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed_noev = time.perf_counter() - t1
+
+    t = torch.tensor([elapsed, kern_ms, elapsed_noev], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms_max = float(t[0]), float(t[1])
+    elapsed, kern_ms_max, elapsed_noev = float(t[0]), float(t[1]), float(t[2])
 
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
@@ -237,6 +249,8 @@ def main():
                        "elements_per_gpu": n, "bytes_per_operand": n * 4,
                        "parallelism": f"{world} rank(s), one per GPU, independent shards"},
             "payload_GiB_s": round(world * args.steps * n * 4 / elapsed / 2**30, 2),
+            "value_without_event_records": round(total_bytes / elapsed_noev / 2**30, 2),
+            "ms_per_step_without_event_records": round(elapsed_noev / args.steps * 1e3, 4),
             "pct_hbm_peak": round(100 * value * 2**30 / 1e9 / (world * HBM_PEAK_GBS), 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

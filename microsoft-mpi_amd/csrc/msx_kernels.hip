@@ -363,7 +363,7 @@ namespace {
 using namespace dev;
 
 constexpr int kBlock = 256;
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 1;
 
 template <class T>
 inline void split(const void* in, const void* io, size_t count, size_t& head, size_t& nvec,
@@ -400,9 +400,11 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
     return hipGetLastError();
 }
 
-// Default launch of every (op, type): 4 x 16 B per lane per operand, 256-thread
-// workgroups, non-temporal loads (measured on MI355X: 6.9 TB/s vs 5.5 TB/s
-// with default-policy loads for the 256 MiB fp32 SUM, profiles/r01).
+// Default launch of every (op, type): one 16-B vector per lane per operand,
+// 256-thread workgroups (one-shot grid, 65536 workgroups at 256 MiB fp32),
+// non-temporal loads.  Measured on MI355X for the 256 MiB fp32 SUM
+// (profiles/r01/bench_sweep.log): 7.05 TB/s vs 6.8 TB/s at 4 vectors per lane
+// and 5.5 TB/s with default-policy loads.
 template <int OP, class T>
 hipError_t run_default(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
 {
@@ -422,18 +424,16 @@ struct Variant {
     hipError_t (*fn)(const void*, void*, size_t, hipStream_t, const LaunchCfg&);
 };
 const Variant kF32SumVariants[] = {
-    {"u4_b256_ntld", run_combine<O_SUM, float, float, 4, 256, true, false>},
-    {"u2_b256_ntld", run_combine<O_SUM, float, float, 2, 256, true, false>},
-    {"u8_b256_ntld", run_combine<O_SUM, float, float, 8, 256, true, false>},
-    {"u4_b512_ntld", run_combine<O_SUM, float, float, 4, 512, true, false>},
-    {"u2_b512_ntld", run_combine<O_SUM, float, float, 2, 512, true, false>},
-    {"u4_b128_ntld", run_combine<O_SUM, float, float, 4, 128, true, false>},
-    {"u8_b128_ntld", run_combine<O_SUM, float, float, 8, 128, true, false>},
     {"u1_b256_ntld", run_combine<O_SUM, float, float, 1, 256, true, false>},
-    {"u2_b1024_ntld", run_combine<O_SUM, float, float, 2, 1024, true, false>},
-    {"u16_b256_ntld", run_combine<O_SUM, float, float, 16, 256, true, false>},
-    {"u4_b256_ntall", run_combine<O_SUM, float, float, 4, 256, true, true>},
-    {"u4_b256_plain", run_combine<O_SUM, float, float, 4, 256, false, false>},
+    {"u1_b128_ntld", run_combine<O_SUM, float, float, 1, 128, true, false>},
+    {"u1_b512_ntld", run_combine<O_SUM, float, float, 1, 512, true, false>},
+    {"u1_b1024_ntld", run_combine<O_SUM, float, float, 1, 1024, true, false>},
+    {"u2_b256_ntld", run_combine<O_SUM, float, float, 2, 256, true, false>},
+    {"u2_b128_ntld", run_combine<O_SUM, float, float, 2, 128, true, false>},
+    {"u4_b256_ntld", run_combine<O_SUM, float, float, 4, 256, true, false>},
+    {"u1_b64_ntld", run_combine<O_SUM, float, float, 1, 64, true, false>},
+    {"u1_b256_ntall", run_combine<O_SUM, float, float, 1, 256, true, true>},
+    {"u1_b256_plain", run_combine<O_SUM, float, float, 1, 256, false, false>},
 };
 constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
 
