@@ -109,6 +109,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
+    # one rank per GPU; ranks beyond the visible GPUs share them round-robin
+    # (lets the N>1 path run on a one-GPU box too)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
