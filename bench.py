@@ -47,7 +47,36 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--elems", type=int, default=N_ELEM)
+    ap.add_argument("--no-collectives", action="store_true",
+                    help="skip the N>1 collective configs (c3-c5, bench_collectives.py)")
+    ap.add_argument("--coll-scale", type=float, default=1.0, help="size factor for c3-c5")
     return ap.parse_args()
+
+
+def run_collectives_child(world, rank, local, scale):
+    """c3-c5 in a child MPI process per rank (isolated from the headline line)."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"msx_coll_{os.environ.get('MASTER_PORT', '0')}.json")
+    env = dict(os.environ)
+    env.update({"MSX_SIZE": str(world), "MSX_RANK": str(rank), "MSX_DEVICE": str(local),
+                "MSX_BOOTSTRAP_ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                "MSX_BOOTSTRAP_PORT": str((int(os.environ.get("MASTER_PORT", "29500")) + 113) % 65536),
+                "MSX_BOOTSTRAP_TIMEOUT": "90"})
+    try:
+        pr = subprocess.run([sys.executable, os.path.join(REPO, "bench_collectives.py"), out, str(scale)],
+                            env=env, capture_output=True, text=True, timeout=420)
+        if pr.returncode != 0:
+            return {"error": f"rank {rank} child rc={pr.returncode}: {pr.stderr[-600:]}"}
+    except subprocess.TimeoutExpired:
+        return {"error": f"rank {rank} child timed out"}
+    if rank == 0:
+        try:
+            with open(out) as f:
+                return json.load(f)
+        except OSError as e:
+            return {"error": str(e)}
+    return {}
 
 
 def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 1, 256, true, false>"):
@@ -193,6 +222,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms_max = float(t[0]), float(t[1])
 
+    # N > 1: the collective configs c3-c5 in child MPI processes (not part of
+    # `value`); each rank reports whether its child succeeded.
+    coll = None
+    if world > 1 and not args.no_collectives:
+        mine = run_collectives_child(world, rank, local, args.coll_scale)
+        ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        coll = mine if rank == 0 else None
+        if rank == 0 and not ok.item() and "error" not in coll:
+            coll["error"] = "a non-zero rank's child failed"
+
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
     host = None
@@ -253,6 +293,8 @@ def main():
         }
         if host is not None:
             out["host_path"] = host
+        if coll is not None:
+            out["collectives"] = coll
         if sweep:
             out["variant_sweep_GB_s"] = sweep
         if world == 1:

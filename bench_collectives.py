@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""bench_collectives.py — the multi-rank configs of BASELINE.json, run by
+bench.py at N > 1 as one child process per rank (so a failure here can never
+take the headline local-reduce line down with it).
+
+  c3  MPI_Allreduce      MPI_SUM  MPI_FLOAT     1 GiB per rank
+  c4  MPI_Reduce_scatter MPI_MAX  MPI_DOUBLE    4 GiB sendbuf per rank, recvcount = total/p
+  c5  MPI_Iallreduce     MPI_BAND MPI_UINT64_T  512 MiB, overlapped with a host compute loop
+
+Each rank is an MPI process of libmsmpi_mi355x.so (MSX_SIZE/MSX_RANK/MSX_DEVICE
+set by the parent).  Inputs are integer-valued patterns whose reductions are
+exact in any order, so every result is checked in full on the GPU against a
+closed form.  busBW = (S/t)·2(p−1)/p for allreduce, (S/t)·(p−1)/p for
+reduce_scatter (S = bytes per rank).  Rank 0 writes one JSON object to the
+path in argv[1].
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
+
+
+def main(out_path, scale):
+    import torch
+    import msx
+
+    L = msx.init(errors_return=True)
+    C = msx.C
+    r_, s_ = ctypes.c_int(), ctypes.c_int()
+    L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r_))
+    L.MPI_Comm_size(C.MPI_COMM_WORLD, ctypes.byref(s_))
+    rank, p = r_.value, s_.value
+    dev = torch.device("cuda", int(os.environ.get("MSX_DEVICE", "0")))
+    torch.cuda.set_device(dev)
+    res = {"ranks": p}
+
+    def barrier():
+        L.MPI_Barrier(C.MPI_COMM_WORLD)
+
+    # ---- c3: allreduce SUM fp32, 1 GiB per rank ------------------------------
+    n = int((256 << 20) * scale)
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    send = (((i * 7 + rank * 13) % 17) - 8).to(torch.float32)
+    recv = torch.empty_like(send)
+    exp = torch.zeros(n, device=dev, dtype=torch.float32)
+    for r in range(p):
+        exp += (((i * 7 + r * 13) % 17) - 8).to(torch.float32)
+    del i
+    torch.cuda.synchronize()
+    times = []
+    for it in range(4):
+        barrier()
+        t0 = time.perf_counter()
+        rc = L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+        times.append(time.perf_counter() - t0)
+        if rc:
+            res["c3_error"] = f"rc={rc} {msx.last_error()}"
+            break
+    if "c3_error" not in res:
+        t = sorted(times[1:])[len(times[1:]) // 2]
+        S = n * 4
+        res["c3_allreduce_sum_f32"] = {
+            "bytes_per_rank": S, "seconds": round(t, 5), "algbw_GB_s": round(S / t / 1e9, 2),
+            "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 2),
+            "correct": bool(torch.equal(recv, exp))}
+    del send, recv, exp
+    torch.cuda.empty_cache()
+
+    # ---- c4: reduce_scatter MAX fp64, 4 GiB per rank sendbuf ----------------
+    per = int((512 << 20) * scale) // p                  # recvcount per rank (c4: 2^29 / p)
+    tot = per * p
+    i = torch.arange(tot, device=dev, dtype=torch.int64)
+    send = ((i * 2654435761 + rank * 40503) % 1000003).to(torch.float64)
+    recv = torch.empty(per, device=dev, dtype=torch.float64)
+    counts = (ctypes.c_int * p)(*([per] * p))
+    lo, hi = rank * per, (rank + 1) * per
+    ii = i[lo:hi]
+    exp = torch.full((per,), -1.0, device=dev, dtype=torch.float64)
+    for r in range(p):
+        exp = torch.maximum(exp, ((ii * 2654435761 + r * 40503) % 1000003).to(torch.float64))
+    del i, ii
+    torch.cuda.synchronize()
+    times = []
+    for it in range(3):
+        barrier()
+        t0 = time.perf_counter()
+        rc = L.MPI_Reduce_scatter(send.data_ptr(), recv.data_ptr(), counts, C.MPI_DOUBLE, C.MPI_MAX,
+                                  C.MPI_COMM_WORLD)
+        times.append(time.perf_counter() - t0)
+        if rc:
+            res["c4_error"] = f"rc={rc} {msx.last_error()}"
+            break
+    if "c4_error" not in res:
+        t = sorted(times[1:])[len(times[1:]) // 2]
+        S = tot * 8
+        res["c4_reduce_scatter_max_f64"] = {
+            "bytes_per_rank": S, "seconds": round(t, 5), "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 2),
+            "correct": bool(torch.equal(recv, exp))}
+    del send, recv, exp
+    torch.cuda.empty_cache()
+
+    # ---- c5: iallreduce BAND u64, 512 MiB, overlapped with host compute ------
+    n = int((64 << 20) * scale)
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    one = torch.ones((), dtype=torch.int64, device=dev)
+    send = ~torch.bitwise_left_shift(one, (i + rank) % 64)          # all bits but one
+    exp = torch.full((n,), -1, device=dev, dtype=torch.int64)
+    for r in range(p):
+        exp &= ~torch.bitwise_left_shift(one, (i + r) % 64)
+    del i
+    recv = torch.empty_like(send)
+    import numpy as np
+    host = np.random.default_rng(rank).random(1 << 22)
+
+    def host_work(k):
+        x = host
+        for _ in range(k):
+            x = x * 1.000001 + 0.5
+        return x
+
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    rc = L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD)
+    t_comm = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    host_work(20)
+    t_host = time.perf_counter() - t0
+    barrier()
+    req = ctypes.c_int()
+    t0 = time.perf_counter()
+    rc2 = L.MPI_Iallreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD,
+                           ctypes.byref(req))
+    host_work(20)
+    rc3 = L.MPI_Wait(ctypes.byref(req), None)
+    t_total = time.perf_counter() - t0
+    if rc or rc2 or rc3:
+        res["c5_error"] = f"rc={rc},{rc2},{rc3} {msx.last_error()}"
+    else:
+        S = n * 8
+        res["c5_iallreduce_band_u64"] = {
+            "bytes_per_rank": S, "t_comm_s": round(t_comm, 5), "t_host_s": round(t_host, 5),
+            "t_overlapped_s": round(t_total, 5),
+            "busbw_GB_s": round(S / t_comm / 1e9 * 2 * (p - 1) / p, 2),
+            "overlap_efficiency": round((t_comm + t_host - t_total) / min(t_comm, t_host), 3),
+            "correct": bool(torch.equal(recv, exp))}
+    barrier()
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    L.MPI_Finalize()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 1.0)
