@@ -62,14 +62,16 @@ def run_collectives_child(world, rank, local, scale):
     env.update({"MSX_SIZE": str(world), "MSX_RANK": str(rank), "MSX_DEVICE": str(local),
                 "MSX_BOOTSTRAP_ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
                 "MSX_BOOTSTRAP_PORT": str((int(os.environ.get("MASTER_PORT", "29500")) + 113) % 65536),
-                "MSX_BOOTSTRAP_TIMEOUT": "90"})
+                "MSX_BOOTSTRAP_TIMEOUT": "90",
+                "MSX_BENCH_LOG": os.environ.get("MSX_BENCH_LOG", os.devnull)})
     try:
         pr = subprocess.run([sys.executable, os.path.join(REPO, "bench_collectives.py"), out, str(scale)],
-                            env=env, capture_output=True, text=True, timeout=420)
+                            env=env, capture_output=True, text=True,
+                            timeout=float(os.environ.get("MSX_COLL_TIMEOUT", "420")))
         if pr.returncode != 0:
             return {"error": f"rank {rank} child rc={pr.returncode}: {pr.stderr[-600:]}"}
-    except subprocess.TimeoutExpired:
-        return {"error": f"rank {rank} child timed out"}
+    except subprocess.TimeoutExpired as e:
+        return {"error": f"rank {rank} child timed out: {str(e.stderr)[-600:] if e.stderr else ''}"}
     if rank == 0:
         try:
             with open(out) as f:

@@ -37,6 +37,13 @@ def main(out_path, scale):
     dev = torch.device("cuda", int(os.environ.get("MSX_DEVICE", "0")))
     torch.cuda.set_device(dev)
     res = {"ranks": p}
+    logf = open(os.environ.get("MSX_BENCH_LOG", os.devnull), "a")
+
+    def log(msg):
+        logf.write(f"[{time.strftime('%H:%M:%S')}] rank {rank}: {msg}\n")
+        logf.flush()
+
+    log(f"init ok p={p} scale={scale}")
 
     def barrier():
         L.MPI_Barrier(C.MPI_COMM_WORLD)
@@ -51,12 +58,14 @@ def main(out_path, scale):
         exp += (((i * 7 + r * 13) % 17) - 8).to(torch.float32)
     del i
     torch.cuda.synchronize()
+    log("c3 data ready")
     times = []
     for it in range(4):
         barrier()
         t0 = time.perf_counter()
         rc = L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
         times.append(time.perf_counter() - t0)
+        log(f"c3 iter {it} rc={rc} {times[-1]:.4f}s")
         if rc:
             res["c3_error"] = f"rc={rc} {msx.last_error()}"
             break
@@ -91,6 +100,7 @@ def main(out_path, scale):
         rc = L.MPI_Reduce_scatter(send.data_ptr(), recv.data_ptr(), counts, C.MPI_DOUBLE, C.MPI_MAX,
                                   C.MPI_COMM_WORLD)
         times.append(time.perf_counter() - t0)
+        log(f"c4 iter {it} rc={rc} {times[-1]:.4f}s")
         if rc:
             res["c4_error"] = f"rc={rc} {msx.last_error()}"
             break
@@ -123,13 +133,19 @@ def main(out_path, scale):
         return x
 
     torch.cuda.synchronize()
-    barrier()
-    t0 = time.perf_counter()
-    rc = L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD)
-    t_comm = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    host_work(20)
-    t_host = time.perf_counter() - t0
+    host_work(20)                                   # warm the host loop (page-in)
+    rc = 0
+    t_comm = 1e30
+    for _ in range(2):
+        barrier()
+        t0 = time.perf_counter()
+        rc |= L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD)
+        t_comm = min(t_comm, time.perf_counter() - t0)
+    t_host = 1e30
+    for _ in range(2):
+        t0 = time.perf_counter()
+        host_work(20)
+        t_host = min(t_host, time.perf_counter() - t0)
     barrier()
     req = ctypes.c_int()
     t0 = time.perf_counter()
@@ -138,6 +154,7 @@ def main(out_path, scale):
     host_work(20)
     rc3 = L.MPI_Wait(ctypes.byref(req), None)
     t_total = time.perf_counter() - t0
+    log(f"c5 done rc={rc},{rc2},{rc3} comm={t_comm:.4f} host={t_host:.4f} total={t_total:.4f}")
     if rc or rc2 or rc3:
         res["c5_error"] = f"rc={rc},{rc2},{rc3} {msx.last_error()}"
     else:

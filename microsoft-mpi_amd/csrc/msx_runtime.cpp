@@ -11,6 +11,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
+#include <unistd.h>
 
 namespace msx {
 
@@ -51,6 +53,21 @@ void set_error(const char* fmt, ...)
 }
 
 const char* last_error() { return g_err; }
+
+void trace(const char* fmt, ...)
+{
+    static const bool on = getenv("MSX_TRACE") && atoi(getenv("MSX_TRACE")) > 0;
+    if (!on) return;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[msx %ld.%06ld pid %d] %s\n", (long)ts.tv_sec, ts.tv_nsec / 1000, (int)getpid(), buf);
+    fflush(stderr);
+}
 
 int hip_fail(hipError_t e, const char* what)
 {

@@ -20,6 +20,9 @@ struct BufInfo {
     int device = -1;
 };
 
+// MSX_TRACE=1: timestamped engine trace on stderr
+void trace(const char* fmt, ...);
+
 // thread-local error text (msx_last_error)
 void set_error(const char* fmt, ...);
 const char* last_error();

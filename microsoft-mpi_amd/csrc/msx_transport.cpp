@@ -626,7 +626,9 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
 
     // Exchange: every rank's input (this allgather is also the entry barrier).
     std::vector<char*> pin, pout;
+    trace("allreduce: count=%zu esz=%zu algo=%d map inputs", count, esz, algo);
     if ((rc = tp->map_peers(dev_in, pin)) != MPI_SUCCESS) return rc;
+    trace("allreduce: inputs mapped");
 
     const int n = newrank_of(me, p);
     if (algo == A_RECURSIVE_DOUBLING) {
@@ -646,6 +648,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // Rabenseifner: newrank n owns block bitrev(n); evaluate it in place,
         // then pull every other block from its owner.
         if ((rc = tp->map_peers(dev_out, pout)) != MPI_SUCCESS) return rc;
+        trace("allreduce: outputs mapped");
         const int pof2 = pof2_floor(p);
         if (n >= 0) {
             const int j = allreduce_block_of_newrank(p, n);
@@ -653,9 +656,12 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             allreduce_block(p, count, j, &st, &ln);
             RankTree t = tree_allreduce(p, n);
             rc = run_rank_tree(op.opidx, k, t, pin, esz, st, ln, dev_out + st * esz, s);
+            trace("allreduce: block %d launched (%zu elems)", j, ln);
             if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce reduce-scatter");
+            trace("allreduce: block done rc=%d", rc);
         }
         if (rc == MPI_SUCCESS) rc = tp->barrier();   // every block reduced
+        trace("allreduce: barrier 2 rc=%d", rc);
         if (rc != MPI_SUCCESS) return rc;
         std::vector<const void*> srcs;
         std::vector<void*> dsts;
@@ -672,7 +678,9 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         hipError_t e = launch_copy_segs(srcs.data(), dsts.data(), nbs.data(), (int)srcs.size(), true, s);
         if (e != hipSuccess) return hip_fail(e, "allreduce allgather");
     }
+    trace("allreduce: gather launched");
     if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce");
+    trace("allreduce: gather done rc=%d", rc);
     if (rc == MPI_SUCCESS) rc = tp->barrier();   // nobody reads our buffers any more
     if (rc == MPI_SUCCESS && need_stage_out) {
         hipError_t e = hipMemcpyAsync(recvbuf, dev_out, bytes, hipMemcpyDefault, s);
