@@ -225,7 +225,9 @@ public:
         void* base = nullptr;
         size_t asz = 0;
         hipError_t e = hipMemGetAddressRange(&base, &asz, const_cast<void*>(ptr));
+        trace("map_peers: ptr=%p base=%p size=%zu rc=%d", ptr, base, asz, (int)e);
         if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, base);
+        trace("map_peers: handle rc=%d", (int)e);
         if (e == hipSuccess) {
             mine.ok = 1;
             mine.offset = (uint64_t)((const char*)ptr - (const char*)base);
@@ -235,6 +237,7 @@ public:
         }
         std::vector<IpcRec> all((size_t)size);
         int rc = hub_.allgather(&mine, sizeof(mine), all.data());
+        trace("map_peers: exchanged rc=%d", rc);
         if (rc != MPI_SUCCESS) return rc;
         out.assign((size_t)size, nullptr);
         for (int r = 0; r < size; ++r) {
@@ -250,6 +253,7 @@ public:
                 pbase = it->second;
             } else {
                 e = hipIpcOpenMemHandle(&pbase, all[r].h, hipIpcMemLazyEnablePeerAccess);
+                trace("map_peers: opened rank %d handle -> %p rc=%d", r, pbase, (int)e);
                 if (e != hipSuccess) return hip_fail(e, "hipIpcOpenMemHandle");
                 opened_[key] = pbase;
             }
