@@ -14,6 +14,7 @@
 
 #include <arpa/inet.h>
 #include <condition_variable>
+#include <algorithm>
 #include <deque>
 #include <errno.h>
 #include <functional>
@@ -508,13 +509,6 @@ int sync_stream(hipStream_t s, const char* what)
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
 }
 
-// A device-resident view of a user buffer: the buffer itself if it is in
-// HBM, else a staging slice of the window.
-struct DevView {
-    char* dev = nullptr;
-    bool staged = false;
-};
-
 // Evaluate RankTree `t` over [start, start+len) elements of the per-rank
 // source pointers `srcs` into `out`.
 int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>& srcs, size_t esz,
@@ -581,8 +575,70 @@ int host_user_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t coun
     return copy_any(recvbuf, v[src].data(), bytes);
 }
 
+// Engine-private device scratch (grows, never shrinks; engine worker only).
+char* dev_scratch(size_t bytes)
+{
+    static char* p = nullptr;
+    static size_t cap = 0;
+    if (bytes > cap) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&p), bytes) != hipSuccess) return nullptr;
+        cap = bytes;
+    }
+    return p;
+}
+
+// ---- window-staged collectives ---------------------------------------------
+// Every rank owns one IPC-mapped device window of 4*C bytes: two slots, each an
+// IN half (this rank's staged input chunk) and an OUT half (this rank's
+// reduced part).  User buffers are never IPC-mapped (ROCm 7.2 hangs opening
+// handles of allocations > 2 GiB, and user memory may be host memory), so a
+// collective streams chunks of C bytes through the windows:
+//   stage  : my chunk of input -> IN(me, s)            (HBM copy / H2D)
+//   barrier A (every input chunk staged)
+//   reduce : my part of the chunk, reading IN(r, s) of every rank over xGMI,
+//            the reference's expression tree per element -> OUT(me, s)
+//   barrier B (every part reduced)            [allreduce only]
+//   gather : every rank's part OUT(r, s) -> my recvbuf  [allreduce only]
+// Slot s alternates; a rank syncs its stream before the next barrier, so a
+// slot is never rewritten while a peer still reads it.
+size_t chunk_bytes()
+{
+    static size_t c = [] {
+        size_t v = (size_t)256 << 20;
+        if (const char* e = getenv("MSX_CHUNK_BYTES")) v = (size_t)atoll(e);
+        if (v < ((size_t)1 << 16)) v = (size_t)1 << 16;
+        if (v > ((size_t)480 << 20)) v = (size_t)480 << 20;   // window 4*C < 2 GiB
+        return v & ~(size_t)4095;
+    }();
+    return c;
+}
+
+struct Windows {
+    std::vector<char*> base;
+    size_t C = 0;
+    char* in(int r, int s) const { return base[(size_t)r] + (size_t)s * 2 * C; }
+    char* out(int r, int s) const { return base[(size_t)r] + (size_t)s * 2 * C + C; }
+};
+
+int get_windows(Transport* tp, Windows* w)
+{
+    w->C = chunk_bytes();
+    return tp->window(4 * w->C, w->base);
+}
+
+int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
+{
+    if (!bytes) return MPI_SUCCESS;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s);
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "stage copy");
+}
+
+// root < 0: allreduce; root >= 0: only `root` gathers the result (MPI_Reduce).
 int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                 const OpRef& op)
+                 const OpRef& op, int root = -1)
 {
     // user functions are host code: no GPU needed on this path
     if (op.opidx == O_NULL) return host_user_allreduce(c, sendbuf, recvbuf, count, dt, op);
@@ -593,177 +649,166 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     const int p = c->size, me = c->rank;
     const TypeInfo* ti = type_info(dt);
     const Kind k = ti->kind;
-    const size_t esz = (size_t)ti->size, bytes = count * esz;
+    const size_t esz = (size_t)ti->size;
     hipStream_t s = tp->stream();
-    const void* src = (sendbuf == MPI_IN_PLACE) ? recvbuf : sendbuf;
-    const bool in_place = (sendbuf == MPI_IN_PLACE);
-    const BufInfo bsrc = classify(src), bdst = classify(recvbuf);
+    const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
+    char* dst = static_cast<char*>(recvbuf);
+    const bool want = (root < 0 || root == me);          // this rank receives the result
     const int algo = allreduce_algo(p, count, (int)esz, true);
-
-    // Window layout: [0, bytes) staged input, [bytes, 2*bytes) result/temp.
-    // Every rank decides identically whether it needs the window? No: staging
-    // is per-rank, so the window is sized collectively for the worst case.
-    const bool need_stage_in = bsrc.place != Place::Device;
-    const bool need_stage_out = bdst.place != Place::Device;
-    // Recursive doubling reads every peer's whole input, so an in-place result
-    // goes to a temporary until the closing barrier.
-    const bool need_temp = (algo == A_RECURSIVE_DOUBLING) && in_place;
-    uint8_t need = (uint8_t)(need_stage_in || need_stage_out || need_temp);
-    std::vector<uint8_t> needs((size_t)p);
-    rc = tp->allgather(&need, 1, needs.data());
-    if (rc != MPI_SUCCESS) return rc;
-    bool any_window = false;
-    for (uint8_t v : needs) any_window = any_window || v;
-    std::vector<char*> win;
-    if (any_window) {
-        rc = tp->window(2 * bytes, win);   // [0,bytes) input, [bytes,2*bytes) result
-        if (rc != MPI_SUCCESS) return rc;
-    }
-    char* dev_in = need_stage_in ? win[me] : static_cast<char*>(bsrc.dev);
-    char* dev_out = need_stage_out ? win[me] + bytes : static_cast<char*>(bdst.dev);
-    if (in_place) dev_out = dev_in;
-    if (need_stage_in) {
-        hipError_t e = hipMemcpyAsync(dev_in, src, bytes, hipMemcpyDefault, s);
-        if (e != hipSuccess) return hip_fail(e, "stage in");
-        if ((rc = sync_stream(s, "stage in")) != MPI_SUCCESS) return rc;
-    }
-
-    // Exchange: every rank's input (this allgather is also the entry barrier).
-    std::vector<char*> pin, pout;
-    trace("allreduce: count=%zu esz=%zu algo=%d map inputs", count, esz, algo);
-    if ((rc = tp->map_peers(dev_in, pin)) != MPI_SUCCESS) return rc;
-    trace("allreduce: inputs mapped");
-
+    Windows w;
+    if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
+    // chunk = whole 16-byte vectors of whole elements
+    size_t ce = w.C / esz;
+    ce -= ce % (16 / (esz < 16 ? esz : 16) ? 16 / (esz < 16 ? esz : 16) : 1);
+    const int pof2 = pof2_floor(p);
     const int n = newrank_of(me, p);
-    if (algo == A_RECURSIVE_DOUBLING) {
-        // Every rank evaluates its own lineage's tree over the whole vector
-        // (folded even ranks receive their odd partner's result, :4071-4092).
-        const int nn = n >= 0 ? n : newrank_of(me + 1, p);
-        RankTree t = tree_allreduce(p, nn);
-        char* out = (dev_out == dev_in) ? win[me] + bytes : dev_out;
-        rc = run_rank_tree(op.opidx, k, t, pin, esz, 0, count, out, s);
-        if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce combine");
-        if (rc == MPI_SUCCESS) rc = tp->barrier();   // everyone has read the inputs
-        if (rc == MPI_SUCCESS && out != dev_out) {
-            hipError_t e = hipMemcpyAsync(dev_out, out, bytes, hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) return hip_fail(e, "allreduce result copy");
+    const int lineage = n >= 0 ? n : newrank_of(me + 1, p);
+    trace("allreduce: count=%zu esz=%zu algo=%d chunk=%zu elems", count, esz, algo, ce);
+
+    std::vector<char*> ins((size_t)p), outs((size_t)p);
+    int slot = 0;
+    for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce, slot ^= 1) {
+        const size_t len = (count - o < ce) ? count - o : ce;
+        for (int r = 0; r < p; ++r) { ins[r] = w.in(r, slot); outs[r] = w.out(r, slot); }
+        if ((rc = copy_async(ins[me], src + o * esz, len * esz, s)) != MPI_SUCCESS) break;
+        if ((rc = sync_stream(s, "allreduce stage")) != MPI_SUCCESS) break;
+        if ((rc = tp->barrier()) != MPI_SUCCESS) break;                  // A
+        if (algo == A_RECURSIVE_DOUBLING) {
+            // every rank evaluates its own lineage's tree on the whole chunk
+            RankTree t = tree_allreduce(p, lineage);
+            if (want) rc = run_rank_tree(op.opidx, k, t, ins, esz, 0, len, outs[me], s);
+            if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, outs[me], len * esz, s);
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce chunk");
+            continue;
         }
-    } else {
-        // Rabenseifner: newrank n owns block bitrev(n); evaluate it in place,
-        // then pull every other block from its owner.
-        if ((rc = tp->map_peers(dev_out, pout)) != MPI_SUCCESS) return rc;
-        trace("allreduce: outputs mapped");
-        const int pof2 = pof2_floor(p);
-        if (n >= 0) {
-            const int j = allreduce_block_of_newrank(p, n);
-            size_t st, ln;
-            allreduce_block(p, count, j, &st, &ln);
-            RankTree t = tree_allreduce(p, n);
-            rc = run_rank_tree(op.opidx, k, t, pin, esz, st, ln, dev_out + st * esz, s);
-            trace("allreduce: block %d launched (%zu elems)", j, ln);
-            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce reduce-scatter");
-            trace("allreduce: block done rc=%d", rc);
+        // Rabenseifner order: element e of the vector belongs to block j(e),
+        // whose value the reference computes at newrank bitrev(j).  The chunk
+        // is split evenly over all p ranks (work balance only); each piece is
+        // evaluated with the tree of its block's owner.
+        const size_t q = (len + p - 1) / p;
+        const size_t qv = (q + 15) & ~(size_t)15;                        // 16-element granules
+        const size_t plo = std::min(len, (size_t)me * qv), phi = std::min(len, plo + qv);
+        for (size_t e0 = plo; e0 < phi && rc == MPI_SUCCESS;) {
+            const size_t ge = o + e0;                                    // global element
+            const size_t rs = count / (size_t)pof2;
+            int j = rs ? (int)std::min((size_t)pof2 - 1, ge / rs) : pof2 - 1;
+            size_t bs, bl;
+            allreduce_block(p, count, j, &bs, &bl);
+            const size_t e1 = std::min(phi, bs + bl - o);
+            RankTree t = tree_allreduce(p, allreduce_block_owner(p, j));
+            rc = run_rank_tree(op.opidx, k, t, ins, esz, e0, e1 - e0, outs[me] + e0 * esz, s);
+            e0 = e1;
         }
-        if (rc == MPI_SUCCESS) rc = tp->barrier();   // every block reduced
-        trace("allreduce: barrier 2 rc=%d", rc);
-        if (rc != MPI_SUCCESS) return rc;
-        std::vector<const void*> srcs;
-        std::vector<void*> dsts;
-        std::vector<size_t> nbs;
-        for (int j = 0; j < pof2; ++j) {
-            const int owner = real_of_newrank(allreduce_block_owner(p, j), p);
-            if (owner == me) continue;
-            size_t st, ln;
-            allreduce_block(p, count, j, &st, &ln);
-            srcs.push_back(pout[owner] + st * esz);
-            dsts.push_back(dev_out + st * esz);
-            nbs.push_back(ln * esz);
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce reduce");
+        if (rc == MPI_SUCCESS) rc = tp->barrier();                       // B
+        if (rc != MPI_SUCCESS) break;
+        if (!want) continue;
+        // gather every part (peer OUT windows over xGMI) into recvbuf
+        const BufInfo bd = classify(dst);
+        char* gdst = (bd.place == Place::Device) ? static_cast<char*>(bd.dev) + o * esz : ins[me];
+        std::vector<const void*> gs;
+        std::vector<void*> gd;
+        std::vector<size_t> gn;
+        for (int r = 0; r < p; ++r) {
+            const size_t lo = std::min(len, (size_t)r * qv), hi = std::min(len, lo + qv);
+            if (hi <= lo) continue;
+            gs.push_back(outs[r] + lo * esz);
+            gd.push_back(gdst + lo * esz);
+            gn.push_back((hi - lo) * esz);
         }
-        hipError_t e = launch_copy_segs(srcs.data(), dsts.data(), nbs.data(), (int)srcs.size(), true, s);
-        if (e != hipSuccess) return hip_fail(e, "allreduce allgather");
+        hipError_t e = launch_copy_segs(gs.data(), gd.data(), gn.data(), (int)gs.size(), true, s);
+        if (e != hipSuccess) { rc = hip_fail(e, "allreduce gather"); break; }
+        if (bd.place != Place::Device) rc = copy_async(dst + o * esz, gdst, len * esz, s);
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce gather");
     }
-    trace("allreduce: gather launched");
-    if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce");
-    trace("allreduce: gather done rc=%d", rc);
-    if (rc == MPI_SUCCESS) rc = tp->barrier();   // nobody reads our buffers any more
-    if (rc == MPI_SUCCESS && need_stage_out) {
-        hipError_t e = hipMemcpyAsync(recvbuf, dev_out, bytes, hipMemcpyDefault, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hip_fail(e, "stage out");
-    }
+    if (rc == MPI_SUCCESS) rc = tp->barrier();   // windows free for the next collective
+    trace("allreduce: done rc=%d", rc);
     return rc;
 }
 
 int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
                       MPI_Datatype dt, const OpRef& op)
 {
-    int rc = ensure_device();
-    if (rc != MPI_SUCCESS) return rc;
     Transport* tp = c->tp;
     const int p = c->size, me = c->rank;
-    const int esz_i = type_size(dt);
-    const size_t esz = (size_t)esz_i;
+    const size_t esz = (size_t)type_size(dt);
     std::vector<size_t> disp((size_t)p + 1, 0);
-    for (int r = 0; r < p; ++r) disp[r + 1] = disp[r] + (size_t)recvcounts[r];
+    size_t maxcnt = 0;
+    for (int r = 0; r < p; ++r) {
+        disp[r + 1] = disp[r] + (size_t)recvcounts[r];
+        maxcnt = std::max(maxcnt, (size_t)recvcounts[r]);
+    }
     const size_t total = disp[p];
     if (total == 0) return MPI_SUCCESS;
-    const size_t bytes = total * esz;
     const bool in_place = (sendbuf == MPI_IN_PLACE);
-    const void* src = in_place ? recvbuf : sendbuf;
+    const char* src = static_cast<const char*>(in_place ? recvbuf : sendbuf);
 
     if (op.opidx == O_NULL) {
-        // user op: full allreduce on host, keep our block.
-        std::vector<char> full(bytes);
-        rc = copy_any(full.data(), src, bytes);
-        if (rc == MPI_SUCCESS) rc = host_user_allreduce(c, full.data(), full.data() + 0, total, dt, op);
+        // user op: full allreduce on host, keep our block
+        std::vector<char> full(total * esz), res(total * esz);
+        int rc = copy_any(full.data(), src, total * esz);
+        if (rc == MPI_SUCCESS) rc = host_user_allreduce(c, full.data(), res.data(), total, dt, op);
         if (rc == MPI_SUCCESS && recvcounts[me])
-            rc = copy_any(recvbuf, full.data() + disp[me] * esz, (size_t)recvcounts[me] * esz);
+            rc = copy_any(recvbuf, res.data() + disp[me] * esz, (size_t)recvcounts[me] * esz);
         return rc;
     }
-
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
     const Kind k = type_info(dt)->kind;
     hipStream_t s = tp->stream();
-    const BufInfo bsrc = classify(src), bdst = classify(recvbuf);
-    const bool mine_stage_in = bsrc.place != Place::Device;
-    const bool mine_stage_out = recvcounts[me] > 0 && bdst.place != Place::Device;
-    // In place, our own block's result overwrites input that others read, so
-    // it is produced into the window and copied after the closing barrier.
-    const bool mine_temp = in_place && recvcounts[me] > 0;
-    uint8_t need = (uint8_t)(mine_stage_in || mine_stage_out || mine_temp);
-    std::vector<uint8_t> needs((size_t)p);
-    if ((rc = tp->allgather(&need, 1, needs.data())) != MPI_SUCCESS) return rc;
-    bool any = false;
-    for (uint8_t v : needs) any = any || v;
-    std::vector<char*> win;
-    if (any && (rc = tp->window(2 * bytes, win)) != MPI_SUCCESS) return rc;
-
-    char* dev_in = mine_stage_in ? win[me] : static_cast<char*>(bsrc.dev);
-    if (mine_stage_in) {
-        hipError_t e = hipMemcpyAsync(dev_in, src, bytes, hipMemcpyDefault, s);
-        if (e != hipSuccess) return hip_fail(e, "stage in");
-        if ((rc = sync_stream(s, "stage in")) != MPI_SUCCESS) return rc;
-    }
-    std::vector<char*> pin;
-    if ((rc = tp->map_peers(dev_in, pin)) != MPI_SUCCESS) return rc;
-
-    const int algo = reduce_scatter_algo(p, total, esz_i, op.commutative);
+    Windows w;
+    if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
+    // IN slot holds p sub-chunks of `ce` elements, one per destination rank
+    size_t ce = w.C / esz / (size_t)p;
+    ce -= ce % 16;
+    if (ce == 0) ce = 1;
+    const int algo = reduce_scatter_algo(p, total, (int)esz, op.commutative);
+    const int n = newrank_of(me, p);
+    RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
+                                         : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
+    trace("reduce_scatter: total=%zu esz=%zu algo=%d chunk=%zu", total, esz, algo, ce);
     const size_t mycnt = (size_t)recvcounts[me];
-    char* out = nullptr;
-    if (mycnt) {
-        out = (mine_stage_out || mine_temp) ? win[me] + bytes : static_cast<char*>(bdst.dev);
-        RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
-                                             : tree_reduce_scatter(p, newrank_of(me, p) >= 0
-                                                                          ? newrank_of(me, p)
-                                                                          : newrank_of(me + 1, p));
-        rc = run_rank_tree(op.opidx, k, t, pin, esz, disp[me], mycnt, out, s);
-        if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter combine");
+    const BufInfo bd = classify(recvbuf);
+    char* dst = static_cast<char*>(recvbuf);
+    std::vector<char*> ins((size_t)p);
+    char* hold = nullptr;
+    if (in_place && mycnt) {
+        hold = dev_scratch(mycnt * esz);
+        if (!hold) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
     }
-    if (rc == MPI_SUCCESS) rc = tp->barrier();
-    if (rc == MPI_SUCCESS && mycnt && out != static_cast<char*>(bdst.dev)) {
-        hipError_t e = hipMemcpyAsync(recvbuf, out, mycnt * esz, hipMemcpyDefault, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hip_fail(e, "reduce_scatter result copy");
+    int slot = 0;
+    for (size_t o = 0; o < maxcnt && rc == MPI_SUCCESS; o += ce, slot ^= 1) {
+        // stage, for every destination r, our contribution to r's block range [o, o+ce)
+        char* mine = w.in(me, slot);
+        for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
+            const size_t cnt = (size_t)recvcounts[r];
+            if (o >= cnt) continue;
+            const size_t len = std::min(ce, cnt - o);
+            rc = copy_async(mine + (size_t)r * ce * esz, src + (disp[r] + o) * esz, len * esz, s);
+        }
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter stage");
+        if (rc == MPI_SUCCESS) rc = tp->barrier();
+        if (rc != MPI_SUCCESS) break;
+        if (o < mycnt) {
+            const size_t len = std::min(ce, mycnt - o);
+            for (int r = 0; r < p; ++r) ins[r] = w.in(r, slot) + (size_t)me * ce * esz;
+            // In place, recvbuf is still our input for later chunks: results go
+            // to a private device scratch and are copied out at the end.
+            char* out = in_place ? hold + o * esz
+                                 : (bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz
+                                                              : w.out(me, slot));
+            rc = run_rank_tree(op.opidx, k, t, ins, esz, 0, len, out, s);
+            if (rc == MPI_SUCCESS && out == w.out(me, slot))
+                rc = copy_async(dst + o * esz, out, len * esz, s);
+        }
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter reduce");
     }
+    if (rc == MPI_SUCCESS) rc = tp->barrier();   // every rank finished reading the windows
+    if (rc == MPI_SUCCESS && in_place && mycnt) {
+        rc = copy_async(recvbuf, hold, mycnt * esz, s);
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter result");
+    }
+    trace("reduce_scatter: done rc=%d", rc);
     return rc;
 }
 
@@ -788,15 +833,18 @@ int engine_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int
 int engine_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                   const OpRef& op, int root)
 {
-    // Root receives the allreduce result (root-0 trees coincide with the
-    // allreduce trees, reduce.cpp:226-299, 489-537); other ranks discard it.
+    // The root receives the allreduce expression tree (identical to the
+    // reference's Rabenseifner / binomial reduce for root 0, reduce.cpp:226-299,
+    // 489-537); other ranks only contribute.  User ops: host allreduce.
     return worker()
         .submit([=]() -> int {
-            const size_t bytes = count * (size_t)type_size(dt);
-            if (c->rank == root) return do_allreduce(c, sendbuf, recvbuf, count, dt, op);
-            std::vector<char> scratch(bytes);
-            const void* sb = sendbuf;
-            return do_allreduce(c, sb, scratch.data(), count, dt, op);
+            if (op.opidx == O_NULL) {
+                const size_t bytes = count * (size_t)type_size(dt);
+                std::vector<char> tmp(bytes);
+                int rc = host_user_allreduce(c, sendbuf, c->rank == root ? recvbuf : tmp.data(), count, dt, op);
+                return rc;
+            }
+            return do_allreduce(c, sendbuf, recvbuf, count, dt, op, root);
         })
         .get();
 }

@@ -152,8 +152,8 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("p", [2, 3, 4])
-def test_collectives_p_ranks_on_one_gpu(p):
+@pytest.mark.parametrize("p,chunk", [(2, None), (3, 65536), (4, 1 << 20), (5, None)])
+def test_collectives_p_ranks_on_one_gpu(p, chunk):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -164,6 +164,8 @@ def test_collectives_p_ranks_on_one_gpu(p):
         env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
                     "MSX_BOOTSTRAP_TIMEOUT": "180"})
+        if chunk:
+            env["MSX_CHUNK_BYTES"] = str(chunk)     # many chunks, pieces across block edges
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
