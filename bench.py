@@ -67,7 +67,7 @@ def run_collectives_child(world, rank, local, scale):
     try:
         pr = subprocess.run([sys.executable, os.path.join(REPO, "bench_collectives.py"), out, str(scale)],
                             env=env, capture_output=True, text=True,
-                            timeout=float(os.environ.get("MSX_COLL_TIMEOUT", "420")))
+                            timeout=float(os.environ.get("MSX_COLL_TIMEOUT", "240")))
         if pr.returncode != 0:
             return {"error": f"rank {rank} child rc={pr.returncode}: {pr.stderr[-600:]}"}
     except subprocess.TimeoutExpired as e:
