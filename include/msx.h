@@ -69,11 +69,13 @@ int msx_set_staging_chunk(int64_t bytes);
 /* schedule introspection for host-side tests of the collective engine
  * (mpid/reduce.cpp:3884-4066, 917-1334 restated as expression trees):
  * which = 0 allreduce tree of newrank n, 1 reduce_scatter tree of newrank n,
- * 2 pairwise chain of real rank n.  src32[i] = real rank in kernel slot i. */
+ * 2 pairwise chain of real rank n, 3 MPI_Reduce Rabenseifner tree of newrank n,
+ * 4 MPI_Reduce binomial tree for root n.  src32[i] = real rank in kernel slot
+ * i (-1 = empty). */
 int msx_schedule_tree(int which, int p, int n, int* src32, int* P, unsigned* pairmask,
                       int* chain);
-/* which = 0 allreduce, 1 reduce_scatter: 0 recursive doubling, 1 Rabenseifner,
- * 2 recursive halving, 3 pairwise */
+/* which = 0 allreduce, 1 reduce_scatter, 2 reduce: 0 recursive doubling,
+ * 1 Rabenseifner, 2 recursive halving, 3 pairwise, 4 binomial */
 int msx_schedule_algo(int which, int p, int64_t count, int type_size);
 int msx_schedule_newrank(int rank, int p);
 int msx_schedule_block(int p, int64_t count, int n, int64_t* start, int64_t* len);

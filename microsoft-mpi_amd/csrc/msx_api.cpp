@@ -756,9 +756,14 @@ MSX_EXPORT int msx_schedule_tree(int which, int p, int n, int* src32, int* P, un
     if (which == 0) t = tree_allreduce(p, n);
     else if (which == 1) t = tree_reduce_scatter(p, n);
     else if (which == 2) t = tree_pairwise(p, n);
+    else if (which == 3) t = tree_reduce_rsag(p, n);
+    else if (which == 4) t = tree_reduce_binomial(p, n);
     else return MPI_ERR_ARG;
     for (int i = 0; i < 32; ++i) src32[i] = t.src[i];
     *P = t.P;
+    if (t.nleaves) {   // absent leaves are reported as -1
+        for (int i = 2 * t.nleaves; i < 32; ++i) src32[i] = -1;
+    }
     *pairmask = t.pairmask;
     *chain = t.chain ? 1 : 0;
     return MPI_SUCCESS;
@@ -768,6 +773,7 @@ MSX_EXPORT int msx_schedule_tree(int which, int p, int n, int* src32, int* P, un
 MSX_EXPORT int msx_schedule_algo(int which, int p, int64_t count, int type_size)
 {
     if (which == 0) return allreduce_algo(p, (size_t)count, type_size, true);
+    if (which == 2) return reduce_algo(p, (size_t)count, type_size, true);
     return reduce_scatter_algo(p, (size_t)count, type_size, true);
 }
 

@@ -36,6 +36,7 @@ hipError_t launch_tree(int opidx, Kind k, const void* const* srcs_dev, int p, vo
 struct TreeSpec {
     const void* src[32] = {};
     int P = 1;
+    int nleaves = 0;        // 0 = P; else leaves [nleaves, P) are absent (binomial trees)
     unsigned pairmask = 0;
     bool chain = false;
     bool sys = false;   // sources/output shared with peers: system acquire/release

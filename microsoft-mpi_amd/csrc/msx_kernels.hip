@@ -244,6 +244,7 @@ constexpr int kMaxLeaves = 16;
 struct TreeArgs {
     const void* s[2 * kMaxLeaves];
     int P;
+    int nleaves;   // leaves present (<= P); the rest of the P-leaf tree is empty
     unsigned pairmask;
     int chain;
     int sys;   // sources/outputs shared with other GPUs: system-coherent access
@@ -273,10 +274,12 @@ __device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
         for (int k = 1; k < a.P; ++k) v = F::apply(v, load(k));
         return v;
     }
+    // leaves >= nleaves are absent (binomial trees over a non-power-of-two p):
+    // a node whose right subtree is empty passes its left value up unchanged.
     V v[kMaxLeaves];
 #pragma unroll
     for (int k = 0; k < kMaxLeaves; ++k) {
-        if (k < a.P) {
+        if (k < a.nleaves) {
             v[k] = load(2 * k);
             if ((a.pairmask >> k) & 1u) v[k] = F::apply(v[k], load(2 * k + 1));
         }
@@ -285,7 +288,7 @@ __device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
     for (int w = 1; w < kMaxLeaves; w *= 2) {
 #pragma unroll
         for (int k = 0; k + w < kMaxLeaves; k += 2 * w)
-            if (k + w < a.P) v[k] = F::apply(v[k], v[k + w]);
+            if (k + w < a.nleaves) v[k] = F::apply(v[k], v[k + w]);
     }
     return v[0];
 }
@@ -595,7 +598,9 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         if (t.P & (t.P - 1)) return hipErrorInvalidValue;
         for (int i = 0; i < 2 * t.P; ++i) a.s[i] = t.src[i];
         ns = 0;
-        for (int i = 0; i < t.P; ++i) {
+        const int nl = (t.nleaves > 0 && t.nleaves <= t.P) ? t.nleaves : t.P;
+        for (int i = nl; i < t.P; ++i) a.s[2 * i] = a.s[2 * i + 1] = t.src[0];   // never read
+        for (int i = 0; i < nl; ++i) {
             if (!t.src[2 * i]) return hipErrorInvalidValue;
             if ((t.pairmask >> i) & 1u) { if (!t.src[2 * i + 1]) return hipErrorInvalidValue; }
             else a.s[2 * i + 1] = t.src[2 * i];   // keep alignment check simple
@@ -603,6 +608,7 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         ns = 2 * t.P;
     }
     a.P = t.P;
+    a.nleaves = (t.nleaves > 0 && t.nleaves <= t.P) ? t.nleaves : t.P;
     a.pairmask = t.pairmask;
     a.chain = t.chain ? 1 : 0;
     a.sys = t.sys ? 1 : 0;

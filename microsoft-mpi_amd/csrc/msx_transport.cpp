@@ -423,6 +423,48 @@ RankTree tree_reduce_scatter(int p, int n)
     return tree_from_leaves(p, lv, P);
 }
 
+int reduce_algo(int p, size_t count, int type_size, bool builtin)
+{
+    // reduce.cpp:151: (unsigned)(count*type_size) > reduce_short_msg (64 KiB)
+    const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)type_size);
+    return (nbytes > 65536u && builtin && count >= (size_t)pof2_floor(p)) ? A_RABENSEIFNER : A_BINOMIAL;
+}
+
+RankTree tree_reduce_rsag(int p, int n)
+{
+    // MPI_Reduce folds the ODD rank into the even one below it (reduce.cpp:
+    // 136-165: Uop(tmp = x_{2n+1}, recvbuf = x_{2n})), newrank n -> real 2n.
+    const int P = pof2_floor(p), rem = p - P;
+    RankTree t;
+    t.P = P;
+    for (int i = 0; i < 32; ++i) t.src[i] = -1;
+    for (int k = 0; k < P; ++k) {
+        const int m = n ^ k;
+        if (m < rem) {
+            t.src[2 * k] = 2 * m;
+            t.src[2 * k + 1] = 2 * m + 1;
+            t.pairmask |= 1u << k;
+        } else {
+            t.src[2 * k] = m + rem;
+        }
+    }
+    return t;
+}
+
+RankTree tree_reduce_binomial(int p, int root)
+{
+    // relrank k receives from k|mask (reduce.cpp:489-537): a balanced tree over
+    // relative ranks with the leaves >= p absent
+    RankTree t;
+    int P = 1;
+    while (P < p) P *= 2;
+    t.P = P;
+    t.nleaves = p;
+    for (int i = 0; i < 32; ++i) t.src[i] = -1;
+    for (int k = 0; k < p; ++k) t.src[2 * k] = (k + root) % p;
+    return t;
+}
+
 RankTree tree_pairwise(int p, int r)
 {
     RankTree t;
@@ -517,10 +559,11 @@ int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>
     if (len == 0) return MPI_SUCCESS;
     TreeSpec spec;
     spec.P = t.P;
+    spec.nleaves = t.nleaves;
     spec.pairmask = t.pairmask;
     spec.chain = t.chain;
     spec.sys = true;
-    const int nslots = t.chain ? t.P : 2 * t.P;
+    const int nslots = t.chain ? t.P : 2 * (t.nleaves ? t.nleaves : t.P);
     for (int i = 0; i < nslots; ++i)
         spec.src[i] = t.src[i] >= 0 ? srcs[(size_t)t.src[i]] + start * esz : nullptr;
     hipError_t e = launch_tree_spec(opidx, k, spec, out, len, s);
@@ -654,7 +697,9 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
     char* dst = static_cast<char*>(recvbuf);
     const bool want = (root < 0 || root == me);          // this rank receives the result
-    const int algo = allreduce_algo(p, count, (int)esz, true);
+    const bool is_reduce = root >= 0;
+    const int algo = is_reduce ? reduce_algo(p, count, (int)esz, true)
+                               : allreduce_algo(p, count, (int)esz, true);
     Windows w;
     if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
     // chunk = whole 16-byte vectors of whole elements
@@ -673,9 +718,10 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         if ((rc = copy_async(ins[me], src + o * esz, len * esz, s)) != MPI_SUCCESS) break;
         if ((rc = sync_stream(s, "allreduce stage")) != MPI_SUCCESS) break;
         if ((rc = tp->barrier()) != MPI_SUCCESS) break;                  // A
-        if (algo == A_RECURSIVE_DOUBLING) {
-            // every rank evaluates its own lineage's tree on the whole chunk
-            RankTree t = tree_allreduce(p, lineage);
+        if (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) {
+            // recursive doubling: every rank evaluates its own lineage's tree on
+            // the whole chunk; binomial reduce: the root evaluates its tree
+            RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
             if (want) rc = run_rank_tree(op.opidx, k, t, ins, esz, 0, len, outs[me], s);
             if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, outs[me], len * esz, s);
             if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce chunk");
@@ -695,7 +741,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             size_t bs, bl;
             allreduce_block(p, count, j, &bs, &bl);
             const size_t e1 = std::min(phi, bs + bl - o);
-            RankTree t = tree_allreduce(p, allreduce_block_owner(p, j));
+            const int owner = allreduce_block_owner(p, j);
+            RankTree t = is_reduce ? tree_reduce_rsag(p, owner) : tree_allreduce(p, owner);
             rc = run_rank_tree(op.opidx, k, t, ins, esz, e0, e1 - e0, outs[me] + e0 * esz, s);
             e0 = e1;
         }

@@ -42,7 +42,8 @@ void transport_destroy(Transport* t);
 // ---- schedules (pure functions; exported for host-side tests) ----------------
 // Reference algorithm selected for an allreduce (reduce.cpp:3884-3888) and for a
 // reduce_scatter (reduce.cpp:1705-1750).
-enum Algo { A_RECURSIVE_DOUBLING = 0, A_RABENSEIFNER = 1, A_RS_HALVING = 2, A_RS_PAIRWISE = 3 };
+enum Algo { A_RECURSIVE_DOUBLING = 0, A_RABENSEIFNER = 1, A_RS_HALVING = 2, A_RS_PAIRWISE = 3,
+            A_BINOMIAL = 4 };
 
 struct Leaf { int a = -1, b = -1; };   // real ranks: value = a, or a op b when b >= 0
 
@@ -52,6 +53,8 @@ int real_of_newrank(int n, int p);
 Leaf leaf_of(int n, int p);                       // leaf value of newrank n
 int allreduce_algo(int p, size_t count, int type_size, bool builtin);
 int reduce_scatter_algo(int p, size_t total_count, int type_size, bool commutative);
+// MPI_Reduce (reduce.cpp:151-153): Rabenseifner or binomial
+int reduce_algo(int p, size_t count, int type_size, bool builtin);
 // allreduce Rabenseifner blocks: block j = [start, start+len), computed at newrank owner
 void allreduce_block(int p, size_t count, int j, size_t* start, size_t* len);
 int allreduce_block_owner(int p, int j);           // newrank that owns block j
@@ -62,6 +65,7 @@ int allreduce_block_of_newrank(int p, int n);
 //   pairwise:       chain x_r, x_{r-1}, ..., x_{r-p+1}
 struct RankTree {
     int P = 1;
+    int nleaves = 0;        // 0 = P (binomial trees over non-power-of-two p use fewer)
     unsigned pairmask = 0;
     bool chain = false;
     int src[32];            // real ranks in kernel slot order
@@ -69,6 +73,10 @@ struct RankTree {
 RankTree tree_allreduce(int p, int n);
 RankTree tree_reduce_scatter(int p, int n);
 RankTree tree_pairwise(int p, int r);
+//   reduce, Rabenseifner: leaves y_k = leafR(n ^ k), leafR = even-first fold
+RankTree tree_reduce_rsag(int p, int n);
+//   reduce, binomial:     leaves x_{(k + root) % p}, k < p, of a nextpow2(p) tree
+RankTree tree_reduce_binomial(int p, int root);
 
 // ---- engine entry points (msx_comm.cpp routes size > 1 here) ---------------
 int engine_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,

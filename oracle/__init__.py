@@ -43,6 +43,8 @@ def lib():
     L.oracle_reduce_local_mt.argtypes = [i, i, p, p, i64, i]
     L.oracle_allreduce.restype = i
     L.oracle_allreduce.argtypes = [i, i, i, i64, ctypes.POINTER(p), ctypes.POINTER(p)]
+    L.oracle_reduce.restype = i
+    L.oracle_reduce.argtypes = [i, i, i, i, i64, ctypes.POINTER(p), p]
     L.oracle_reduce_scatter.restype = i
     L.oracle_reduce_scatter.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(p), ctypes.POINTER(p)]
     _lib = L
@@ -82,3 +84,9 @@ def reduce_scatter(op, dt, recvcounts, sendbufs, recvbufs):
     R = (ctypes.c_void_p * p)(*[_addr(b) for b in recvbufs])
     C = (ctypes.c_int * p)(*recvcounts)
     return lib().oracle_reduce_scatter(op, dt, p, C, S, R)
+
+
+def reduce(op, dt, root, sendbufs, recvbuf):
+    p = len(sendbufs)
+    S = (ctypes.c_void_p * p)(*[_addr(b) for b in sendbufs])
+    return lib().oracle_reduce(op, dt, p, root, sendbufs[0].size, S, _addr(recvbuf))

@@ -271,11 +271,112 @@ int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcoun
     return rc ? MPI_ERR_OP : MPI_SUCCESS;
 }
 
+/* MPIR_Reduce_intra_flat (reduce.cpp:63-566), commutative builtin ops.
+ * Rabenseifner (bytes > 64 KiB, count >= pof2): ODD ranks < 2*rem fold into
+ * the even rank below (:136-165), recursive halving as in allreduce (with
+ * real rank = newdst < rem ? 2*newdst : newdst + rem), then a gather to root
+ * that only moves data (:330-450): root's block j is the value its owner
+ * computed.  Binomial (otherwise, :489-537): relative ranks to root, node
+ * relrank receives from relrank|mask and combines Uop(tmp=received, recvbuf). */
 int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
                   const void* const* sendbufs, void* recvbuf_root)
 {
-    (void)op; (void)dt; (void)p; (void)root; (void)count; (void)sendbufs; (void)recvbuf_root;
-    return MPI_ERR_INTERN;   /* rooted schedules: see DESIGN.md §Next */
+    if (oracle_op_check(op, dt) != MPI_SUCCESS) return MPI_ERR_OP;
+    if (p < 1 || root < 0 || root >= p) return MPI_ERR_ARG;
+    if (count == 0) return MPI_SUCCESS;
+    const int64_t esz = oracle_kind_size(oracle_kind_of(dt));
+    const int64_t bytes = count * esz;
+    char** rb = (char**)calloc((size_t)p, sizeof(char*));
+    char** tmp = (char**)calloc((size_t)p, sizeof(char*));
+    char** snap = (char**)calloc((size_t)p, sizeof(char*));
+    int rc = 0;
+    for (int r = 0; r < p; ++r) {
+        rb[r] = (char*)malloc((size_t)bytes);
+        tmp[r] = (char*)malloc((size_t)bytes);
+        snap[r] = (char*)malloc((size_t)bytes);
+        memcpy(rb[r], sendbufs[r], (size_t)bytes);
+    }
+    const int pof2 = pof2_floor(p), rem = p - pof2;
+    const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)esz);   /* :151 */
+    if (nbytes > 65536u && count >= pof2) {
+        int* real = (int*)calloc((size_t)pof2, sizeof(int));
+        for (int r = 0; r < p; ++r) {
+            if (r < 2 * rem) {
+                if ((r & 1) == 0) {                 /* even: receive from r+1 and combine */
+                    memcpy(tmp[r], rb[r + 1], (size_t)bytes);
+                    rc |= combine(op, dt, tmp[r], rb[r], count);
+                    real[r / 2] = r;
+                }
+            } else {
+                real[r - rem] = r;
+            }
+        }
+        const int64_t reduceSize = count / pof2, endSize = count % pof2;
+        int *send_idx = calloc((size_t)pof2, sizeof(int)), *recv_idx = calloc((size_t)pof2, sizeof(int));
+        int *last_idx = calloc((size_t)pof2, sizeof(int)), *idx_shift = calloc((size_t)pof2, sizeof(int));
+        int64_t* rcnt = calloc((size_t)pof2, sizeof(int64_t));
+        for (int n = 0; n < pof2; ++n) { last_idx[n] = pof2; idx_shift[n] = pof2 >> 1; }
+        for (int mask = 1; mask < pof2; mask <<= 1) {
+            for (int n = 0; n < pof2; ++n) {
+                const int nd = n ^ mask;
+                if (n < nd) {
+                    send_idx[n] = recv_idx[n] + idx_shift[n];
+                    rcnt[n] = (int64_t)(send_idx[n] - recv_idx[n]) * reduceSize;
+                } else {
+                    recv_idx[n] = send_idx[n] + idx_shift[n];
+                    rcnt[n] = (int64_t)(last_idx[n] - recv_idx[n]) * reduceSize;
+                    if (last_idx[n] == pof2) rcnt[n] += endSize;
+                }
+            }
+            for (int n = 0; n < pof2; ++n) memcpy(snap[real[n]], rb[real[n]], (size_t)bytes);
+            for (int n = 0; n < pof2; ++n) {
+                const int r = real[n], d = n ^ mask;
+                const int64_t off = reduceSize * recv_idx[n] * esz;
+                memcpy(tmp[r] + off, snap[real[d]] + reduceSize * send_idx[d] * esz, (size_t)(rcnt[n] * esz));
+                rc |= combine(op, dt, tmp[r] + off, rb[r] + off, rcnt[n]);
+            }
+            for (int n = 0; n < pof2; ++n) {
+                send_idx[n] = recv_idx[n];
+                if ((mask << 1) < pof2) {
+                    last_idx[n] = recv_idx[n] + idx_shift[n];
+                    idx_shift[n] >>= 1;
+                }
+            }
+        }
+        /* gather: block j lives at newrank bitrev(j) after the halving */
+        int bits = 0;
+        while ((1 << bits) < pof2) ++bits;
+        char* out = (char*)recvbuf_root;
+        for (int j = 0; j < pof2; ++j) {
+            int o = 0;
+            for (int b = 0; b < bits; ++b) o |= ((j >> b) & 1) << (bits - 1 - b);
+            const int64_t lo = (int64_t)j * reduceSize, ln = reduceSize + (j == pof2 - 1 ? endSize : 0);
+            memcpy(out + lo * esz, rb[real[o]] + lo * esz, (size_t)(ln * esz));
+        }
+        free(real); free(send_idx); free(recv_idx); free(last_idx); free(idx_shift); free(rcnt);
+    } else {
+        /* binomial (:489-537), commutative: lroot = root */
+        for (int mask = 1; mask < p; mask <<= 1) {
+            for (int r = 0; r < p; ++r) memcpy(snap[r], rb[r], (size_t)bytes);
+            for (int r = 0; r < p; ++r) {
+                int rel = r - root;
+                if (rel < 0) rel += p;
+                if ((rel & (mask - 1)) != 0) continue;          /* already sent and left */
+                if ((rel & mask) == 0) {
+                    int src = rel | mask;
+                    if (src < p) {
+                        src = (src + root) % p;
+                        memcpy(tmp[r], snap[src], (size_t)bytes);
+                        rc |= combine(op, dt, tmp[r], rb[r], count);
+                    }
+                }
+            }
+        }
+        memcpy(recvbuf_root, rb[root], (size_t)bytes);
+    }
+    for (int r = 0; r < p; ++r) { free(rb[r]); free(tmp[r]); free(snap[r]); }
+    free(rb); free(tmp); free(snap);
+    return rc ? MPI_ERR_OP : MPI_SUCCESS;
 }
 
 int oracle_scan(MPI_Op op, MPI_Datatype dt, int p, int64_t count, int exclusive,

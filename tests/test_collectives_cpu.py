@@ -68,6 +68,9 @@ def eval_tree(tree, xs, op, dt, lo, hi):
         return v
     leaves = []
     for k in range(P):
+        if src[2 * k] < 0:            # absent leaf (binomial tree over non-pof2 p)
+            leaves.append(None)
+            continue
         v = xs[src[2 * k]][lo:hi].copy()
         if (pm >> k) & 1:
             oracle.reduce_local(op, dt, xs[src[2 * k + 1]][lo:hi].copy(), v)
@@ -75,7 +78,8 @@ def eval_tree(tree, xs, op, dt, lo, hi):
     w = 1
     while w < P:
         for k in range(0, P, 2 * w):
-            oracle.reduce_local(op, dt, leaves[k + w], leaves[k])
+            if leaves[k + w] is not None:
+                oracle.reduce_local(op, dt, leaves[k + w], leaves[k])
         w *= 2
     return leaves[0]
 
@@ -93,6 +97,19 @@ def engine_allreduce_result(xs, op, dt, rank):
     for m in range(pof2):                   # every block, computed by its owner m
         lo, ln = schedule_block(p, count, m)
         out[lo:lo + ln] = eval_tree(schedule_tree(0, p, m), xs, op, dt, lo, lo + ln)
+    return out
+
+
+def engine_reduce_result(xs, op, dt, root):
+    """What the engine's MPI_Reduce leaves in root's recvbuf."""
+    p, count = len(xs), xs[0].size
+    if algo(2, p, count, xs[0].dtype.itemsize) == 4:                 # binomial
+        return eval_tree(schedule_tree(4, p, root), xs, op, dt, 0, count)
+    out = np.empty_like(xs[0])
+    pof2 = 1 << (p.bit_length() - 1)
+    for m in range(pof2):
+        lo, ln = schedule_block(p, count, m)
+        out[lo:lo + ln] = eval_tree(schedule_tree(3, p, m), xs, op, dt, lo, lo + ln)
     return out
 
 
@@ -150,6 +167,19 @@ def test_engine_reduce_scatter_schedule_matches_reference_simulation(p, per, opn
         assert np.array_equal(got.view(np.uint32), rb[r].view(np.uint32)), (p, per, r)
 
 
+@pytest.mark.parametrize("p", [1, 2, 3, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("count", [13, 30000])        # binomial / Rabenseifner (> 64 KiB)
+@pytest.mark.parametrize("opname", ["MPI_SUM", "MPI_MAX"])
+def test_engine_reduce_schedule_matches_reference_simulation(p, count, opname):
+    op = getattr(C, opname)
+    xs = _data(p, count, op, 31 * p + count % 89)
+    for root in sorted({0, p - 1, p // 2}):
+        exp = np.zeros(count, np.float32)
+        assert oracle.reduce(op, C.MPI_FLOAT, root, xs, exp) == 0
+        got = engine_reduce_result(xs, op, C.MPI_FLOAT, root)
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), (p, count, root)
+
+
 def test_algorithm_gates_follow_reference_32bit_arithmetic():
     # allreduce: RD iff (unsigned)(count*size) <= 256 KiB or count < pof2 (reduce.cpp:3884)
     assert algo(0, 8, 65536, 4) == 0 and algo(0, 8, 65537, 4) == 1
@@ -158,6 +188,8 @@ def test_algorithm_gates_follow_reference_32bit_arithmetic():
     # reduce_scatter: c4 (536870912 doubles = 2^32 B) wraps to 0 -> recursive halving
     assert algo(1, 8, 536870912, 8) == 2
     assert algo(1, 8, 65536, 8) == 3 and algo(1, 8, 65535, 8) == 2
+    # reduce: Rabenseifner iff (unsigned)(count*size) > 64 KiB and count >= pof2 (reduce.cpp:151)
+    assert algo(2, 8, 16384, 4) == 4 and algo(2, 8, 16385, 4) == 1
 
 
 # ---------------------------------------------------------------------------

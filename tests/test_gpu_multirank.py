@@ -107,17 +107,21 @@ for i, (opn, dtn, per) in enumerate(RS):
             continue
         check(f"reduce_scatter {opn} {dtn} {per} {mode}", fromdev(rb, exp[rank], counts[rank]), exp[rank])
 
-# MPI_Reduce (integer: order-independent) at two roots
-xs = inputs("MPI_SUM", "MPI_INT", 5000, 3000)
-exp = np.sum(np.stack(xs).astype(np.int64), axis=0).astype(np.int32)
-for root in (0, p - 1):
-    sb = todev(xs[rank])
-    rb = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
-    rc = L.MPI_Reduce(sb.data_ptr(), rb.data_ptr(), 5000, C.MPI_INT, C.MPI_SUM, root, C.MPI_COMM_WORLD)
-    if rc != 0:
-        fails.append(f"reduce root={root} rc={rc} {msx.last_error()}")
-    elif rank == root:
-        check(f"reduce root={root}", fromdev(rb, xs[rank]), exp)
+# MPI_Reduce, binomial (small) and Rabenseifner (> 64 KiB) orders, several roots
+for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 5000), ("MPI_SUM", "MPI_FLOAT", 70003),
+                                       ("MPI_MAX", "MPI_DOUBLE", 3000), ("MPI_MAX", "MPI_DOUBLE", 40000)]):
+    op, dt = getattr(C, opn), getattr(C, dtn)
+    xs = inputs(opn, dtn, count, 3000 + i)
+    for root in sorted({0, p - 1, p // 2}):
+        exp = raw(np.zeros_like(xs[0]))
+        assert oracle.reduce(op, dt, root, xs, exp) == 0
+        sb = todev(xs[rank])
+        rb = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+        rc = L.MPI_Reduce(sb.data_ptr(), rb.data_ptr(), count, dt, op, root, C.MPI_COMM_WORLD)
+        if rc != 0:
+            fails.append(f"reduce {opn} {count} root={root} rc={rc} {msx.last_error()}")
+        elif rank == root:
+            check(f"reduce {opn} {dtn} {count} root={root}", fromdev(rb, xs[rank]), exp)
 
 # MPI_Iallreduce BAND u64 (config 5 op/type) overlapped with host compute
 xs = inputs("MPI_BAND", "MPI_UINT64_T", 1 << 18, 4000)
