@@ -896,12 +896,137 @@ int engine_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI
         .get();
 }
 
+namespace {
+
+// MPI_Scan / MPI_Exscan: the reference builds a recursive-doubling task list
+// (IscanBuildTaskList reduce.cpp:5285-5576, IexscanBuildTaskList :5671-5960,
+// NbcTask::ExecuteScan tasks.cpp:694-766).  At step mask, rank r exchanges its
+// partial result with dst = r ^ mask; if r > dst it folds the received value
+// into both its partial and its result (Uop(tmp, partial), Uop(tmp, recvbuf);
+// the first such step of Exscan copies tmp into recvbuf), else only into its
+// partial.  The schedule is run step by step here, the exchange going through
+// the IPC windows, so every combine has the reference's operands and roles.
+int host_user_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                   const OpRef& op, bool exclusive)
+{
+    const int p = c->size, me = c->rank, esz = type_size(dt);
+    const size_t bytes = count * (size_t)esz;
+    std::vector<char> mine(bytes), all((size_t)p * bytes);
+    int rc = copy_any(mine.data(), sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, bytes);
+    if (rc == MPI_SUCCESS) rc = c->tp->allgather(mine.data(), bytes, all.data());
+    if (rc != MPI_SUCCESS) return rc;
+    auto call = [&](const char* in, char* io) {
+        for (size_t off = 0; off < count;) {
+            size_t n = std::min(count - off, (size_t)0x7fffffff);
+            int len = (int)n;
+            MPI_Datatype d = dt;
+            op.user_fn(const_cast<char*>(in) + off * esz, io + off * esz, &len, &d);
+            off += n;
+        }
+    };
+    std::vector<std::vector<char>> part((size_t)p), res((size_t)p);
+    std::vector<bool> have((size_t)p, !exclusive);
+    for (int r = 0; r < p; ++r) {
+        part[r].assign(all.begin() + (size_t)r * bytes, all.begin() + (size_t)(r + 1) * bytes);
+        res[r] = part[r];
+    }
+    for (int mask = 1; mask < p; mask <<= 1) {
+        std::vector<std::vector<char>> snap = part;
+        const bool last = (mask << 1) >= p;
+        for (int r = 0; r < p; ++r) {
+            const int dst = r ^ mask;
+            if (dst >= p || (last && r < dst)) continue;
+            std::vector<char> tmp = snap[dst];
+            if (r > dst) {
+                call(tmp.data(), part[r].data());
+                if (exclusive && !have[r]) { res[r] = tmp; have[r] = true; }
+                else call(tmp.data(), res[r].data());
+            } else if (op.commutative) {
+                call(tmp.data(), part[r].data());
+            } else {
+                call(part[r].data(), tmp.data());
+                part[r] = tmp;
+            }
+        }
+    }
+    if (exclusive && !have[me]) return MPI_SUCCESS;     // rank 0: recvbuf undefined
+    return copy_any(recvbuf, res[me].data(), bytes);
+}
+
+int combine2(int opidx, Kind k, const char* inout_src, const char* in, char* out, size_t n, hipStream_t s)
+{
+    TreeSpec t;
+    t.P = 2;
+    t.src[0] = inout_src;
+    t.src[2] = in;
+    t.sys = true;
+    hipError_t e = launch_tree_spec(opidx, k, t, out, n, s);
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "scan combine");
+}
+
+int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+            const OpRef& op, bool exclusive)
+{
+    if (op.opidx == O_NULL) return host_user_scan(c, sendbuf, recvbuf, count, dt, op, exclusive);
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    Transport* tp = c->tp;
+    const int p = c->size, me = c->rank;
+    const Kind k = type_info(dt)->kind;
+    const size_t esz = (size_t)type_info(dt)->size, bytes = count * esz;
+    hipStream_t s = tp->stream();
+    const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
+    Windows w;
+    if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
+    size_t ce = w.C / esz;
+    ce -= ce % 16;
+    char* partial = dev_scratch(2 * bytes + 256);
+    if (!partial) { set_error("scan: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+    char* res = partial + ((bytes + 255) & ~(size_t)255);
+    rc = copy_async(partial, src, bytes, s);
+    if (rc == MPI_SUCCESS && !exclusive) rc = copy_async(res, src, bytes, s);
+    if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan init");
+    bool have = !exclusive;
+    int slot = 0;
+    for (int mask = 1; mask < p && rc == MPI_SUCCESS; mask <<= 1) {
+        const int dst = me ^ mask;
+        const bool last = (mask << 1) >= p;
+        const bool use = dst < p && !(last && me < dst);     // this rank consumes dst's partial
+        for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce, slot ^= 1) {
+            const size_t len = std::min(ce, count - o);
+            char* stage = w.in(me, slot);
+            rc = copy_async(stage, partial + o * esz, len * esz, s);       // partial at step start
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan stage");
+            if (rc == MPI_SUCCESS) rc = tp->barrier();
+            if (rc != MPI_SUCCESS || !use) continue;
+            const char* tmp = w.in(dst, slot);
+            char* pp = partial + o * esz;
+            char* rr = res + o * esz;
+            if (me > dst) {
+                rc = combine2(op.opidx, k, pp, tmp, pp, len, s);
+                if (rc == MPI_SUCCESS)
+                    rc = have ? combine2(op.opidx, k, rr, tmp, rr, len, s) : copy_async(rr, tmp, len * esz, s);
+            } else {
+                rc = combine2(op.opidx, k, pp, tmp, pp, len, s);             // builtins commute
+            }
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan step");
+        }
+        if (use && me > dst) have = true;
+    }
+    if (rc == MPI_SUCCESS) rc = tp->barrier();
+    if (rc == MPI_SUCCESS && have) {
+        rc = copy_async(recvbuf, res, bytes, s);
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan result");
+    }
+    return rc;
+}
+
+}  // namespace
+
 int engine_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                 const OpRef& op, bool exclusive)
 {
-    (void)c; (void)sendbuf; (void)recvbuf; (void)count; (void)dt; (void)op; (void)exclusive;
-    set_error("MPI_Scan/MPI_Exscan on more than one rank is not implemented yet");
-    return MPI_ERR_INTERN;
+    return worker().submit([=] { return do_scan(c, sendbuf, recvbuf, count, dt, op, exclusive); }).get();
 }
 
 std::shared_future<int> engine_async(std::function<int()> fn) { return worker().submit(std::move(fn)); }

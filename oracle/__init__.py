@@ -45,6 +45,8 @@ def lib():
     L.oracle_allreduce.argtypes = [i, i, i, i64, ctypes.POINTER(p), ctypes.POINTER(p)]
     L.oracle_reduce.restype = i
     L.oracle_reduce.argtypes = [i, i, i, i, i64, ctypes.POINTER(p), p]
+    L.oracle_scan.restype = i
+    L.oracle_scan.argtypes = [i, i, i, i64, i, ctypes.POINTER(p), ctypes.POINTER(p)]
     L.oracle_reduce_scatter.restype = i
     L.oracle_reduce_scatter.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(p), ctypes.POINTER(p)]
     _lib = L
@@ -90,3 +92,10 @@ def reduce(op, dt, root, sendbufs, recvbuf):
     p = len(sendbufs)
     S = (ctypes.c_void_p * p)(*[_addr(b) for b in sendbufs])
     return lib().oracle_reduce(op, dt, p, root, sendbufs[0].size, S, _addr(recvbuf))
+
+
+def scan(op, dt, sendbufs, recvbufs, exclusive=False):
+    p = len(sendbufs)
+    S = (ctypes.c_void_p * p)(*[_addr(b) for b in sendbufs])
+    R = (ctypes.c_void_p * p)(*[_addr(b) for b in recvbufs])
+    return lib().oracle_scan(op, dt, p, sendbufs[0].size, 1 if exclusive else 0, S, R)

@@ -379,9 +379,47 @@ int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
     return rc ? MPI_ERR_OP : MPI_SUCCESS;
 }
 
+/* MPI_Scan / MPI_Exscan as the reference runs them: the NBC task lists of
+ * IscanBuildTaskList (reduce.cpp:5285-5576) and IexscanBuildTaskList
+ * (:5671-5960) executed by NbcTask::ExecuteScan (tasks.cpp:694-766).
+ * partial = x_r (and recvbuf = x_r for Scan); for mask = 1, 2, ...:
+ * dst = r ^ mask (< p); the last step only goes from the lower to the higher
+ * rank.  rank > dst: Uop(tmp, partial); Uop(tmp, recvbuf), or recvbuf = tmp on
+ * Exscan's first such step (copyOnly).  rank < dst: Uop(tmp, partial).
+ * Exscan leaves rank 0's recvbuf untouched (undefined). */
 int oracle_scan(MPI_Op op, MPI_Datatype dt, int p, int64_t count, int exclusive,
                 const void* const* sendbufs, void* const* recvbufs)
 {
-    (void)op; (void)dt; (void)p; (void)count; (void)exclusive; (void)sendbufs; (void)recvbufs;
-    return MPI_ERR_INTERN;
+    if (oracle_op_check(op, dt) != MPI_SUCCESS) return MPI_ERR_OP;
+    if (count == 0 || p < 1) return MPI_SUCCESS;
+    const int64_t esz = oracle_kind_size(oracle_kind_of(dt));
+    const int64_t bytes = count * esz;
+    char** part = (char**)calloc((size_t)p, sizeof(char*));
+    char** snap = (char**)calloc((size_t)p, sizeof(char*));
+    char* tmp = (char*)malloc((size_t)bytes);
+    int* have = (int*)calloc((size_t)p, sizeof(int));
+    int rc = 0;
+    for (int r = 0; r < p; ++r) {
+        part[r] = (char*)malloc((size_t)bytes);
+        snap[r] = (char*)malloc((size_t)bytes);
+        memcpy(part[r], sendbufs[r], (size_t)bytes);
+        if (!exclusive) { memcpy(recvbufs[r], sendbufs[r], (size_t)bytes); have[r] = 1; }
+    }
+    for (int mask = 1; mask < p; mask <<= 1) {
+        const int last = (mask << 1) >= p;
+        for (int r = 0; r < p; ++r) memcpy(snap[r], part[r], (size_t)bytes);
+        for (int r = 0; r < p; ++r) {
+            const int dst = r ^ mask;
+            if (dst >= p || (last && r < dst)) continue;
+            memcpy(tmp, snap[dst], (size_t)bytes);
+            rc |= combine(op, dt, tmp, part[r], count);
+            if (r > dst) {
+                if (exclusive && !have[r]) { memcpy(recvbufs[r], tmp, (size_t)bytes); have[r] = 1; }
+                else rc |= combine(op, dt, tmp, recvbufs[r], count);
+            }
+        }
+    }
+    for (int r = 0; r < p; ++r) { free(part[r]); free(snap[r]); }
+    free(part); free(snap); free(tmp); free(have);
+    return rc ? MPI_ERR_OP : MPI_SUCCESS;
 }

@@ -312,3 +312,48 @@ def test_two_mpi_processes_bootstrap_and_user_op_allreduce():
         gpu = res[rk][1].rstrip().endswith("1")
         rc2 = int(res[rk][1].split()[-2])
         assert rc2 == (0 if gpu else C.MPI_ERR_OTHER)
+
+
+SCAN_WORKER = r'''
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
+import numpy as np
+import msx
+C = msx.C
+L = msx.init(errors_return=True)
+r = ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r))
+UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+def sub(a, b, n, dt):   # non-commutative, non-associative: inout = in - inout
+    x = np.ctypeslib.as_array((ctypes.c_double * n[0]).from_address(a))
+    y = np.ctypeslib.as_array((ctypes.c_double * n[0]).from_address(b))
+    y[:] = x - y
+fn = UF(sub)
+op = ctypes.c_int()
+assert L.MPI_Op_create(fn, 0, ctypes.byref(op)) == 0
+for f in (L.MPI_Scan, L.MPI_Exscan):
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+send = np.array([10.0 * (r.value + 1)] * 3, dtype=np.float64)
+inc, exc = np.zeros(3), np.full(3, 7.0)
+assert L.MPI_Scan(send.ctypes.data, inc.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD) == 0, msx.last_error()
+assert L.MPI_Exscan(send.ctypes.data, exc.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD) == 0
+print("OUT", r.value, inc[0], exc[0], flush=True)
+assert L.MPI_Finalize() == 0
+'''
+
+
+def test_four_mpi_processes_user_op_scan_follows_reference_task_order():
+    """A non-associative user op exposes the recursive-doubling association of
+    the reference's scan (IscanBuildTaskList, reduce.cpp:5285-5576): with
+    x = [10, 20, 30, 40] and a op b = a - b, rank 3 gets (x0-x1)-(x2-x3) = 0
+    (a sequential prefix would give -80) and Exscan rank 3 gets (x0-x1)-x2."""
+    port = _free_port()
+    outs = _spawn(SCAN_WORKER, 4, lambda r: {"MSX_SIZE": "4", "MSX_RANK": str(r),
+                                             "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1"})
+    got = {}
+    for rc, o, e in outs:
+        assert rc == 0, e[-3000:]
+        _, rk, inc, exc = [l for l in o.splitlines() if l.startswith("OUT")][0].split()
+        got[int(rk)] = (float(inc), float(exc))
+    assert [got[k][0] for k in range(4)] == [10.0, -10.0, -40.0, 0.0]
+    assert [got[k][1] for k in range(4)] == [7.0, 10.0, -10.0, -40.0]

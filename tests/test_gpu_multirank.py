@@ -123,6 +123,24 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 5000), ("MPI_SUM
         elif rank == root:
             check(f"reduce {opn} {dtn} {count} root={root}", fromdev(rb, xs[rank]), exp)
 
+# MPI_Scan / MPI_Exscan (recursive-doubling task lists of the reference)
+for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MAX", "MPI_FLOAT", 3000),
+                                       ("MPI_PROD", "MPI_DOUBLE_COMPLEX", 1000)]):
+    op, dt = getattr(C, opn), getattr(C, dtn)
+    xs = inputs(opn, dtn, count, 5000 + i)
+    for excl in (False, True):
+        exp = [raw(np.zeros_like(xs[0])) for _ in range(p)]
+        assert oracle.scan(op, dt, xs, exp, exclusive=excl) == 0
+        sb = todev(xs[rank])
+        rb = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+        fn = L.MPI_Exscan if excl else L.MPI_Scan
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        rc = fn(sb.data_ptr(), rb.data_ptr(), count, dt, op, C.MPI_COMM_WORLD)
+        if rc != 0:
+            fails.append(f"scan {opn} excl={excl} rc={rc} {msx.last_error()}")
+        elif not (excl and rank == 0):
+            check(f"scan {opn} {dtn} excl={excl}", fromdev(rb, xs[rank]), exp[rank])
+
 # MPI_Iallreduce BAND u64 (config 5 op/type) overlapped with host compute
 xs = inputs("MPI_BAND", "MPI_UINT64_T", 1 << 18, 4000)
 exp = [raw(x.copy()) for x in xs]

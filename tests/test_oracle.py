@@ -163,3 +163,25 @@ def test_oracle_allreduce_integer_any_p(p):
         exp = np.sum(np.stack(xs).astype(np.int64), axis=0).astype(np.int32)   # wraps mod 2^32
         for r in range(p):
             assert np.array_equal(rb[r], exp)
+
+
+def test_oracle_scan_association_fp32():
+    # recursive-doubling scan (IscanBuildTaskList reduce.cpp:5285-5576): rank 5 of 8
+    # ends with (x5+x4) + ((x1+x0) + (x3+x2)); Exscan rank 5: x4 + ((x1+x0) + (x3+x2))
+    rng = np.random.default_rng(21)
+    p, n = 8, 4096
+    xs = [(rng.standard_normal(n) * 10.0 ** rng.integers(-6, 7, n)).astype(np.float32) for _ in range(p)]
+    rb = [np.zeros(n, np.float32) for _ in range(p)]
+    assert oracle.scan(C.MPI_SUM, C.MPI_FLOAT, xs, rb) == 0
+    exp5 = (xs[5] + xs[4]) + ((xs[1] + xs[0]) + (xs[3] + xs[2]))
+    assert np.array_equal(rb[5].view(np.uint32), exp5.view(np.uint32))
+    ex = [np.full(n, 7.0, np.float32) for _ in range(p)]
+    assert oracle.scan(C.MPI_SUM, C.MPI_FLOAT, xs, ex, exclusive=True) == 0
+    assert np.array_equal(ex[5].view(np.uint32), (xs[4] + ((xs[1] + xs[0]) + (xs[3] + xs[2]))).view(np.uint32))
+    assert (ex[0] == 7.0).all()          # rank 0's Exscan result is undefined: left untouched
+    ints = [rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32) for _ in range(5)]
+    ri = [np.zeros(n, np.int32) for _ in range(5)]
+    assert oracle.scan(C.MPI_SUM, C.MPI_INT, ints, ri) == 0
+    cs = np.cumsum(np.stack(ints).astype(np.int64), axis=0).astype(np.int32)
+    for r in range(5):
+        assert np.array_equal(ri[r], cs[r])
