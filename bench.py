@@ -53,15 +53,18 @@ def parse():
     return ap.parse_args()
 
 
-def run_collectives_child(world, rank, local, scale):
-    """c3-c5 in a child MPI process per rank (isolated from the headline line)."""
+def run_collectives_child(world, rank, local, scale, transport="ipc"):
+    """c3-c5 in a child MPI process per rank (isolated from the headline line).
+    transport "ipc": IPC windows + xGMI remote writes; "rccl": RCCL send/recv."""
     import subprocess
     import tempfile
-    out = os.path.join(tempfile.gettempdir(), f"msx_coll_{os.environ.get('MASTER_PORT', '0')}.json")
+    out = os.path.join(tempfile.gettempdir(), f"msx_coll_{transport}_{os.environ.get('MASTER_PORT', '0')}.json")
     env = dict(os.environ)
+    off = 113 if transport == "ipc" else 127
     env.update({"MSX_SIZE": str(world), "MSX_RANK": str(rank), "MSX_DEVICE": str(local),
+                "MSX_TRANSPORT": transport,
                 "MSX_BOOTSTRAP_ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                "MSX_BOOTSTRAP_PORT": str((int(os.environ.get("MASTER_PORT", "29500")) + 113) % 65536),
+                "MSX_BOOTSTRAP_PORT": str((int(os.environ.get("MASTER_PORT", "29500")) + off) % 65536),
                 "MSX_BOOTSTRAP_TIMEOUT": "90",
                 "MSX_BENCH_LOG": os.environ.get("MSX_BENCH_LOG", os.devnull)})
     try:
@@ -79,6 +82,34 @@ def run_collectives_child(world, rank, local, scale):
         except OSError as e:
             return {"error": str(e)}
     return {}
+
+
+def rccl_native_allreduce(dist, torch, world, dev, scale):
+    """xGMI reference point: RCCL's own fp32 SUM allreduce (its ring/tree order,
+    NOT the reference's association) on c3's 1 GiB/rank, same GPUs."""
+    try:
+        g = dist.new_group(backend="nccl")
+        n = int((1 << 28) * scale)
+        x = torch.ones(n, device=dev)
+        for _ in range(2):
+            dist.all_reduce(x, group=g)
+        torch.cuda.synchronize()
+        dist.barrier()
+        reps, t0 = 5, time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(x, group=g)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+        alg = n * 4 / dt / 1e9
+        del x
+        torch.cuda.empty_cache()
+        return {"bytes_per_rank": n * 4, "seconds": round(dt, 5), "algbw_GB_s": round(alg, 2),
+                "busbw_GB_s": round(alg * 2 * (world - 1) / world, 2)}
+    except Exception as e:      # reported, never fatal for the headline line
+        return {"error": repr(e)[:300]}
 
 
 def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 1, 256, true, false>"):
@@ -226,14 +257,21 @@ def main():
 
     # N > 1: the collective configs c3-c5 in child MPI processes (not part of
     # `value`); each rank reports whether its child succeeded.
-    coll = None
+    coll = coll_rccl = rccl_native = None
+    distinct = torch.cuda.device_count() >= world      # one GPU per rank (RCCL needs it)
     if world > 1 and not args.no_collectives:
-        mine = run_collectives_child(world, rank, local, args.coll_scale)
-        ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        coll = mine if rank == 0 else None
-        if rank == 0 and not ok.item() and "error" not in coll:
-            coll["error"] = "a non-zero rank's child failed"
+        def collect(transport):
+            mine = run_collectives_child(world, rank, local, args.coll_scale, transport)
+            ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            res = mine if rank == 0 else None
+            if rank == 0 and not ok.item() and "error" not in res:
+                res["error"] = "a non-zero rank's child failed"
+            return res
+        coll = collect("ipc")
+        if distinct:
+            coll_rccl = collect("rccl")
+            rccl_native = rccl_native_allreduce(dist, torch, world, dev, args.coll_scale)
 
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
@@ -297,6 +335,10 @@ def main():
             out["host_path"] = host
         if coll is not None:
             out["collectives"] = coll
+        if coll_rccl is not None:
+            out["collectives_rccl_transport"] = coll_rccl
+        if rccl_native is not None:
+            out["rccl_native_allreduce_f32"] = rccl_native
         if sweep:
             out["variant_sweep_GB_s"] = sweep
         if world == 1:

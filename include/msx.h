@@ -37,6 +37,10 @@ extern "C" {
 const char* msx_version(void);
 /* number of visible GPUs (0 on a host without one); never aborts */
 int msx_device_count(void);
+/* data plane of the collective engine for MPI_COMM_WORLD: "rccl" (RCCL
+ * send/recv over xGMI, MSX_TRANSPORT=rccl and one GPU per rank), "ipc" (IPC
+ * windows + remote writes) or "self" (one rank) */
+const char* msx_engine_transport(void);
 /* text of the last error raised on the calling thread ("" if none) */
 const char* msx_last_error(void);
 

@@ -23,6 +23,7 @@
 
 #include "../../include/msx.h"
 #include "msx_comm.h"
+#include "msx_transport.h"
 #include "msx_kernels.h"
 #include "msx_runtime.h"
 #include "msx_types.h"
@@ -676,6 +677,12 @@ MSX_ALIAS(MPI_Op_commutative) int PMPI_Op_commutative(MPI_Op, int*);
 // device-side extension ABI (include/msx.h)
 // ===========================================================================
 MSX_EXPORT const char* msx_version(void) { return "msmpi-mi355x 0.1 (gfx950)"; }
+
+MSX_EXPORT const char* msx_engine_transport(void)
+{
+    Comm* c = world();
+    return engine_transport_name(c ? c->tp : nullptr);
+}
 MSX_EXPORT int msx_device_count(void) { return device_count_noinit(); }
 MSX_EXPORT const char* msx_last_error(void) { return last_error(); }
 

@@ -13,6 +13,7 @@
 #include "msx_transport.h"
 
 #include <arpa/inet.h>
+#include <dlfcn.h>
 #include <condition_variable>
 #include <algorithm>
 #include <deque>
@@ -29,9 +30,17 @@
 #include <stdlib.h>
 #include <string.h>
 #include <string>
+#include <atomic>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sched.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
 #include <thread>
 #include <unistd.h>
+
+#include <rccl/rccl.h>
 
 #include "msx_kernels.h"
 #include "msx_runtime.h"
@@ -179,6 +188,90 @@ private:
 };
 
 // ===========================================================================
+// node-local barrier in POSIX shared memory (all ranks of a communicator are
+// on one node: the IPC engine requires it).  Sense-reversing counter: a few
+// microseconds instead of a TCP round trip through the hub.
+// ===========================================================================
+struct ShmBar {
+    std::atomic<uint32_t> count;
+    std::atomic<uint32_t> gen;
+};
+
+class ShmBarrier {
+public:
+    ~ShmBarrier()
+    {
+        if (bar_) munmap(bar_, 4096);
+    }
+
+    // Collective over the hub.  Returns false (and stays unused) when shared
+    // memory is unavailable; the caller then keeps the hub barrier.
+    bool init(Hub& hub, int rank, int size, double timeout_s)
+    {
+        size_ = size;
+        timeout_ = timeout_s;
+        char name[64] = {0};
+        if (rank == 0) snprintf(name, sizeof(name), "/msx_bar_%d_%ld", (int)getpid(), (long)(now_s() * 1e6));
+        std::vector<char> all((size_t)size * sizeof(name));
+        if (hub.allgather(name, sizeof(name), all.data()) != MPI_SUCCESS) return false;
+        memcpy(name, all.data(), sizeof(name));
+        int ok = 1;
+        int fd = shm_open(name, rank == 0 ? (O_CREAT | O_RDWR) : O_RDWR, 0600);
+        if (rank == 0) {
+            if (fd < 0 || ftruncate(fd, 4096) != 0) ok = 0;
+        }
+        // rank 0 has sized the segment before anyone maps it
+        std::vector<int> oks((size_t)size);
+        if (hub.allgather(&ok, sizeof(int), oks.data()) != MPI_SUCCESS) ok = 0;
+        for (int v : oks) ok &= v;
+        void* m = MAP_FAILED;
+        if (ok && fd >= 0) m = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (fd >= 0) close(fd);
+        int mine = (m != MAP_FAILED) ? 1 : 0;
+        if (hub.allgather(&mine, sizeof(int), oks.data()) != MPI_SUCCESS) mine = 0;
+        bool all_ok = mine != 0;
+        for (int v : oks) all_ok = all_ok && v;
+        if (rank == 0) shm_unlink(name);
+        if (!all_ok) {
+            if (m != MAP_FAILED) munmap(m, 4096);
+            trace("shm barrier unavailable; hub barrier in use");
+            return false;
+        }
+        bar_ = static_cast<ShmBar*>(m);    // zero-filled by ftruncate
+        return true;
+    }
+
+    bool ready() const { return bar_ != nullptr; }
+
+    int wait()
+    {
+        const uint32_t g = bar_->gen.load(std::memory_order_acquire);
+        if (bar_->count.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)size_) {
+            bar_->count.store(0, std::memory_order_relaxed);
+            bar_->gen.store(g + 1, std::memory_order_release);
+            syscall(SYS_futex, reinterpret_cast<uint32_t*>(&bar_->gen), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+            return MPI_SUCCESS;
+        }
+        // short spin (the common case when ranks arrive together), then sleep
+        // in the kernel on the generation word
+        for (int it = 0; it < 4000; ++it)
+            if (bar_->gen.load(std::memory_order_acquire) != g) return MPI_SUCCESS;
+        const double t_end = now_s() + timeout_;
+        while (bar_->gen.load(std::memory_order_acquire) == g) {
+            if (now_s() > t_end) { set_error("barrier: timed out"); return MPI_ERR_OTHER; }
+            struct timespec ts = {0, 100 * 1000 * 1000};
+            syscall(SYS_futex, reinterpret_cast<uint32_t*>(&bar_->gen), FUTEX_WAIT, g, &ts, nullptr, 0);
+        }
+        return MPI_SUCCESS;
+    }
+
+private:
+    ShmBar* bar_ = nullptr;
+    int size_ = 1;
+    double timeout_ = 600.0;
+};
+
+// ===========================================================================
 // IPC transport
 // ===========================================================================
 struct IpcRec {
@@ -201,13 +294,19 @@ public:
     {
         rank = r;
         size = s;
-        return hub_.init(r, s);
+        int rc = hub_.init(r, s);
+        if (rc != MPI_SUCCESS) return rc;
+        double t = 600.0;
+        if (const char* v = getenv("MSX_BOOTSTRAP_TIMEOUT")) t = atof(v);
+        if (!getenv("MSX_NO_SHM_BARRIER")) (void)shm_.init(hub_, r, s, t);
+        return MPI_SUCCESS;
     }
 
     int allgather(const void* mine, size_t n, void* all) override { return hub_.allgather(mine, n, all); }
 
     int barrier() override
     {
+        if (shm_.ready()) return shm_.wait();
         char b = 0;
         std::vector<char> all((size_t)size);
         return hub_.allgather(&b, 1, all.data());
@@ -287,6 +386,7 @@ public:
 
 private:
     Hub hub_;
+    ShmBarrier shm_;
     hipStream_t stream_ = nullptr;
     std::map<std::string, void*> opened_;
     void* win_ = nullptr;
@@ -633,27 +733,33 @@ char* dev_scratch(size_t bytes)
     return p;
 }
 
-// ---- window-staged collectives ---------------------------------------------
-// Every rank owns one IPC-mapped device window of 4*C bytes: two slots, each an
-// IN half (this rank's staged input chunk) and an OUT half (this rank's
-// reduced part).  User buffers are never IPC-mapped (ROCm 7.2 hangs opening
-// handles of allocations > 2 GiB, and user memory may be host memory), so a
-// collective streams chunks of C bytes through the windows:
-//   stage  : my chunk of input -> IN(me, s)            (HBM copy / H2D)
-//   barrier A (every input chunk staged)
-//   reduce : my part of the chunk, reading IN(r, s) of every rank over xGMI,
-//            the reference's expression tree per element -> OUT(me, s)
-//   barrier B (every part reduced)            [allreduce only]
-//   gather : every rank's part OUT(r, s) -> my recvbuf  [allreduce only]
-// Slot s alternates; a rank syncs its stream before the next barrier, so a
-// slot is never rewritten while a peer still reads it.
+// ---- window collectives (push model) ----------------------------------------
+// Every rank owns one IPC-mapped device window of 2*C bytes: an IN area of p
+// sub-slots of Q = C/p bytes (sub-slot k receives rank k's contribution) and an
+// OUT area of C bytes (the reduced chunk, assembled from every owner's piece).
+// User buffers are never IPC-mapped (ROCm 7.2 hangs opening handles of
+// allocations > 2 GiB, and user memory may be host memory).  Data crosses
+// xGMI only as REMOTE WRITES (posted stores, all peer links at once);
+// reductions read local HBM only:
+//   scatter : piece r of my chunk -> IN(r)[sub-slot me]             (xGMI writes)
+//   barrier A (every contribution landed: writers synced before it)
+//   reduce  : my piece from IN(me)[0..p-1], the reference's expression tree
+//             per element -> OUT(me)[my piece]                        (local)
+//   push    : OUT(me)[my piece] -> OUT(r)[my piece], every r          (xGMI writes)
+//   barrier B (every piece landed)
+//   collect : OUT(me) -> recvbuf                                      (local / D2H)
+// One slot suffices: a peer scatters chunk i+1 into IN(me) only after barrier B
+// of chunk i (I finished reading IN(me) before it) and pushes into OUT(me)
+// only after barrier A of chunk i+1 (I collected chunk i before it).  After a
+// collective's last barrier B no peer touches my window, so the next
+// collective needs no extra barrier.
 size_t chunk_bytes()
 {
     static size_t c = [] {
-        size_t v = (size_t)256 << 20;
+        size_t v = (size_t)512 << 20;
         if (const char* e = getenv("MSX_CHUNK_BYTES")) v = (size_t)atoll(e);
         if (v < ((size_t)1 << 16)) v = (size_t)1 << 16;
-        if (v > ((size_t)480 << 20)) v = (size_t)480 << 20;   // window 4*C < 2 GiB
+        if (v > ((size_t)1000 << 20)) v = (size_t)1000 << 20;   // window 2*C < 2 GiB
         return v & ~(size_t)4095;
     }();
     return c;
@@ -661,15 +767,17 @@ size_t chunk_bytes()
 
 struct Windows {
     std::vector<char*> base;
-    size_t C = 0;
-    char* in(int r, int s) const { return base[(size_t)r] + (size_t)s * 2 * C; }
-    char* out(int r, int s) const { return base[(size_t)r] + (size_t)s * 2 * C + C; }
+    size_t C = 0, Q = 0;
+    char* in(int r) const { return base[(size_t)r]; }
+    char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * Q; }
+    char* out(int r) const { return base[(size_t)r] + C; }
 };
 
 int get_windows(Transport* tp, Windows* w)
 {
     w->C = chunk_bytes();
-    return tp->window(4 * w->C, w->base);
+    w->Q = (w->C / (size_t)tp->size) & ~(size_t)255;
+    return tp->window(2 * w->C, w->base);
 }
 
 int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
@@ -679,7 +787,321 @@ int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "stage copy");
 }
 
-// root < 0: allreduce; root >= 0: only `root` gathers the result (MPI_Reduce).
+// A batch of byte ranges moved by one k_copy_segs launch (one grid row each).
+struct Segs {
+    std::vector<const void*> src;
+    std::vector<void*> dst;
+    std::vector<size_t> n;
+    void add(const void* s, void* d, size_t bytes)
+    {
+        if (!bytes) return;
+        src.push_back(s);
+        dst.push_back(d);
+        n.push_back(bytes);
+    }
+    int run(hipStream_t s, const char* what)
+    {
+        if (src.empty()) return MPI_SUCCESS;
+        hipError_t e = launch_copy_segs(src.data(), dst.data(), n.data(), (int)src.size(), true, s);
+        return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
+    }
+};
+
+// Device view of `len` bytes of a user buffer at byte offset `off`: the buffer
+// itself when it is device memory, else staged into `stage` (H2D).
+int device_view(const BufInfo& b, const char* user, size_t off, size_t len, char* stage,
+                hipStream_t s, const char** out)
+{
+    if (b.place == Place::Device) {
+        *out = static_cast<const char*>(b.dev) + off;
+        return MPI_SUCCESS;
+    }
+    *out = stage;
+    return copy_async(stage, user + off, len, s);
+}
+
+// ---- RCCL plane (MSX_TRANSPORT=rccl) -------------------------------------------
+// The same reference-order trees, with the bytes moved by RCCL point-to-point
+// (ncclSend/ncclRecv groups over xGMI) instead of IPC windows: no host
+// barriers, no peer mappings, user device buffers sent and received in place,
+// everything ordered on the engine stream.  RCCL needs one GPU per rank; a
+// communicator whose ranks share a GPU keeps the IPC window engine.
+// librccl is opened lazily so the library has no link-time RCCL dependency.
+struct RcclApi {
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+    bool ok = false;
+};
+
+const RcclApi* rccl_api()
+{
+    static RcclApi a = [] {
+        RcclApi r;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return r;
+        r.get_id = reinterpret_cast<decltype(r.get_id)>(dlsym(h, "ncclGetUniqueId"));
+        r.init_rank = reinterpret_cast<decltype(r.init_rank)>(dlsym(h, "ncclCommInitRank"));
+        r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
+        r.send = reinterpret_cast<decltype(r.send)>(dlsym(h, "ncclSend"));
+        r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(h, "ncclRecv"));
+        r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+        r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+        r.err = reinterpret_cast<decltype(r.err)>(dlsym(h, "ncclGetErrorString"));
+        r.ok = r.get_id && r.init_rank && r.destroy && r.send && r.recv && r.group_start && r.group_end && r.err;
+        return r;
+    }();
+    return a.ok ? &a : nullptr;
+}
+
+bool rccl_requested()
+{
+    static const bool v = [] {
+        const char* e = getenv("MSX_TRANSPORT");
+        return e && strcmp(e, "rccl") == 0;
+    }();
+    return v;
+}
+
+std::map<Transport*, ncclComm_t> g_rccl_comms;
+
+// Communicator for `tp` (collective on first use; nullptr = use IPC windows).
+ncclComm_t rccl_comm(Transport* tp)
+{
+    auto& comms = g_rccl_comms;
+    static std::map<Transport*, bool> refused;
+    auto it = comms.find(tp);
+    if (it != comms.end()) return it->second;
+    if (refused.count(tp)) return nullptr;
+    const RcclApi* api = rccl_api();
+    // every rank must take the same decision: agree on (api ok, device identity)
+    struct Id { int32_t ok; int32_t dev; char bus[32]; };
+    Id mine;
+    memset(&mine, 0, sizeof(mine));
+    mine.ok = api ? 1 : 0;
+    (void)hipGetDevice(&mine.dev);
+    (void)hipDeviceGetPCIBusId(mine.bus, sizeof(mine.bus), mine.dev);
+    std::vector<Id> all((size_t)tp->size);
+    if (tp->allgather(&mine, sizeof(mine), all.data()) != MPI_SUCCESS) { refused[tp] = true; return nullptr; }
+    bool usable = true;
+    for (int r = 0; r < tp->size; ++r) {
+        usable = usable && all[r].ok;
+        for (int q = 0; q < r; ++q) usable = usable && strncmp(all[r].bus, all[q].bus, sizeof(all[r].bus)) != 0;
+    }
+    if (!usable) {
+        trace("rccl: not usable (library missing or ranks share a GPU); IPC windows in use");
+        refused[tp] = true;
+        return nullptr;
+    }
+    ncclUniqueId id;
+    memset(&id, 0, sizeof(id));
+    if (tp->rank == 0) api->get_id(&id);
+    std::vector<ncclUniqueId> ids((size_t)tp->size);
+    if (tp->allgather(&id, sizeof(id), ids.data()) != MPI_SUCCESS) { refused[tp] = true; return nullptr; }
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = api->init_rank(&comm, tp->size, ids[0], tp->rank);
+    trace("rccl: ncclCommInitRank rc=%d", (int)r);
+    if (r != ncclSuccess) {
+        set_error("ncclCommInitRank: %s", api->err(r));
+        refused[tp] = true;
+        return nullptr;
+    }
+    comms[tp] = comm;
+    return comm;
+}
+
+// One ncclGroupStart/End batch of sends and receives (bytes), stream-ordered.
+struct P2p {
+    struct Op { bool send; void* buf; size_t n; int peer; };
+    std::vector<Op> ops;
+    void send(const void* b, size_t n, int peer) { if (n) ops.push_back({true, const_cast<void*>(b), n, peer}); }
+    void recv(void* b, size_t n, int peer) { if (n) ops.push_back({false, b, n, peer}); }
+    int run(ncclComm_t comm, hipStream_t s, const char* what)
+    {
+        if (ops.empty()) return MPI_SUCCESS;
+        const RcclApi* api = rccl_api();
+        ncclResult_t r = api->group_start();
+        for (const Op& o : ops) {
+            if (r != ncclSuccess) break;
+            r = o.send ? api->send(o.buf, o.n, ncclUint8, o.peer, comm, s)
+                       : api->recv(o.buf, o.n, ncclUint8, o.peer, comm, s);
+        }
+        ncclResult_t r2 = api->group_end();
+        if (r == ncclSuccess) r = r2;
+        if (r != ncclSuccess) { set_error("%s: %s", what, api->err(r)); return MPI_ERR_OTHER; }
+        return MPI_SUCCESS;
+    }
+};
+
+int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf, size_t count,
+                   MPI_Datatype dt, const OpRef& op, int root)
+{
+    Transport* tp = c->tp;
+    const int p = c->size, me = c->rank;
+    const TypeInfo* ti = type_info(dt);
+    const Kind k = ti->kind;
+    const size_t esz = (size_t)ti->size;
+    hipStream_t s = tp->stream();
+    const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
+    char* dst = static_cast<char*>(recvbuf);
+    const bool want = (root < 0 || root == me);
+    const bool is_reduce = root >= 0;
+    const int algo = is_reduce ? reduce_algo(p, count, (int)esz, true)
+                               : allreduce_algo(p, count, (int)esz, true);
+    const BufInfo bs = classify(src), bd = classify(dst);
+    size_t qmax = (chunk_bytes() / (size_t)p) / esz;
+    qmax -= qmax % 16;
+    // scratch: [IN: p sub-slots of qmax][OUT: p*qmax][stage: p*qmax]
+    const size_t sub_b = qmax * esz, area = (size_t)p * sub_b;
+    char* scratch = dev_scratch(3 * area);
+    if (!scratch) { set_error("allreduce: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+    char* inb = scratch;
+    char* outb = scratch + area;
+    char* stage = scratch + 2 * area;
+    std::vector<char*> srcs((size_t)p);
+    const int pof2 = pof2_floor(p);
+    const int n = newrank_of(me, p);
+    const int lineage = n >= 0 ? n : newrank_of(me + 1, p);
+    int rc = MPI_SUCCESS;
+    trace("rccl allreduce: count=%zu algo=%d qmax=%zu", count, algo, qmax);
+    if (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) {
+        const RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
+        for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += qmax) {
+            const size_t len = std::min(qmax, count - o);
+            const char* mine = nullptr;
+            rc = device_view(bs, src, o * esz, len * esz, stage, s, &mine);
+            P2p x;
+            for (int r = 0; r < p; ++r) {
+                if (r == me) continue;
+                if (root < 0 || r == root) x.send(mine, len * esz, r);
+                if (want) x.recv(inb + (size_t)r * sub_b, len * esz, r);
+            }
+            if (rc == MPI_SUCCESS) rc = x.run(comm, s, "allreduce exchange");
+            if (rc == MPI_SUCCESS && want) {
+                for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(mine) : inb + (size_t)r * sub_b;
+                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz : outb;
+                rc = run_rank_tree(op.opidx, k, t, srcs, esz, 0, len, out, s);
+                if (rc == MPI_SUCCESS && out == outb) rc = copy_async(dst + o * esz, out, len * esz, s);
+            }
+        }
+        return rc == MPI_SUCCESS ? sync_stream(s, "allreduce") : rc;
+    }
+    const size_t ce = (size_t)p * qmax;
+    for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce) {
+        const size_t len = std::min(ce, count - o);
+        const size_t q = (len + p - 1) / p;
+        const size_t qv = (q + 15) & ~(size_t)15;
+        auto lo_of = [&](int r) { return std::min(len, (size_t)r * qv); };
+        auto hi_of = [&](int r) { return std::min(len, (size_t)(r + 1) * qv); };
+        const size_t plo = lo_of(me), phi = hi_of(me);
+        const char* mine = nullptr;
+        rc = device_view(bs, src, o * esz, len * esz, stage, s, &mine);
+        P2p x;                                        // reduce-scatter as all-to-all
+        for (int r = 0; r < p; ++r) {
+            if (r == me) continue;
+            x.send(mine + lo_of(r) * esz, (hi_of(r) - lo_of(r)) * esz, r);
+            x.recv(inb + (size_t)r * sub_b, (phi - plo) * esz, r);
+        }
+        if (rc == MPI_SUCCESS) rc = x.run(comm, s, "allreduce scatter");
+        for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(mine) + plo * esz : inb + (size_t)r * sub_b;
+        char* outp = (want && bd.place == Place::Device) ? static_cast<char*>(bd.dev) + o * esz : outb;
+        for (size_t e0 = plo; e0 < phi && rc == MPI_SUCCESS;) {
+            const size_t ge = o + e0;
+            const size_t rs = count / (size_t)pof2;
+            const int j = rs ? (int)std::min((size_t)pof2 - 1, ge / rs) : pof2 - 1;
+            size_t bst, bl;
+            allreduce_block(p, count, j, &bst, &bl);
+            const size_t e1 = std::min(phi, bst + bl - o);
+            const int owner = allreduce_block_owner(p, j);
+            const RankTree t = is_reduce ? tree_reduce_rsag(p, owner) : tree_allreduce(p, owner);
+            rc = run_rank_tree(op.opidx, k, t, srcs, esz, e0 - plo, e1 - e0, outp + e0 * esz, s);
+            e0 = e1;
+        }
+        P2p g;                                        // allgather (or gather at root)
+        for (int r = 0; r < p; ++r) {
+            if (r == me) continue;
+            if (root < 0 || r == root) g.send(outp + plo * esz, (phi - plo) * esz, r);
+            if (want) g.recv(outp + lo_of(r) * esz, (hi_of(r) - lo_of(r)) * esz, r);
+        }
+        if (rc == MPI_SUCCESS) rc = g.run(comm, s, "allreduce gather");
+        if (rc == MPI_SUCCESS && want && outp == outb) rc = copy_async(dst + o * esz, outb, len * esz, s);
+    }
+    return rc == MPI_SUCCESS ? sync_stream(s, "allreduce") : rc;
+}
+
+int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
+                        MPI_Datatype dt, const OpRef& op)
+{
+    Transport* tp = c->tp;
+    const int p = c->size, me = c->rank;
+    const size_t esz = (size_t)type_size(dt);
+    std::vector<size_t> disp((size_t)p + 1, 0);
+    size_t maxcnt = 0;
+    for (int r = 0; r < p; ++r) {
+        disp[r + 1] = disp[r] + (size_t)recvcounts[r];
+        maxcnt = std::max(maxcnt, (size_t)recvcounts[r]);
+    }
+    const size_t total = disp[p];
+    const bool in_place = (sendbuf == MPI_IN_PLACE);
+    const char* src = static_cast<const char*>(in_place ? recvbuf : sendbuf);
+    const Kind k = type_info(dt)->kind;
+    hipStream_t s = tp->stream();
+    size_t qe = (chunk_bytes() / (size_t)p) / esz;
+    qe -= qe % 16;
+    const int algo = reduce_scatter_algo(p, total, (int)esz, op.commutative);
+    const int n = newrank_of(me, p);
+    const RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
+                                               : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
+    const size_t mycnt = (size_t)recvcounts[me];
+    const BufInfo bs = classify(src), bd = classify(recvbuf);
+    char* dst = static_cast<char*>(recvbuf);
+    // scratch: [IN: p*qe][OUT: qe][stage: p*qe][hold: mycnt if in place]
+    const size_t sub_b = qe * esz, area = (size_t)p * sub_b;
+    const size_t hold_b = in_place ? mycnt * esz : 0;
+    char* scratch = dev_scratch(2 * area + sub_b + hold_b);
+    if (!scratch) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+    char* inb = scratch;
+    char* outb = scratch + area;
+    char* stage = outb + sub_b;
+    char* hold = stage + area;
+    std::vector<char*> srcs((size_t)p);
+    int rc = MPI_SUCCESS;
+    trace("rccl reduce_scatter: total=%zu algo=%d round=%zu", total, algo, qe);
+    for (size_t o = 0; o < maxcnt && rc == MPI_SUCCESS; o += qe) {
+        P2p x;
+        const char* myseg = nullptr;
+        for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
+            const size_t cnt = (size_t)recvcounts[r];
+            if (o >= cnt) continue;
+            const size_t len = std::min(qe, cnt - o);
+            const char* v = nullptr;
+            rc = device_view(bs, src, (disp[r] + o) * esz, len * esz, stage + (size_t)r * sub_b, s, &v);
+            if (r == me) myseg = v;
+            else x.send(v, len * esz, r);
+        }
+        const size_t len = o < mycnt ? std::min(qe, mycnt - o) : 0;
+        for (int r = 0; r < p; ++r)
+            if (r != me) x.recv(inb + (size_t)r * sub_b, len * esz, r);
+        if (rc == MPI_SUCCESS) rc = x.run(comm, s, "reduce_scatter exchange");
+        if (rc == MPI_SUCCESS && len) {
+            for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(myseg) : inb + (size_t)r * sub_b;
+            char* out = in_place ? hold + o * esz
+                                 : (bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz : outb);
+            rc = run_rank_tree(op.opidx, k, t, srcs, esz, 0, len, out, s);
+            if (rc == MPI_SUCCESS && out == outb) rc = copy_async(dst + o * esz, out, len * esz, s);
+        }
+    }
+    if (rc == MPI_SUCCESS && in_place && mycnt) rc = copy_async(recvbuf, hold, mycnt * esz, s);
+    return rc == MPI_SUCCESS ? sync_stream(s, "reduce_scatter") : rc;
+}
+
+// root < 0: allreduce; root >= 0: only `root` receives the result (MPI_Reduce).
 int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                  const OpRef& op, int root = -1)
 {
@@ -689,6 +1111,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     if (rc != MPI_SUCCESS) return rc;
 
     Transport* tp = c->tp;
+    if (rccl_requested())
+        if (ncclComm_t rcomm = rccl_comm(tp)) return rccl_allreduce(rcomm, c, sendbuf, recvbuf, count, dt, op, root);
     const int p = c->size, me = c->rank;
     const TypeInfo* ti = type_info(dt);
     const Kind k = ti->kind;
@@ -702,73 +1126,93 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                                : allreduce_algo(p, count, (int)esz, true);
     Windows w;
     if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
-    // chunk = whole 16-byte vectors of whole elements
-    size_t ce = w.C / esz;
-    ce -= ce % (16 / (esz < 16 ? esz : 16) ? 16 / (esz < 16 ? esz : 16) : 1);
+    const BufInfo bs = classify(src), bd = classify(dst);
+    // elements per sub-slot, whole 16-element granules
+    size_t qmax = w.Q / esz;
+    qmax -= qmax % 16;
+    if (qmax == 0) { set_error("allreduce: window too small"); return MPI_ERR_INTERN; }
+    char* stage = nullptr;
+    if (bs.place != Place::Device) {
+        stage = dev_scratch(std::min(count, (size_t)p * qmax) * esz);
+        if (!stage) { set_error("allreduce: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+    }
     const int pof2 = pof2_floor(p);
     const int n = newrank_of(me, p);
     const int lineage = n >= 0 ? n : newrank_of(me + 1, p);
-    trace("allreduce: count=%zu esz=%zu algo=%d chunk=%zu elems", count, esz, algo, ce);
+    std::vector<char*> subs((size_t)p);
+    for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r);
+    trace("allreduce: count=%zu esz=%zu algo=%d qmax=%zu", count, esz, algo, qmax);
 
-    std::vector<char*> ins((size_t)p), outs((size_t)p);
-    int slot = 0;
-    for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce, slot ^= 1) {
-        const size_t len = (count - o < ce) ? count - o : ce;
-        for (int r = 0; r < p; ++r) { ins[r] = w.in(r, slot); outs[r] = w.out(r, slot); }
-        if ((rc = copy_async(ins[me], src + o * esz, len * esz, s)) != MPI_SUCCESS) break;
-        if ((rc = sync_stream(s, "allreduce stage")) != MPI_SUCCESS) break;
-        if ((rc = tp->barrier()) != MPI_SUCCESS) break;                  // A
-        if (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) {
-            // recursive doubling: every rank evaluates its own lineage's tree on
-            // the whole chunk; binomial reduce: the root evaluates its tree
-            RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
-            if (want) rc = run_rank_tree(op.opidx, k, t, ins, esz, 0, len, outs[me], s);
-            if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, outs[me], len * esz, s);
-            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce chunk");
-            continue;
+    if (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) {
+        // every rank that evaluates a tree needs every contribution whole:
+        // recursive doubling -> all ranks evaluate their own lineage's tree;
+        // binomial reduce -> only the root evaluates
+        const RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
+        for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += qmax) {
+            const size_t len = std::min(qmax, count - o);
+            const char* mine = nullptr;
+            rc = device_view(bs, src, o * esz, len * esz, stage, s, &mine);
+            Segs sg;
+            for (int r = 0; r < p; ++r)
+                if (root < 0 || r == root) sg.add(mine, w.sub(r, me), len * esz);
+            if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
+            if (rc == MPI_SUCCESS) rc = tp->barrier();                              // A
+            if (rc == MPI_SUCCESS && want) {
+                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz : w.out(me);
+                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, len, out, s);
+                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst + o * esz, out, len * esz, s);
+                if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce tree");
+            }
+            if (rc == MPI_SUCCESS) rc = tp->barrier();                              // B
         }
-        // Rabenseifner order: element e of the vector belongs to block j(e),
-        // whose value the reference computes at newrank bitrev(j).  The chunk
-        // is split evenly over all p ranks (work balance only); each piece is
-        // evaluated with the tree of its block's owner.
+        trace("allreduce: done rc=%d", rc);
+        return rc;
+    }
+
+    // Rabenseifner order: element e belongs to block j(e), whose value the
+    // reference computes at newrank bitrev(j).  Each chunk is cut into p
+    // pieces (work balance only, 16-element granules); each element of a piece
+    // is evaluated with the tree of its block's owner.
+    const size_t ce = (size_t)p * qmax;
+    for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce) {
+        const size_t len = std::min(ce, count - o);
         const size_t q = (len + p - 1) / p;
-        const size_t qv = (q + 15) & ~(size_t)15;                        // 16-element granules
-        const size_t plo = std::min(len, (size_t)me * qv), phi = std::min(len, plo + qv);
+        const size_t qv = (q + 15) & ~(size_t)15;
+        auto lo_of = [&](int r) { return std::min(len, (size_t)r * qv); };
+        auto hi_of = [&](int r) { return std::min(len, (size_t)(r + 1) * qv); };
+        const char* mine = nullptr;
+        rc = device_view(bs, src, o * esz, len * esz, stage, s, &mine);
+        Segs scatter;
+        for (int r = 0; r < p; ++r)
+            scatter.add(mine + lo_of(r) * esz, w.sub(r, me), (hi_of(r) - lo_of(r)) * esz);
+        if (rc == MPI_SUCCESS) rc = scatter.run(s, "allreduce scatter");
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce scatter");
+        if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // A
+        if (rc != MPI_SUCCESS) break;
+        const size_t plo = lo_of(me), phi = hi_of(me);
         for (size_t e0 = plo; e0 < phi && rc == MPI_SUCCESS;) {
-            const size_t ge = o + e0;                                    // global element
+            const size_t ge = o + e0;                                             // global element
             const size_t rs = count / (size_t)pof2;
-            int j = rs ? (int)std::min((size_t)pof2 - 1, ge / rs) : pof2 - 1;
-            size_t bs, bl;
-            allreduce_block(p, count, j, &bs, &bl);
-            const size_t e1 = std::min(phi, bs + bl - o);
+            const int j = rs ? (int)std::min((size_t)pof2 - 1, ge / rs) : pof2 - 1;
+            size_t bst, bl;
+            allreduce_block(p, count, j, &bst, &bl);
+            const size_t e1 = std::min(phi, bst + bl - o);
             const int owner = allreduce_block_owner(p, j);
-            RankTree t = is_reduce ? tree_reduce_rsag(p, owner) : tree_allreduce(p, owner);
-            rc = run_rank_tree(op.opidx, k, t, ins, esz, e0, e1 - e0, outs[me] + e0 * esz, s);
+            const RankTree t = is_reduce ? tree_reduce_rsag(p, owner) : tree_allreduce(p, owner);
+            rc = run_rank_tree(op.opidx, k, t, subs, esz, e0 - plo, e1 - e0, w.out(me) + e0 * esz, s);
             e0 = e1;
         }
-        if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce reduce");
-        if (rc == MPI_SUCCESS) rc = tp->barrier();                       // B
-        if (rc != MPI_SUCCESS) break;
-        if (!want) continue;
-        // gather every part (peer OUT windows over xGMI) into recvbuf
-        const BufInfo bd = classify(dst);
-        char* gdst = (bd.place == Place::Device) ? static_cast<char*>(bd.dev) + o * esz : ins[me];
-        std::vector<const void*> gs;
-        std::vector<void*> gd;
-        std::vector<size_t> gn;
-        for (int r = 0; r < p; ++r) {
-            const size_t lo = std::min(len, (size_t)r * qv), hi = std::min(len, lo + qv);
-            if (hi <= lo) continue;
-            gs.push_back(outs[r] + lo * esz);
-            gd.push_back(gdst + lo * esz);
-            gn.push_back((hi - lo) * esz);
-        }
-        hipError_t e = launch_copy_segs(gs.data(), gd.data(), gn.data(), (int)gs.size(), true, s);
-        if (e != hipSuccess) { rc = hip_fail(e, "allreduce gather"); break; }
-        if (bd.place != Place::Device) rc = copy_async(dst + o * esz, gdst, len * esz, s);
-        if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce gather");
+        Segs push;
+        for (int r = 0; r < p; ++r)
+            if (r != me && (root < 0 || r == root))
+                push.add(w.out(me) + plo * esz, w.out(r) + plo * esz, (phi - plo) * esz);
+        if (rc == MPI_SUCCESS) rc = push.run(s, "allreduce push");
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
+        if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // B
+        if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, w.out(me), len * esz, s);
     }
-    if (rc == MPI_SUCCESS) rc = tp->barrier();   // windows free for the next collective
+    if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce collect");
     trace("allreduce: done rc=%d", rc);
     return rc;
 }
@@ -801,56 +1245,65 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
     }
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
+    if (rccl_requested())
+        if (ncclComm_t rcomm = rccl_comm(tp)) return rccl_reduce_scatter(rcomm, c, sendbuf, recvbuf, recvcounts, dt, op);
     const Kind k = type_info(dt)->kind;
     hipStream_t s = tp->stream();
     Windows w;
     if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
-    // IN slot holds p sub-chunks of `ce` elements, one per destination rank
-    size_t ce = w.C / esz / (size_t)p;
-    ce -= ce % 16;
-    if (ce == 0) ce = 1;
+    // sub-slot k of IN(r) receives rank k's contribution to r's block, qe
+    // elements per round
+    size_t qe = w.Q / esz;
+    qe -= qe % 16;
+    if (qe == 0) { set_error("reduce_scatter: window too small"); return MPI_ERR_INTERN; }
     const int algo = reduce_scatter_algo(p, total, (int)esz, op.commutative);
     const int n = newrank_of(me, p);
-    RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
-                                         : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
-    trace("reduce_scatter: total=%zu esz=%zu algo=%d chunk=%zu", total, esz, algo, ce);
+    const RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
+                                               : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
+    trace("reduce_scatter: total=%zu esz=%zu algo=%d round=%zu", total, esz, algo, qe);
     const size_t mycnt = (size_t)recvcounts[me];
-    const BufInfo bd = classify(recvbuf);
+    const BufInfo bs = classify(src), bd = classify(recvbuf);
     char* dst = static_cast<char*>(recvbuf);
-    std::vector<char*> ins((size_t)p);
-    char* hold = nullptr;
-    if (in_place && mycnt) {
-        hold = dev_scratch(mycnt * esz);
-        if (!hold) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+    // scratch: [hold: in-place results][stage: host-resident input pieces]
+    const size_t hold_b = in_place ? ((mycnt * esz + 255) & ~(size_t)255) : 0;
+    const size_t stage_b = bs.place == Place::Device ? 0 : (size_t)p * qe * esz;
+    char* scratch = nullptr;
+    if (hold_b + stage_b) {
+        scratch = dev_scratch(hold_b + stage_b);
+        if (!scratch) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
     }
-    int slot = 0;
-    for (size_t o = 0; o < maxcnt && rc == MPI_SUCCESS; o += ce, slot ^= 1) {
-        // stage, for every destination r, our contribution to r's block range [o, o+ce)
-        char* mine = w.in(me, slot);
+    char* hold = scratch;
+    char* stage = scratch ? scratch + hold_b : nullptr;
+    std::vector<char*> subs((size_t)p);
+    for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r);
+    for (size_t o = 0; o < maxcnt && rc == MPI_SUCCESS; o += qe) {
+        // my contribution to every destination's block range [o, o+qe)
+        Segs scatter;
         for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
             const size_t cnt = (size_t)recvcounts[r];
             if (o >= cnt) continue;
-            const size_t len = std::min(ce, cnt - o);
-            rc = copy_async(mine + (size_t)r * ce * esz, src + (disp[r] + o) * esz, len * esz, s);
+            const size_t len = std::min(qe, cnt - o);
+            const char* v = nullptr;
+            rc = device_view(bs, src, (disp[r] + o) * esz, len * esz, stage ? stage + (size_t)r * qe * esz : nullptr,
+                             s, &v);
+            scatter.add(v, w.sub(r, me), len * esz);
         }
-        if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter stage");
-        if (rc == MPI_SUCCESS) rc = tp->barrier();
+        if (rc == MPI_SUCCESS) rc = scatter.run(s, "reduce_scatter scatter");
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter scatter");
+        if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // A
         if (rc != MPI_SUCCESS) break;
         if (o < mycnt) {
-            const size_t len = std::min(ce, mycnt - o);
-            for (int r = 0; r < p; ++r) ins[r] = w.in(r, slot) + (size_t)me * ce * esz;
-            // In place, recvbuf is still our input for later chunks: results go
+            const size_t len = std::min(qe, mycnt - o);
+            // In place, recvbuf is still our input for later rounds: results go
             // to a private device scratch and are copied out at the end.
             char* out = in_place ? hold + o * esz
-                                 : (bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz
-                                                              : w.out(me, slot));
-            rc = run_rank_tree(op.opidx, k, t, ins, esz, 0, len, out, s);
-            if (rc == MPI_SUCCESS && out == w.out(me, slot))
-                rc = copy_async(dst + o * esz, out, len * esz, s);
+                                 : (bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz : w.out(me));
+            rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, len, out, s);
+            if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst + o * esz, out, len * esz, s);
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter reduce");
         }
-        if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter reduce");
+        if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // B
     }
-    if (rc == MPI_SUCCESS) rc = tp->barrier();   // every rank finished reading the windows
     if (rc == MPI_SUCCESS && in_place && mycnt) {
         rc = copy_async(recvbuf, hold, mycnt * esz, s);
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter result");
@@ -858,7 +1311,6 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
     trace("reduce_scatter: done rc=%d", rc);
     return rc;
 }
-
 }  // namespace
 
 // ---- public engine entry points --------------------------------------------
@@ -978,8 +1430,11 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
     Windows w;
     if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
-    size_t ce = w.C / esz;
+    // partials staged in two alternating halves of IN(me): a peer may still be
+    // reading step i's partial while step i+1's is staged
+    size_t ce = w.C / 2 / esz;
     ce -= ce % 16;
+    if (ce == 0) { set_error("scan: window too small"); return MPI_ERR_INTERN; }
     char* partial = dev_scratch(2 * bytes + 256);
     if (!partial) { set_error("scan: scratch allocation failed"); return MPI_ERR_NO_MEM; }
     char* res = partial + ((bytes + 255) & ~(size_t)255);
@@ -994,12 +1449,12 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
         const bool use = dst < p && !(last && me < dst);     // this rank consumes dst's partial
         for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce, slot ^= 1) {
             const size_t len = std::min(ce, count - o);
-            char* stage = w.in(me, slot);
+            char* stage = w.in(me) + (size_t)slot * (w.C / 2);
             rc = copy_async(stage, partial + o * esz, len * esz, s);       // partial at step start
             if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan stage");
             if (rc == MPI_SUCCESS) rc = tp->barrier();
             if (rc != MPI_SUCCESS || !use) continue;
-            const char* tmp = w.in(dst, slot);
+            const char* tmp = w.in(dst) + (size_t)slot * (w.C / 2);
             char* pp = partial + o * esz;
             char* rr = res + o * esz;
             if (me > dst) {
@@ -1027,6 +1482,12 @@ int engine_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_D
                 const OpRef& op, bool exclusive)
 {
     return worker().submit([=] { return do_scan(c, sendbuf, recvbuf, count, dt, op, exclusive); }).get();
+}
+
+const char* engine_transport_name(Transport* tp)
+{
+    if (!tp) return "self";
+    return worker().submit([tp]() -> int { return g_rccl_comms.count(tp) ? 1 : 0; }).get() ? "rccl" : "ipc";
 }
 
 std::shared_future<int> engine_async(std::function<int()> fn) { return worker().submit(std::move(fn)); }

@@ -37,6 +37,8 @@ public:
 };
 
 int transport_create(int rank, int size, Transport** out);
+// data plane the engine uses for `tp`: "rccl", "ipc" or "self" (size 1)
+const char* engine_transport_name(Transport* tp);
 void transport_destroy(Transport* t);
 
 // ---- schedules (pure functions; exported for host-side tests) ----------------

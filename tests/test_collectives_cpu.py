@@ -337,6 +337,11 @@ send = np.array([10.0 * (r.value + 1)] * 3, dtype=np.float64)
 inc, exc = np.zeros(3), np.full(3, 7.0)
 assert L.MPI_Scan(send.ctypes.data, inc.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD) == 0, msx.last_error()
 assert L.MPI_Exscan(send.ctypes.data, exc.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD) == 0
+import time
+t0 = time.perf_counter()
+for _ in range(500):                       # node-local shared-memory barrier
+    assert L.MPI_Barrier(C.MPI_COMM_WORLD) == 0
+print("BARRIER_US", (time.perf_counter() - t0) / 500 * 1e6, flush=True)
 print("OUT", r.value, inc[0], exc[0], flush=True)
 assert L.MPI_Finalize() == 0
 '''

@@ -161,6 +161,8 @@ else:
     check("iallreduce band u64", fromdev(rb, xs[rank]), exp[rank])
 assert req.value == C.MPI_REQUEST_NULL
 
+L.msx_engine_transport.restype = ctypes.c_char_p
+print("TRANSPORT", L.msx_engine_transport().decode(), flush=True)
 print("RESULT", rank, p, len(fails), fails[:5], flush=True)
 L.MPI_Finalize()
 '''
@@ -174,8 +176,9 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("p,chunk", [(2, None), (3, 65536), (4, 1 << 20), (5, None)])
-def test_collectives_p_ranks_on_one_gpu(p, chunk):
+@pytest.mark.parametrize("p,chunk,transport", [(2, None, None), (3, 65536, None), (4, 1 << 20, None),
+                                               (5, None, None), (3, 65536, "rccl")])
+def test_collectives_p_ranks_on_one_gpu(p, chunk, transport):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -188,6 +191,8 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk):
                     "MSX_BOOTSTRAP_TIMEOUT": "180"})
         if chunk:
             env["MSX_CHUNK_BYTES"] = str(chunk)     # many chunks, pieces across block edges
+        if transport:
+            env["MSX_TRANSPORT"] = transport
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
@@ -203,3 +208,7 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk):
         line = [l for l in o.splitlines() if l.startswith("RESULT")]
         assert line, (o + e)[-3000:]
         assert line[0].split()[3] == "0", line[0]
+        used = [l.split()[1] for l in o.splitlines() if l.startswith("TRANSPORT")]
+        # RCCL needs one GPU per rank: ranks sharing a GPU keep the IPC engine
+        n_dev = torch.cuda.device_count()
+        assert used == ["rccl" if transport == "rccl" and n_dev >= p else "ipc"], used
