@@ -233,6 +233,12 @@ MPI_METHOD MPI_Exscan(const void* sendbuf, void* recvbuf, int count,
 MPI_METHOD MPI_Iallreduce(const void* sendbuf, void* recvbuf, int count,
                           MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
                           MPI_Request* request);
+MPI_METHOD MPI_Iscan(const void* sendbuf, void* recvbuf, int count,
+                     MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                     MPI_Request* request);
+MPI_METHOD MPI_Iexscan(const void* sendbuf, void* recvbuf, int count,
+                       MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                       MPI_Request* request);
 MPI_METHOD MPI_Ireduce(const void* sendbuf, void* recvbuf, int count,
                        MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
                        MPI_Request* request);
@@ -263,6 +269,25 @@ MPI_METHOD PMPI_Reduce_scatter(const void* sendbuf, void* recvbuf, const int rec
 MPI_METHOD PMPI_Iallreduce(const void* sendbuf, void* recvbuf, int count,
                            MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
                            MPI_Request* request);
+MPI_METHOD PMPI_Iscan(const void* sendbuf, void* recvbuf, int count,
+                      MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                      MPI_Request* request);
+MPI_METHOD PMPI_Iexscan(const void* sendbuf, void* recvbuf, int count,
+                        MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                        MPI_Request* request);
+MPI_METHOD PMPI_Scan(const void* sendbuf, void* recvbuf, int count,
+                     MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD PMPI_Exscan(const void* sendbuf, void* recvbuf, int count,
+                       MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+MPI_METHOD PMPI_Ireduce(const void* sendbuf, void* recvbuf, int count,
+                        MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
+                        MPI_Request* request);
+MPI_METHOD PMPI_Ireduce_scatter_block(const void* sendbuf, void* recvbuf, int recvcount,
+                                      MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                                      MPI_Request* request);
+MPI_METHOD PMPI_Ireduce_scatter(const void* sendbuf, void* recvbuf, const int recvcounts[],
+                                MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                                MPI_Request* request);
 MPI_METHOD PMPI_Op_create(MPI_User_function* user_fn, int commute, MPI_Op* op);
 MPI_METHOD PMPI_Op_free(MPI_Op* op);
 MPI_METHOD PMPI_Op_commutative(MPI_Op op, int* commute);

@@ -500,12 +500,19 @@ MSX_EXPORT int MPI_Reduce_scatter_block(const void* sendbuf, void* recvbuf, int 
 
 namespace {
 
+// request == nullptr: blocking MPI_(Ex)scan; else MPI_I(ex)scan
+// (api/mpi_reduce.cpp:1920-2068 validate like the blocking forms)
 int scan_common(const char* fn, const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
-                MPI_Op op, MPI_Comm comm, bool exclusive)
+                MPI_Op op, MPI_Comm comm, bool exclusive, MPI_Request* request = nullptr,
+                bool nonblocking = false)
 {
     Comm* c;
     OpRef r;
     int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && nonblocking) {
+        if (request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
+        else *request = MPI_REQUEST_NULL;
+    }
     if (rc == MPI_SUCCESS) rc = v_dtype(recvbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
     if (rc == MPI_SUCCESS && count > 0) {
@@ -515,8 +522,14 @@ int scan_common(const char* fn, const void* sendbuf, void* recvbuf, int count, M
             if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
         }
     }
-    if (rc == MPI_SUCCESS && count > 0)
+    if (rc == MPI_SUCCESS && nonblocking) {
+        const size_t n = (size_t)count;
+        rc = request_start_generic(c, [=] {
+            return n ? coll_scan(c, sendbuf, recvbuf, n, datatype, r, exclusive) : MPI_SUCCESS;
+        }, request);
+    } else if (rc == MPI_SUCCESS && count > 0) {
         rc = coll_scan(c, sendbuf, recvbuf, (size_t)count, datatype, r, exclusive);
+    }
     return err_return(c, fn, rc);
 }
 
@@ -534,6 +547,20 @@ MSX_EXPORT int MPI_Exscan(const void* sendbuf, void* recvbuf, int count, MPI_Dat
 {
     MSX_REQUIRE_INIT("MPI_Exscan");
     return scan_common("MPI_Exscan", sendbuf, recvbuf, count, datatype, op, comm, true);
+}
+
+MSX_EXPORT int MPI_Iscan(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                         MPI_Op op, MPI_Comm comm, MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Iscan");
+    return scan_common("MPI_Iscan", sendbuf, recvbuf, count, datatype, op, comm, false, request, true);
+}
+
+MSX_EXPORT int MPI_Iexscan(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
+                           MPI_Op op, MPI_Comm comm, MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Iexscan");
+    return scan_common("MPI_Iexscan", sendbuf, recvbuf, count, datatype, op, comm, true, request, true);
 }
 
 // ---- non-blocking variants: stream-ordered requests -----------------------
@@ -669,6 +696,15 @@ MSX_ALIAS(MPI_Allreduce) int PMPI_Allreduce(const void*, void*, int, MPI_Datatyp
 MSX_ALIAS(MPI_Reduce_scatter_block) int PMPI_Reduce_scatter_block(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);
 MSX_ALIAS(MPI_Reduce_scatter) int PMPI_Reduce_scatter(const void*, void*, const int[], MPI_Datatype, MPI_Op, MPI_Comm);
 MSX_ALIAS(MPI_Iallreduce) int PMPI_Iallreduce(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm, MPI_Request*);
+MSX_ALIAS(MPI_Iscan) int PMPI_Iscan(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm, MPI_Request*);
+MSX_ALIAS(MPI_Iexscan) int PMPI_Iexscan(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm, MPI_Request*);
+MSX_ALIAS(MPI_Scan) int PMPI_Scan(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);
+MSX_ALIAS(MPI_Exscan) int PMPI_Exscan(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);
+MSX_ALIAS(MPI_Ireduce) int PMPI_Ireduce(const void*, void*, int, MPI_Datatype, MPI_Op, int, MPI_Comm, MPI_Request*);
+MSX_ALIAS(MPI_Ireduce_scatter_block) int PMPI_Ireduce_scatter_block(const void*, void*, int, MPI_Datatype, MPI_Op,
+                                                                    MPI_Comm, MPI_Request*);
+MSX_ALIAS(MPI_Ireduce_scatter) int PMPI_Ireduce_scatter(const void*, void*, const int*, MPI_Datatype, MPI_Op,
+                                                        MPI_Comm, MPI_Request*);
 MSX_ALIAS(MPI_Op_create) int PMPI_Op_create(MPI_User_function*, int, MPI_Op*);
 MSX_ALIAS(MPI_Op_free) int PMPI_Op_free(MPI_Op*);
 MSX_ALIAS(MPI_Op_commutative) int PMPI_Op_commutative(MPI_Op, int*);

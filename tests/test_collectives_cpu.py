@@ -333,10 +333,20 @@ op = ctypes.c_int()
 assert L.MPI_Op_create(fn, 0, ctypes.byref(op)) == 0
 for f in (L.MPI_Scan, L.MPI_Exscan):
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+for f in (L.MPI_Iscan, L.MPI_Iexscan):
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_void_p]
 send = np.array([10.0 * (r.value + 1)] * 3, dtype=np.float64)
 inc, exc = np.zeros(3), np.full(3, 7.0)
 assert L.MPI_Scan(send.ctypes.data, inc.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD) == 0, msx.last_error()
 assert L.MPI_Exscan(send.ctypes.data, exc.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD) == 0
+# non-blocking forms give the same results
+inc2, exc2, req = np.zeros(3), np.full(3, 7.0), ctypes.c_int()
+assert L.MPI_Iscan(send.ctypes.data, inc2.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD, ctypes.byref(req)) == 0
+assert L.MPI_Wait(ctypes.byref(req), None) == 0 and req.value == C.MPI_REQUEST_NULL
+assert L.MPI_Iexscan(send.ctypes.data, exc2.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD, ctypes.byref(req)) == 0
+assert L.MPI_Wait(ctypes.byref(req), None) == 0
+assert (inc2 == inc).all() and (exc2 == exc).all()
 import time
 t0 = time.perf_counter()
 for _ in range(500):                       # node-local shared-memory barrier

@@ -140,6 +140,18 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
             fails.append(f"scan {opn} excl={excl} rc={rc} {msx.last_error()}")
         elif not (excl and rank == 0):
             check(f"scan {opn} {dtn} excl={excl}", fromdev(rb, xs[rank]), exp[rank])
+        # MPI_Iscan / MPI_Iexscan: same task order, completed in MPI_Wait
+        rb2 = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+        req = ctypes.c_int()
+        fi = L.MPI_Iexscan if excl else L.MPI_Iscan
+        rc = fi(ctypes.c_void_p(sb.data_ptr()), ctypes.c_void_p(rb2.data_ptr()), count, dt, op, C.MPI_COMM_WORLD,
+                ctypes.byref(req))
+        if rc == 0:
+            rc = L.MPI_Wait(ctypes.byref(req), None)
+        if rc != 0:
+            fails.append(f"iscan {opn} excl={excl} rc={rc} {msx.last_error()}")
+        elif not (excl and rank == 0):
+            check(f"iscan {opn} {dtn} excl={excl}", fromdev(rb2, xs[rank]), exp[rank])
 
 # MPI_Iallreduce BAND u64 (config 5 op/type) overlapped with host compute
 xs = inputs("MPI_BAND", "MPI_UINT64_T", 1 << 18, 4000)
