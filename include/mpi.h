@@ -49,8 +49,17 @@ extern "C" {
 #define MPI_ERR_IN_STATUS   17
 #define MPI_ERR_PENDING     18
 #define MPI_ERR_REQUEST     19
+#define MPI_ERR_INFO        28
 #define MPI_ERR_NO_MEM      34
 #define MPI_ERR_NOT_SAME    35
+#define MPI_ERR_WIN         45
+#define MPI_ERR_BASE        46
+#define MPI_ERR_LOCKTYPE    47
+#define MPI_ERR_RMA_CONFLICT 49
+#define MPI_ERR_RMA_SYNC    50
+#define MPI_ERR_SIZE        51
+#define MPI_ERR_DISP        52
+#define MPI_ERR_ASSERT      53
 #define MPI_ERR_LASTCODE    0x3fffffff
 
 #define MPI_MAX_ERROR_STRING 512
@@ -255,6 +264,45 @@ MPI_METHOD MPI_Test(MPI_Request* request, int* flag, MPI_Status* status);
 MPI_METHOD MPI_Waitall(int count, MPI_Request array_of_requests[],
                        MPI_Status array_of_statuses[]);
 
+/* ---- one-sided communication, fence synchronisation (mpi.h:394-395,
+ *      434, 500, 5246-5250; api/mpi_win.cpp, api/mpi_rma.cpp) ------------- */
+typedef int MPI_Win;
+#define MPI_WIN_NULL        ((MPI_Win)0x20000000)
+typedef int MPI_Info;
+#define MPI_INFO_NULL       ((MPI_Info)0x1c000000)
+#define MPI_PROC_NULL       (-1)
+#define MPI_MODE_NOCHECK    1024
+#define MPI_MODE_NOSTORE    2048
+#define MPI_MODE_NOPUT      4096
+#define MPI_MODE_NOPRECEDE  8192
+#define MPI_MODE_NOSUCCEED 16384
+
+MPI_METHOD MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info info,
+                          MPI_Comm comm, MPI_Win* win);
+MPI_METHOD MPI_Win_free(MPI_Win* win);
+MPI_METHOD MPI_Win_fence(int assert, MPI_Win win);
+MPI_METHOD MPI_Win_set_errhandler(MPI_Win win, MPI_Errhandler errhandler);
+MPI_METHOD MPI_Win_get_errhandler(MPI_Win win, MPI_Errhandler* errhandler);
+MPI_METHOD MPI_Put(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                   int target_rank, MPI_Aint target_disp, int target_count,
+                   MPI_Datatype target_datatype, MPI_Win win);
+MPI_METHOD MPI_Get(void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                   int target_rank, MPI_Aint target_disp, int target_count,
+                   MPI_Datatype target_datatype, MPI_Win win);
+MPI_METHOD MPI_Accumulate(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                          int target_rank, MPI_Aint target_disp, int target_count,
+                          MPI_Datatype target_datatype, MPI_Op op, MPI_Win win);
+MPI_METHOD MPI_Get_accumulate(const void* origin_addr, int origin_count,
+                              MPI_Datatype origin_datatype, void* result_addr, int result_count,
+                              MPI_Datatype result_datatype, int target_rank, MPI_Aint target_disp,
+                              int target_count, MPI_Datatype target_datatype, MPI_Op op,
+                              MPI_Win win);
+MPI_METHOD MPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Datatype datatype,
+                            int target_rank, MPI_Aint target_disp, MPI_Op op, MPI_Win win);
+MPI_METHOD MPI_Compare_and_swap(const void* origin_addr, const void* compare_addr,
+                                void* result_addr, MPI_Datatype datatype, int target_rank,
+                                MPI_Aint target_disp, MPI_Win win);
+
 /* ---- profiling interface aliases (msmpi.def:101-102,422-423,478-483,...) -- */
 MPI_METHOD PMPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
                              MPI_Datatype datatype, MPI_Op op);
@@ -288,6 +336,17 @@ MPI_METHOD PMPI_Ireduce_scatter_block(const void* sendbuf, void* recvbuf, int re
 MPI_METHOD PMPI_Ireduce_scatter(const void* sendbuf, void* recvbuf, const int recvcounts[],
                                 MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
                                 MPI_Request* request);
+MPI_METHOD PMPI_Accumulate(const void* origin_addr, int origin_count,
+                           MPI_Datatype origin_datatype, int target_rank, MPI_Aint target_disp,
+                           int target_count, MPI_Datatype target_datatype, MPI_Op op,
+                           MPI_Win win);
+MPI_METHOD PMPI_Get_accumulate(const void* origin_addr, int origin_count,
+                               MPI_Datatype origin_datatype, void* result_addr, int result_count,
+                               MPI_Datatype result_datatype, int target_rank,
+                               MPI_Aint target_disp, int target_count,
+                               MPI_Datatype target_datatype, MPI_Op op, MPI_Win win);
+MPI_METHOD PMPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Datatype datatype,
+                             int target_rank, MPI_Aint target_disp, MPI_Op op, MPI_Win win);
 MPI_METHOD PMPI_Op_create(MPI_User_function* user_fn, int commute, MPI_Op* op);
 MPI_METHOD PMPI_Op_free(MPI_Op* op);
 MPI_METHOD PMPI_Op_commutative(MPI_Op op, int* commute);

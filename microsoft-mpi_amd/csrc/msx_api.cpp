@@ -66,6 +66,11 @@ const char* class_string(int cls)
     case MPI_ERR_INTERN: return "Internal MPI error";
     case MPI_ERR_REQUEST: return "Invalid MPI_Request";
     case MPI_ERR_NO_MEM: return "Out of memory";
+    case MPI_ERR_INFO: return "Invalid info argument";
+    case MPI_ERR_WIN: return "Invalid win argument";
+    case MPI_ERR_RMA_SYNC: return "Wrong synchronization of RMA calls";
+    case MPI_ERR_SIZE: return "Invalid size argument";
+    case MPI_ERR_DISP: return "Invalid disp argument";
     default: return "Unknown error class";
     }
 }
@@ -87,11 +92,9 @@ void not_initialized_exit(const char* fn)
 
 // MPIR_Err_return_comm (mpid/error.cpp:85-134): default handler is the one on
 // MPI_COMM_WORLD; ERRORS_ARE_FATAL aborts the job.
-int err_return(Comm* c, const char* fn, int code)
+int err_return_h(MPI_Errhandler h, const char* fn, int code)
 {
     if (code == MPI_SUCCESS) return code;
-    if (c == nullptr) c = world();
-    MPI_Errhandler h = c ? c->errhandler : MPI_ERRORS_ARE_FATAL;
     if (h == MPI_ERRORS_ARE_FATAL) {
         const char* detail = last_error();
         fprintf(stderr, "Fatal error in %s: %s, error stack:\n%s  %s\n", fn, class_string(code),
@@ -100,6 +103,13 @@ int err_return(Comm* c, const char* fn, int code)
         exit(code);
     }
     return code;
+}
+
+int err_return(Comm* c, const char* fn, int code)
+{
+    if (code == MPI_SUCCESS) return code;
+    if (c == nullptr) c = world();
+    return err_return_h(c ? c->errhandler : MPI_ERRORS_ARE_FATAL, fn, code);
 }
 
 // MpiaCommValidateHandle
@@ -705,9 +715,309 @@ MSX_ALIAS(MPI_Ireduce_scatter_block) int PMPI_Ireduce_scatter_block(const void*,
                                                                     MPI_Comm, MPI_Request*);
 MSX_ALIAS(MPI_Ireduce_scatter) int PMPI_Ireduce_scatter(const void*, void*, const int*, MPI_Datatype, MPI_Op,
                                                         MPI_Comm, MPI_Request*);
+MSX_ALIAS(MPI_Accumulate) int PMPI_Accumulate(const void*, int, MPI_Datatype, int, MPI_Aint, int, MPI_Datatype,
+                                              MPI_Op, MPI_Win);
+MSX_ALIAS(MPI_Get_accumulate) int PMPI_Get_accumulate(const void*, int, MPI_Datatype, void*, int, MPI_Datatype, int,
+                                                      MPI_Aint, int, MPI_Datatype, MPI_Op, MPI_Win);
+MSX_ALIAS(MPI_Fetch_and_op) int PMPI_Fetch_and_op(const void*, void*, MPI_Datatype, int, MPI_Aint, MPI_Op, MPI_Win);
 MSX_ALIAS(MPI_Op_create) int PMPI_Op_create(MPI_User_function*, int, MPI_Op*);
 MSX_ALIAS(MPI_Op_free) int PMPI_Op_free(MPI_Op*);
 MSX_ALIAS(MPI_Op_commutative) int PMPI_Op_commutative(MPI_Op, int*);
+
+// ===========================================================================
+// one-sided communication (api/mpi_win.cpp, api/mpi_rma.cpp), fence epochs
+// ===========================================================================
+namespace {
+
+std::mutex g_win_mu;
+std::vector<RmaWin*> g_wins;          // direct handles 0xA0000000 | index
+constexpr int kWinKindBits = 0xA0000000;
+
+// MpiaWinValidateHandle
+int v_win(MPI_Win h, RmaWin** out)
+{
+    *out = nullptr;
+    if (h == MPI_WIN_NULL) { set_error("null window"); return MPI_ERR_WIN; }
+    std::lock_guard<std::mutex> g(g_win_mu);
+    const unsigned idx = (unsigned)h & 0x03ffffffu;
+    if (((unsigned)h & 0xfc000000u) != (unsigned)kWinKindBits || idx >= g_wins.size() || !g_wins[idx]) {
+        set_error("invalid window 0x%x", h);
+        return MPI_ERR_WIN;
+    }
+    *out = g_wins[idx];
+    return MPI_SUCCESS;
+}
+
+int err_win(RmaWin* w, const char* fn, int code)
+{
+    if (code == MPI_SUCCESS) return code;
+    // MPIR_Err_return_win (mpid/error.cpp:142-151): a window without an
+    // error handler of its own reports through MPI_COMM_WORLD's
+    if (!w || w->errhandler == MPI_ERRHANDLER_NULL) return err_return(nullptr, fn, code);
+    return err_return_h(w->errhandler, fn, code);
+}
+
+// target datatype checks (MpiaDatatypeValidate with MPI_IN_PLACE as buffer),
+// the displacement and the rank, in the order of mpi_rma.cpp:697-735
+int v_target(RmaWin* w, int target_count, MPI_Datatype target_dt, int target_rank, MPI_Aint target_disp)
+{
+    int rc = v_dtype(MPI_IN_PLACE, target_count, target_dt);
+    if (rc != MPI_SUCCESS) return rc;
+    if (target_disp < 0) { set_error("negative target displacement"); return MPI_ERR_DISP; }
+    if (target_rank != MPI_PROC_NULL && (target_rank < 0 || target_rank >= w->comm->size)) {
+        set_error("invalid target rank %d", target_rank);
+        return MPI_ERR_RANK;
+    }
+    return MPI_SUCCESS;
+}
+
+// Predefined datatypes only: the signatures of origin and target must be the
+// same basic type and count (derived datatypes are out of scope).
+int v_match(int ocount, MPI_Datatype odt, int tcount, MPI_Datatype tdt)
+{
+    if (odt != tdt) { set_error("origin and target datatypes differ (0x%x, 0x%x)", odt, tdt); return MPI_ERR_TYPE; }
+    if (ocount != tcount) { set_error("origin and target counts differ (%d, %d)", ocount, tcount); return MPI_ERR_COUNT; }
+    return MPI_SUCCESS;
+}
+
+// Queue a remote operation, or apply it now when the target is this rank
+// (win.cpp:1570-1590: MPIDI_Win_local_accumulate / MPIR_Localcopy).
+int rma_issue(RmaWin* w, RmaKind kind, int target, MPI_Aint disp, int count, MPI_Datatype dt, int opidx,
+              const void* origin, void* result, const void* compare)
+{
+    RmaDesc d;
+    d.kind = kind;
+    d.target = target;
+    d.opidx = opidx;
+    d.dt = dt;
+    d.count = count;
+    d.tdisp = (int64_t)disp * w->disp_units[(size_t)target];    // the TARGET's disp_unit
+    RmaLocal l;
+    l.origin = origin;
+    l.result = result;
+    l.compare = compare;
+    if (target == w->comm->rank) return rma_apply_self(w, d, l);
+    w->q.push_back(d);
+    w->ql.push_back(l);
+    return MPI_SUCCESS;
+}
+
+int rma_op(MPI_Op op, OpRef* r, bool allow_noop)
+{
+    int rc = v_op_handle(op, r);       // MpiaOpValidate(rmaOp = true): handle only
+    if (rc != MPI_SUCCESS) return rc;
+    if (!allow_noop && r->opidx == O_NOOP) { set_error("MPI_NO_OP not allowed"); return MPI_ERR_OP; }
+    if (r->opidx == O_NULL) {
+        // do_accumulate_op: **opnotpredefined (packethandling.cpp:2934-2937)
+        set_error("user-defined operations are not allowed in RMA");
+        return MPI_ERR_OP;
+    }
+    return MPI_SUCCESS;
+}
+
+}  // namespace
+
+MSX_EXPORT int MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info info, MPI_Comm comm,
+                              MPI_Win* win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_create");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && info != MPI_INFO_NULL) { set_error("only MPI_INFO_NULL is supported"); rc = MPI_ERR_INFO; }
+    if (rc == MPI_SUCCESS && size < 0) { set_error("negative window size"); rc = MPI_ERR_SIZE; }
+    if (rc == MPI_SUCCESS && disp_unit <= 0) { set_error("disp_unit must be positive"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS && win == nullptr) { set_error("null win"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Win_create", rc);
+    auto* w = new RmaWin();
+    w->comm = c;
+    w->base = static_cast<char*>(base);
+    w->size = size;
+    w->disp_unit = disp_unit;
+    rc = engine_rma_create(w);
+    if (rc != MPI_SUCCESS) {
+        delete w;
+        return err_return(c, "MPI_Win_create", rc);
+    }
+    std::lock_guard<std::mutex> g(g_win_mu);
+    size_t idx = 0;
+    while (idx < g_wins.size() && g_wins[idx]) ++idx;
+    if (idx == g_wins.size()) g_wins.push_back(nullptr);
+    g_wins[idx] = w;
+    w->handle = kWinKindBits | (int)idx;
+    *win = w->handle;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Win_free(MPI_Win* win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_free");
+    if (!win) { set_error("null win"); return err_return(nullptr, "MPI_Win_free", MPI_ERR_ARG); }
+    RmaWin* w;
+    int rc = v_win(*win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_free", rc);
+    if (!w->q.empty()) { set_error("MPI_Win_free with operations pending (no closing fence)"); return err_win(w, "MPI_Win_free", MPI_ERR_RMA_SYNC); }
+    rc = coll_barrier(w->comm);       // every rank is done with the window
+    if (rc != MPI_SUCCESS) return err_win(w, "MPI_Win_free", rc);
+    {
+        std::lock_guard<std::mutex> g(g_win_mu);
+        g_wins[(size_t)(*win & 0x03ffffff)] = nullptr;
+    }
+    delete w;
+    *win = MPI_WIN_NULL;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Win_fence(int assert_, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_fence");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_fence", rc);
+    (void)assert_;                    // hints only
+    return err_win(w, "MPI_Win_fence", engine_rma_fence(w));
+}
+
+MSX_EXPORT int MPI_Win_set_errhandler(MPI_Win win, MPI_Errhandler eh)
+{
+    MSX_REQUIRE_INIT("MPI_Win_set_errhandler");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc == MPI_SUCCESS && eh != MPI_ERRORS_ARE_FATAL && eh != MPI_ERRORS_RETURN) {
+        set_error("unsupported errhandler 0x%x", eh);
+        rc = MPI_ERR_ARG;
+    }
+    if (rc != MPI_SUCCESS) return err_win(w, "MPI_Win_set_errhandler", rc);
+    w->errhandler = eh;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Win_get_errhandler(MPI_Win win, MPI_Errhandler* eh)
+{
+    MSX_REQUIRE_INIT("MPI_Win_get_errhandler");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc == MPI_SUCCESS && !eh) rc = MPI_ERR_ARG;
+    if (rc != MPI_SUCCESS) return err_win(w, "MPI_Win_get_errhandler", rc);
+    *eh = w->errhandler == MPI_ERRHANDLER_NULL ? MPI_ERRORS_ARE_FATAL : w->errhandler;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Put(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype, int target_rank,
+                       MPI_Aint target_disp, int target_count, MPI_Datatype target_datatype, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Put");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Put", rc);
+    rc = v_dtype(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = rma_issue(w, RMA_PUT, target_rank, target_disp, origin_count, origin_datatype, O_REPLACE, origin_addr,
+                       nullptr, nullptr);
+    return err_win(w, "MPI_Put", rc);
+}
+
+MSX_EXPORT int MPI_Get(void* origin_addr, int origin_count, MPI_Datatype origin_datatype, int target_rank,
+                       MPI_Aint target_disp, int target_count, MPI_Datatype target_datatype, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Get");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Get", rc);
+    rc = v_dtype(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = rma_issue(w, RMA_GET, target_rank, target_disp, origin_count, origin_datatype, O_NOOP, nullptr,
+                       origin_addr, nullptr);
+    return err_win(w, "MPI_Get", rc);
+}
+
+MSX_EXPORT int MPI_Accumulate(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                              int target_rank, MPI_Aint target_disp, int target_count,
+                              MPI_Datatype target_datatype, MPI_Op op, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Accumulate");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Accumulate", rc);
+    OpRef r;
+    rc = v_dtype(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = rma_op(op, &r, false);
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = rma_issue(w, RMA_ACC, target_rank, target_disp, origin_count, origin_datatype, r.opidx, origin_addr,
+                       nullptr, nullptr);
+    return err_win(w, "MPI_Accumulate", rc);
+}
+
+MSX_EXPORT int MPI_Get_accumulate(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                                  void* result_addr, int result_count, MPI_Datatype result_datatype,
+                                  int target_rank, MPI_Aint target_disp, int target_count,
+                                  MPI_Datatype target_datatype, MPI_Op op, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Get_accumulate");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Get_accumulate", rc);
+    OpRef r;
+    rc = v_op_handle(op, &r);
+    const bool noop = rc == MPI_SUCCESS && r.opidx == O_NOOP;
+    if (rc == MPI_SUCCESS && !noop) rc = v_dtype(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype(result_addr, result_count, result_datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS) rc = rma_op(op, &r, true);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && result_count > 0) {
+        rc = v_match(result_count, result_datatype, target_count, target_datatype);
+        if (rc == MPI_SUCCESS && !noop) rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    }
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && target_count > 0)
+        rc = rma_issue(w, noop ? RMA_GET : RMA_GACC, target_rank, target_disp, target_count, target_datatype,
+                       r.opidx, origin_addr, result_addr, nullptr);
+    return err_win(w, "MPI_Get_accumulate", rc);
+}
+
+MSX_EXPORT int MPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Datatype datatype,
+                                int target_rank, MPI_Aint target_disp, MPI_Op op, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Fetch_and_op");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Fetch_and_op", rc);
+    OpRef r;
+    rc = v_op_handle(op, &r);
+    const bool noop = rc == MPI_SUCCESS && r.opidx == O_NOOP;
+    if (rc == MPI_SUCCESS && !noop) rc = v_dtype(origin_addr, 1, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype(result_addr, 1, datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, 1, datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS) rc = rma_op(op, &r, true);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL)
+        rc = rma_issue(w, noop ? RMA_GET : RMA_GACC, target_rank, target_disp, 1, datatype, r.opidx, origin_addr,
+                       result_addr, nullptr);
+    return err_win(w, "MPI_Fetch_and_op", rc);
+}
+
+MSX_EXPORT int MPI_Compare_and_swap(const void* origin_addr, const void* compare_addr, void* result_addr,
+                                    MPI_Datatype datatype, int target_rank, MPI_Aint target_disp, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Compare_and_swap");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Compare_and_swap", rc);
+    rc = v_dtype(origin_addr, 1, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype(compare_addr, 1, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype(result_addr, 1, datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, 1, datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL)
+        rc = rma_issue(w, RMA_CAS, target_rank, target_disp, 1, datatype, O_REPLACE, origin_addr, result_addr,
+                       compare_addr);
+    return err_win(w, "MPI_Compare_and_swap", rc);
+}
 
 // ===========================================================================
 // device-side extension ABI (include/msx.h)

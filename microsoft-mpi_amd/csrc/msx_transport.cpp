@@ -1484,6 +1484,254 @@ int engine_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_D
     return worker().submit([=] { return do_scan(c, sendbuf, recvbuf, count, dt, op, exclusive); }).get();
 }
 
+// ===========================================================================
+// one-sided accumulate: target-side application at the fence
+// ===========================================================================
+namespace {
+
+// target = target (op) origin for `d.count` elements at taddr; the reference's
+// do_accumulate_op / MPIDI_Win_local_accumulate (packethandling.cpp:2917-2960,
+// win.cpp:1405-1450).  An (op, type) pair outside the op's table reaches
+// MPIR_Op_<op>, which only sets op_errno (op.cpp:1791) and leaves the target
+// unchanged; nothing reports it, so neither do we.
+int rma_combine(const RmaDesc& d, const char* payload, char* taddr, hipStream_t s)
+{
+    if (d.opidx == O_NOOP || d.count == 0) return MPI_SUCCESS;
+    const size_t bytes = (size_t)d.count * (size_t)type_size(d.dt);
+    if (d.opidx == O_REPLACE) return copy_async(taddr, payload, bytes, s);
+    if (op_check_dtype(d.opidx, d.dt) != MPI_SUCCESS) return MPI_SUCCESS;
+    const Kind k = type_info(d.dt)->kind;
+    if (classify(taddr).place == Place::Device && classify(payload).place == Place::Device)
+        return combine2(d.opidx, k, taddr, payload, taddr, (size_t)d.count, s);
+    int rc = sync_stream(s, "rma");
+    return rc == MPI_SUCCESS ? reduce_local_any(d.opidx, k, payload, taddr, (size_t)d.count) : rc;
+}
+
+// compare-and-swap of one element (bitwise compare, win.cpp:1909-1990)
+int rma_cas(const RmaDesc& d, const char* origin, const char* cmp, char* taddr, char* fetch, hipStream_t s)
+{
+    const size_t esz = (size_t)type_size(d.dt);
+    int rc = sync_stream(s, "rma cas");
+    char old[16], c[16];
+    if (rc == MPI_SUCCESS) rc = copy_any(old, taddr, esz);
+    if (rc == MPI_SUCCESS) rc = copy_any(c, cmp, esz);
+    if (rc == MPI_SUCCESS && fetch) rc = copy_any(fetch, old, esz);
+    if (rc == MPI_SUCCESS && memcmp(old, c, esz) == 0) rc = copy_any(taddr, origin, esz);
+    return rc;
+}
+
+// One operation on window memory `taddr` of this rank.  `fetch` receives the
+// target's previous contents (GET / GACC / CAS).
+int rma_apply(const RmaDesc& d, const char* payload, const char* cmp, char* taddr, char* fetch, hipStream_t s)
+{
+    const size_t bytes = (size_t)d.count * (size_t)type_size(d.dt);
+    switch (d.kind) {
+    case RMA_PUT: return copy_async(taddr, payload, bytes, s);
+    case RMA_GET: return copy_async(fetch, taddr, bytes, s);
+    case RMA_ACC: return rma_combine(d, payload, taddr, s);
+    case RMA_GACC: {
+        int rc = copy_async(fetch, taddr, bytes, s);
+        return rc == MPI_SUCCESS ? rma_combine(d, payload, taddr, s) : rc;
+    }
+    case RMA_CAS: return rma_cas(d, payload, cmp, taddr, fetch, s);
+    default: set_error("rma: bad operation kind %d", d.kind); return MPI_ERR_INTERN;
+    }
+}
+
+bool rma_in_bounds(const RmaDesc& d, int64_t winsize)
+{
+    const int64_t esz = type_size(d.dt);
+    const int64_t n = (d.kind == RMA_CAS) ? 1 : d.count;
+    if (d.tdisp < 0 || n < 0 || esz <= 0) return false;
+    if (n > (INT64_MAX - d.tdisp) / esz) return false;
+    return d.tdisp + n * esz <= winsize;
+}
+
+hipStream_t rma_self_stream()
+{
+    static hipStream_t s = [] {
+        hipStream_t t = nullptr;
+        (void)hipStreamCreateWithFlags(&t, hipStreamNonBlocking);
+        return t;
+    }();
+    return s;
+}
+
+// A slice [lo, hi) of one queued operation, staged through the engine
+// windows: payload in the target's IN area, fetched bytes in the origin's OUT.
+struct RmaPiece {
+    int origin;
+    int64_t idx;           // index in the origin's queue
+    int64_t lo, hi;        // element range
+    size_t in_off, out_off;
+    size_t in_b, out_b;
+};
+
+int do_rma_fence(RmaWin* win)
+{
+    Comm* c = win->comm;
+    Transport* tp = c->tp;
+    const int p = c->size, me = c->rank;
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    // 1. every origin's queue, on every rank (same order everywhere)
+    int64_t mine = (int64_t)win->q.size();
+    std::vector<int64_t> ns((size_t)p);
+    if ((rc = tp->allgather(&mine, sizeof(mine), ns.data())) != MPI_SUCCESS) return rc;
+    int64_t maxn = 0;
+    for (int64_t v : ns) maxn = std::max(maxn, v);
+    trace("rma fence: %lld local ops, max %lld", (long long)mine, (long long)maxn);
+    if (maxn == 0) return tp->barrier();
+    std::vector<RmaDesc> padded((size_t)maxn), all((size_t)p * (size_t)maxn);
+    std::copy(win->q.begin(), win->q.end(), padded.begin());
+    if ((rc = tp->allgather(padded.data(), (size_t)maxn * sizeof(RmaDesc), all.data())) != MPI_SUCCESS) return rc;
+    Windows w;
+    if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
+    const size_t C = w.C;
+    // 2. cut operations into pieces and pack them into rounds; a target
+    //    applies its pieces in (origin, issue) order, round after round
+    std::vector<std::vector<RmaPiece>> rounds(1);
+    std::vector<size_t> in_used((size_t)p, 0), out_used((size_t)p, 0);
+    int my_err = MPI_SUCCESS;
+    for (int o = 0; o < p; ++o) {
+        for (int64_t i = 0; i < ns[o]; ++i) {
+            const RmaDesc& d = all[(size_t)o * maxn + i];
+            if (!rma_in_bounds(d, win->sizes[(size_t)d.target])) {
+                // packethandling.cpp:1339-1383: **requestrmaoutofbounds
+                if (o == me) {
+                    my_err = MPI_ERR_REQUEST;
+                    set_error("RMA operation outside the target window (target %d, disp %lld)", d.target,
+                              (long long)d.tdisp);
+                }
+                continue;
+            }
+            const size_t esz = (size_t)type_size(d.dt);
+            const int64_t n = (d.kind == RMA_CAS) ? 1 : d.count;
+            const bool sends = d.kind == RMA_PUT || d.kind == RMA_CAS || ((d.kind == RMA_ACC || d.kind == RMA_GACC) && d.opidx != O_NOOP);
+            const bool fetches = d.kind == RMA_GET || d.kind == RMA_GACC || d.kind == RMA_CAS;
+            int64_t per = (int64_t)(C / esz / 2) & ~(int64_t)15;
+            if (per <= 0) per = 1;
+            for (int64_t lo = 0; lo < n || (n == 0 && lo == 0); lo += per) {
+                if (n == 0) break;
+                const int64_t hi = std::min(n, lo + per);
+                RmaPiece pc;
+                pc.origin = o;
+                pc.idx = i;
+                pc.lo = lo;
+                pc.hi = hi;
+                pc.in_b = sends ? (size_t)(hi - lo) * esz * (d.kind == RMA_CAS ? 2 : 1) : 0;
+                pc.out_b = fetches ? (size_t)(hi - lo) * esz : 0;
+                const size_t ia = (pc.in_b + 255) & ~(size_t)255, oa = (pc.out_b + 255) & ~(size_t)255;
+                if (in_used[(size_t)d.target] + ia > C || out_used[(size_t)o] + oa > C) {
+                    rounds.emplace_back();
+                    std::fill(in_used.begin(), in_used.end(), 0);
+                    std::fill(out_used.begin(), out_used.end(), 0);
+                }
+                pc.in_off = in_used[(size_t)d.target];
+                pc.out_off = out_used[(size_t)o];
+                in_used[(size_t)d.target] += ia;
+                out_used[(size_t)o] += oa;
+                rounds.back().push_back(pc);
+            }
+        }
+    }
+    hipStream_t s = tp->stream();
+    for (const auto& round : rounds) {
+        // a. origins write payloads into the targets' IN areas (xGMI writes)
+        for (const RmaPiece& pc : round) {
+            if (pc.origin != me || !pc.in_b) continue;
+            const RmaDesc& d = all[(size_t)me * maxn + pc.idx];
+            const RmaLocal& l = win->ql[(size_t)pc.idx];
+            const size_t esz = (size_t)type_size(d.dt);
+            char* dst = w.in(d.target) + pc.in_off;
+            if (d.kind == RMA_CAS) {
+                rc = copy_async(dst, l.origin, esz, s);
+                if (rc == MPI_SUCCESS) rc = copy_async(dst + esz, l.compare, esz, s);
+            } else {
+                rc = copy_async(dst, static_cast<const char*>(l.origin) + pc.lo * esz, pc.in_b, s);
+            }
+            if (rc != MPI_SUCCESS) return rc;
+        }
+        if ((rc = sync_stream(s, "rma payload")) != MPI_SUCCESS) return rc;
+        if ((rc = tp->barrier()) != MPI_SUCCESS) return rc;
+        // b. targets apply in (origin, issue) order; fetched bytes go to the
+        //    origin's OUT area
+        for (const RmaPiece& pc : round) {
+            const RmaDesc& d0 = all[(size_t)pc.origin * maxn + pc.idx];
+            if (d0.target != me) continue;
+            const size_t esz = (size_t)type_size(d0.dt);
+            RmaDesc d = d0;
+            d.count = (d0.kind == RMA_CAS) ? 1 : pc.hi - pc.lo;
+            char* taddr = win->base + d0.tdisp + pc.lo * (int64_t)esz;
+            const char* payload = w.in(me) + pc.in_off;
+            char* fetch = pc.out_b ? w.out(pc.origin) + pc.out_off : nullptr;
+            rc = rma_apply(d, payload, payload + esz, taddr, fetch, s);
+            if (rc != MPI_SUCCESS) return rc;
+        }
+        if ((rc = sync_stream(s, "rma apply")) != MPI_SUCCESS) return rc;
+        if ((rc = tp->barrier()) != MPI_SUCCESS) return rc;
+        // c. origins deliver fetched values to their result buffers
+        for (const RmaPiece& pc : round) {
+            if (pc.origin != me || !pc.out_b) continue;
+            const RmaDesc& d = all[(size_t)me * maxn + pc.idx];
+            const size_t esz = (size_t)type_size(d.dt);
+            rc = copy_async(static_cast<char*>(win->ql[(size_t)pc.idx].result) + pc.lo * esz,
+                            w.out(me) + pc.out_off, pc.out_b, s);
+            if (rc != MPI_SUCCESS) return rc;
+        }
+        if ((rc = sync_stream(s, "rma deliver")) != MPI_SUCCESS) return rc;
+    }
+    win->q.clear();
+    win->ql.clear();
+    trace("rma fence: %zu rounds done", rounds.size());
+    return my_err;
+}
+
+}  // namespace
+
+int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l)
+{
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    if (!rma_in_bounds(d, w->size)) {
+        set_error("RMA operation outside the window (disp %lld)", (long long)d.tdisp);
+        return MPI_ERR_REQUEST;
+    }
+    hipStream_t s = rma_self_stream();
+    rc = rma_apply(d, static_cast<const char*>(l.origin), static_cast<const char*>(l.compare),
+                   w->base + d.tdisp, static_cast<char*>(l.result), s);
+    return rc == MPI_SUCCESS ? sync_stream(s, "rma self") : rc;
+}
+
+int engine_rma_create(RmaWin* w)
+{
+    Comm* c = w->comm;
+    const int p = c->size;
+    w->sizes.assign((size_t)p, 0);
+    w->disp_units.assign((size_t)p, 1);
+    if (p == 1 || !c->tp) {
+        w->sizes[0] = w->size;
+        w->disp_units[0] = w->disp_unit;
+        return MPI_SUCCESS;
+    }
+    return worker().submit([w, c, p] {
+        int64_t mine[2] = {w->size, (int64_t)w->disp_unit};
+        std::vector<int64_t> all((size_t)p * 2);
+        int rc = c->tp->allgather(mine, sizeof(mine), all.data());
+        for (int r = 0; rc == MPI_SUCCESS && r < p; ++r) {
+            w->sizes[(size_t)r] = all[(size_t)r * 2];
+            w->disp_units[(size_t)r] = (int)all[(size_t)r * 2 + 1];
+        }
+        return rc;
+    }).get();
+}
+
+int engine_rma_fence(RmaWin* w)
+{
+    if (w->comm->size == 1 || !w->comm->tp) return MPI_SUCCESS;   // all operations were local
+    return worker().submit([w] { return do_rma_fence(w); }).get();
+}
+
 const char* engine_transport_name(Transport* tp)
 {
     if (!tp) return "self";

@@ -89,6 +89,45 @@ int engine_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int
                           MPI_Datatype dt, const OpRef& op);
 int engine_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                 const OpRef& op, bool exclusive);
+// ---- one-sided accumulate (MPI_Win, fence synchronisation) -------------------
+// Reference: mpid/win.cpp (MPID_Win_queue, MPIDI_Win_local_accumulate
+// :1405-1450) and the target-side apply of mpid/packethandling.cpp
+// (do_accumulate_op :2917-3000): remote operations are queued at the origin
+// and applied by the TARGET, `target = target op origin` through the op table.
+enum RmaKind : int32_t { RMA_PUT = 0, RMA_GET = 1, RMA_ACC = 2, RMA_GACC = 3, RMA_CAS = 4 };
+struct RmaDesc {                 // exchanged at synchronisation (plain data)
+    int32_t kind = -1;
+    int32_t target = -1;
+    int32_t opidx = 0;           // builtin op index (O_REPLACE / O_NOOP allowed)
+    int32_t dt = 0;              // MPI_Datatype
+    int64_t count = 0;           // elements
+    int64_t tdisp = 0;           // byte offset in the target's window
+};
+struct RmaLocal {                // origin-side addresses of a queued operation
+    const void* origin = nullptr;
+    void* result = nullptr;
+    const void* compare = nullptr;
+};
+struct RmaWin {
+    int handle = 0;
+    Comm* comm = nullptr;
+    char* base = nullptr;
+    int64_t size = 0;
+    int disp_unit = 1;
+    std::vector<int64_t> sizes;  // every rank's window size in bytes
+    std::vector<int> disp_units; // every rank's disp_unit
+    MPI_Errhandler errhandler = MPI_ERRHANDLER_NULL;   // unset: MPI_COMM_WORLD's handler
+    std::vector<RmaDesc> q;      // queued remote operations, issue order
+    std::vector<RmaLocal> ql;
+};
+// Apply one operation on this rank's own window memory now (target == self,
+// as the reference does, win.cpp:1570-1590); blocking.
+int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l);
+// MPI_Win_fence: every queued operation of every origin is applied at its
+// target in (origin rank, issue) order; fetched values are delivered.  Collective.
+int engine_rma_fence(RmaWin* w);
+int engine_rma_create(RmaWin* w);    // exchange window sizes (collective)
+
 // Run `fn` on the collective worker thread, after every collective issued
 // before it (MPI issue order); re-entrant calls from the worker run inline.
 std::shared_future<int> engine_async(std::function<int()> fn);

@@ -85,6 +85,22 @@ def lib():
         "MPI_Iallreduce": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
         "MPI_Ireduce": (i, [p, p, i, i, i, i, i, ctypes.POINTER(i)]),
         "MPI_Ireduce_scatter_block": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Scan": (i, [p, p, i, i, i, i]),
+        "MPI_Exscan": (i, [p, p, i, i, i, i]),
+        "MPI_Iscan": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Iexscan": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Win_create": (i, [p, i64, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Win_free": (i, [ctypes.POINTER(i)]),
+        "MPI_Win_fence": (i, [i, i]),
+        "MPI_Win_set_errhandler": (i, [i, i]),
+        "MPI_Win_get_errhandler": (i, [i, ctypes.POINTER(i)]),
+        "MPI_Put": (i, [p, i, i, i, i64, i, i, i]),
+        "MPI_Get": (i, [p, i, i, i, i64, i, i, i]),
+        "MPI_Accumulate": (i, [p, i, i, i, i64, i, i, i, i]),
+        "MPI_Get_accumulate": (i, [p, i, i, p, i, i, i, i64, i, i, i, i]),
+        "MPI_Fetch_and_op": (i, [p, p, i, i, i64, i, i]),
+        "MPI_Compare_and_swap": (i, [p, p, p, i, i, i64, i]),
+        "msx_engine_transport": (ctypes.c_char_p, []),
         "MPI_Wait": (i, [ctypes.POINTER(i), p]),
         "MPI_Test": (i, [ctypes.POINTER(i), ctypes.POINTER(i), p]),
         "MPI_Wtime": (ctypes.c_double, []),

@@ -152,3 +152,47 @@ def test_errors_are_fatal_by_default_and_require_init():
         print("not reached")
     """)
     assert r.returncode != 0 and "before initializing" in r.stderr
+
+
+def test_rma_window_validation(msxlib):
+    """MPI_Win_create / MPI_Put / MPI_Accumulate argument checks in the order of
+    api/mpi_win.cpp:96-170 and api/mpi_rma.cpp:640-735 (no GPU needed)."""
+    L = msxlib
+    buf = np.zeros(64, np.int32)
+    win = ctypes.c_int()
+    assert L.MPI_Win_create(buf.ctypes.data, -1, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(win)) == C.MPI_ERR_SIZE
+    assert L.MPI_Win_create(buf.ctypes.data, 256, 0, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(win)) == C.MPI_ERR_ARG
+    assert L.MPI_Win_create(buf.ctypes.data, 256, 4, 0x1c000001, C.MPI_COMM_WORLD, ctypes.byref(win)) == C.MPI_ERR_INFO
+    assert L.MPI_Win_create(buf.ctypes.data, 256, 4, C.MPI_INFO_NULL, C.MPI_COMM_NULL, ctypes.byref(win)) == C.MPI_ERR_COMM
+    assert L.MPI_Win_create(buf.ctypes.data, 256, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(win)) == 0
+    assert (win.value & 0xFC000000) == 0xA0000000
+    eh = ctypes.c_int()
+    assert L.MPI_Win_get_errhandler(win, ctypes.byref(eh)) == 0 and eh.value == C.MPI_ERRORS_ARE_FATAL
+    assert L.MPI_Win_set_errhandler(win, C.MPI_ERRORS_RETURN) == 0
+    src = np.arange(8, dtype=np.int32)
+    I = C.MPI_INT
+    # displacement, rank, MPI_PROC_NULL, zero count
+    assert L.MPI_Put(src.ctypes.data, 8, I, 0, -1, 8, I, win) == C.MPI_ERR_DISP
+    assert L.MPI_Put(src.ctypes.data, 8, I, 1, 0, 8, I, win) == C.MPI_ERR_RANK
+    assert L.MPI_Put(src.ctypes.data, 8, I, C.MPI_PROC_NULL, 0, 8, I, win) == 0
+    assert L.MPI_Put(src.ctypes.data, 0, I, 0, 0, 0, I, win) == 0
+    assert L.MPI_Put(src.ctypes.data, -1, I, 0, 0, 8, I, win) == C.MPI_ERR_COUNT
+    assert L.MPI_Put(src.ctypes.data, 8, I, 0, 0, 8, C.MPI_FLOAT, win) == C.MPI_ERR_TYPE
+    # ops: NO_OP and user ops are not accumulate operations; REPLACE is
+    assert L.MPI_Accumulate(src.ctypes.data, 8, I, 0, 0, 8, I, C.MPI_NO_OP, win) == C.MPI_ERR_OP
+    assert L.MPI_Accumulate(src.ctypes.data, 8, I, 0, 0, 8, I, C.MPI_OP_NULL, win) == C.MPI_ERR_OP
+    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+    fn = UF(lambda a, b, n, d: None)
+    op = ctypes.c_int()
+    assert L.MPI_Op_create(fn, 1, ctypes.byref(op)) == 0
+    assert L.MPI_Accumulate(src.ctypes.data, 8, I, 0, 0, 8, I, op.value, win) == C.MPI_ERR_OP
+    assert L.MPI_Op_free(ctypes.byref(op)) == 0
+    assert L.MPI_Accumulate(src.ctypes.data, 8, I, C.MPI_PROC_NULL, 0, 8, I, C.MPI_REPLACE, win) == 0
+    # a real transfer needs the GPU: without one it fails loudly
+    if L.msx_device_count() == 0:
+        assert L.MPI_Accumulate(src.ctypes.data, 8, I, 0, 0, 8, I, C.MPI_SUM, win) == C.MPI_ERR_OTHER
+    assert L.MPI_Win_fence(0, win) == 0
+    assert L.MPI_Win_free(ctypes.byref(win)) == 0 and win.value == C.MPI_WIN_NULL
+    bad = ctypes.c_int(0xA0000000 | 77)
+    assert L.MPI_Win_fence(0, bad) == C.MPI_ERR_WIN
