@@ -70,7 +70,7 @@ def run_collectives_child(world, rank, local, scale, transport="ipc"):
     try:
         pr = subprocess.run([sys.executable, os.path.join(REPO, "bench_collectives.py"), out, str(scale)],
                             env=env, capture_output=True, text=True,
-                            timeout=float(os.environ.get("MSX_COLL_TIMEOUT", "240")))
+                            timeout=float(os.environ.get("MSX_COLL_TIMEOUT", "150" if transport == "ipc" else "120")))
         if pr.returncode != 0:
             return {"error": f"rank {rank} child rc={pr.returncode}: {pr.stderr[-600:]}"}
     except subprocess.TimeoutExpired as e:

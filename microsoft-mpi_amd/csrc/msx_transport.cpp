@@ -371,8 +371,13 @@ public:
                 win_ = nullptr;
             }
             size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
-            hipError_t e = hipMalloc(&win_, want);
-            if (e != hipSuccess) return hip_fail(e, "window hipMalloc");
+            // Uncached device memory: peers write it over xGMI, which does not
+            // snoop this GPU's L2, so no reader (kernel, blit or DMA) may hold a
+            // stale line of it.  MSX_WINDOW_CACHED=1 selects plain hipMalloc.
+            const bool cached = getenv("MSX_WINDOW_CACHED") && atoi(getenv("MSX_WINDOW_CACHED"));
+            hipError_t e = cached ? hipMalloc(&win_, want) : hipExtMallocWithFlags(&win_, want, hipDeviceMallocUncached);
+            trace("window: %zu bytes %s rc=%d", want, cached ? "cached" : "uncached", (int)e);
+            if (e != hipSuccess) return hip_fail(e, "window allocation");
             win_bytes_ = want;
             win_peers_.clear();
         }
