@@ -279,7 +279,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_host_path:
         host = {}
         a_h = src.cpu()
-        for label, pin in (("pageable", False), ("pinned", True)):
+        for label, pin, mode in (("pageable", False, 0), ("pinned_zero_copy", True, 0),
+                                 ("pinned_staged", True, 1)):
+            L.msx_set_host_mode(mode)
             ah = a_h.pin_memory() if pin else a_h.clone()
             bh = acc.cpu()
             bh = bh.pin_memory() if pin else bh
@@ -292,6 +294,7 @@ def main():
             host[label] = {"ms_per_call": round(dt_h * 1e3, 2),
                            "payload_GiB_s": round(n * 4 / dt_h / 2**30, 2),
                            "traffic_GiB_s": round(n * BYTES_PER_ELEM / dt_h / 2**30, 2)}
+        L.msx_set_host_mode(0)
         # blocking MPI_Reduce_local on device buffers (adds launch + sync per call)
         reps, t1 = 10, time.perf_counter()
         for _ in range(reps):

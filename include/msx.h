@@ -69,6 +69,10 @@ const char* msx_tune_variant_name(int variant);
 
 /* host staging chunk size (bytes) for MPI_Reduce_local on host buffers */
 int msx_set_staging_chunk(int64_t bytes);
+/* host operands of MPI_Reduce_local: 0 (default) = pinned host memory is
+ * combined in place by the kernel over PCIe (zero-copy), pageable memory is
+ * staged through HBM; 1 = every host operand is staged */
+int msx_set_host_mode(int mode);
 
 /* schedule introspection for host-side tests of the collective engine
  * (mpid/reduce.cpp:3884-4066, 917-1334 restated as expression trees):

@@ -1095,6 +1095,13 @@ MSX_EXPORT int msx_set_staging_chunk(int64_t bytes)
     return MPI_SUCCESS;
 }
 
+MSX_EXPORT int msx_set_host_mode(int mode)
+{
+    if (mode != 0 && mode != 1) { set_error("host mode must be 0 or 1"); return MPI_ERR_ARG; }
+    set_host_mode(mode);
+    return MPI_SUCCESS;
+}
+
 // ---- schedule introspection (host-side tests of the collective engine) ------
 #include "msx_transport.h"
 

@@ -3,10 +3,13 @@
 // The reference combines in place on host memory (op.cpp:42-52).  On MI355X
 // the combine always runs on the GPU; host-resident MPI buffers are streamed
 // through HBM in chunks: H2D(in), H2D(inout) -> combine -> D2H(inout), with two
-// HIP streams so chunk i+1's copies overlap chunk i's combine and copy-back.
+// HIP streams so chunk i+1's copies overlap chunk i's combine and copy-back;
+// pinned host operands are read and written in place by the kernel (zero-copy)
+// unless msx_set_host_mode(1) asks for staging.
 // There is no CPU fallback: without a GPU the call fails with MPI_ERR_OTHER.
 #include "msx_runtime.h"
 
+#include <atomic>
 #include <mutex>
 #include <stdarg.h>
 #include <stdio.h>
@@ -143,8 +146,8 @@ BufInfo classify(const void* p)
         b.device = a.device;
         break;
     case hipMemoryTypeHost:
-        // pinned host memory: device-visible but PCIe-bound; stage it like any
-        // other host buffer so the combine itself streams from HBM.
+        // pinned host memory: device-visible (PCIe); combined in place by the
+        // kernel in host mode 0, staged through HBM in mode 1.
         b.place = Place::Host;
         b.dev = a.devicePointer;
         b.device = a.device;
@@ -190,6 +193,13 @@ int ensure_staging(DevState& s)
 
 }  // namespace
 
+namespace {
+std::atomic<int> g_host_mode{0};
+}
+
+void set_host_mode(int mode) { g_host_mode.store(mode); }
+int host_mode() { return g_host_mode.load(); }
+
 int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t count)
 {
     int rc = ensure_device();
@@ -197,8 +207,13 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
     const BufInfo bi = classify(in), bo = classify(inout);
     DevState& s = ds();
 
-    if (bi.place == Place::Device && bo.place == Place::Device) {
-        rc = reduce_local_device(opidx, k, bi.dev, bo.dev, count, s.stream);
+    // Device memory, or (host mode 0) pinned host memory the kernel reads and
+    // writes in place over PCIe: reads and the write-back then use both PCIe
+    // directions at once, with no staging copies.
+    const bool direct = (bi.place == Place::Device && bo.place == Place::Device) ||
+                        (g_host_mode.load() == 0 && bi.dev && bo.dev);
+    if (direct) {
+        rc = reduce_local_device(opidx, k, bi.dev, bo.dev, count, s.stream);   // device aliases
         if (rc != MPI_SUCCESS) return rc;
         hipError_t e = hipStreamSynchronize(s.stream);
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "combine kernel");

@@ -37,6 +37,10 @@ BufInfo classify(const void* p);
 
 LaunchCfg& launch_cfg();
 void set_staging_chunk(size_t bytes);
+// host operands: 0 = pinned memory combined in place by the kernel (zero-copy),
+// pageable staged; 1 = every host operand staged through HBM
+void set_host_mode(int mode);
+int host_mode();
 
 // inout = inout (op) in over `count` elements on any combination of host and
 // device buffers; blocking (returns after the result is in `inout`).

@@ -115,6 +115,7 @@ def lib():
         "msx_tune_variant_count": (i, []),
         "msx_tune_variant_name": (ctypes.c_char_p, [i]),
         "msx_set_staging_chunk": (i, [i64]),
+        "msx_set_host_mode": (i, [i]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -157,10 +157,12 @@ def test_known_answer_vectors_on_gpu(L):
     assert np.array_equal(_host(tb, 0, b).view(np.uint32), to_f(case["expect_f32_hex"]).view(np.uint32))
 
 
-@pytest.mark.parametrize("pinned", [False, True])
-def test_mpi_reduce_local_host_buffers_staged(L, pinned):
+@pytest.mark.parametrize("pinned,mode", [(False, 0), (True, 0), (True, 1)])
+def test_mpi_reduce_local_host_buffers_staged(L, pinned, mode):
     # the MPI path starts and ends in host memory: staged through HBM in chunks
+    # (mode 1, and pageable memory), or pinned memory combined in place (mode 0)
     assert L.msx_set_staging_chunk(1 << 20) == 0      # force many chunks
+    assert L.msx_set_host_mode(mode) == 0
     rng = np.random.default_rng(11)
     for dt, op in (("MPI_FLOAT", "MPI_SUM"), ("MPI_UINT64_T", "MPI_BAND"), ("MPI_2INT", "MPI_MINLOC")):
         kind = KIND[dt]
@@ -180,6 +182,7 @@ def test_mpi_reduce_local_host_buffers_staged(L, pinned):
         assert rc == 0, msx.last_error()
         assert got.tobytes() == exp.tobytes()
     assert L.msx_set_staging_chunk(64 << 20) == 0
+    assert L.msx_set_host_mode(0) == 0
 
 
 def test_mpi_reduce_local_device_and_mixed(L):
