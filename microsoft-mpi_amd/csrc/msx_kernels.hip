@@ -230,6 +230,42 @@ __global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* 
     }
 }
 
+// ---- LDS-staged variant (measurement only) ---------------------------------------
+// The north star's "LDS staging of the incoming chunk": the `in` tile goes
+// global -> LDS -> registers before the combine.  Each element is used once,
+// so the stage adds an LDS write + read per byte and a workgroup barrier for no
+// reuse; it is kept as a tuning variant so the sweep measures that cost
+//  instead of asserting it.
+template <int OP, class T, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_combine_lds(const T* __restrict__ in, T* __restrict__ io,
+                                                       size_t head, size_t nvec, size_t tail)
+{
+    __shared__ u32x4 stage[BLOCK];
+    constexpr size_t EPV = 16 / sizeof(T);
+    const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in + head);
+    u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
+    for (size_t t0 = (size_t)blockIdx.x * BLOCK; t0 < nvec; t0 += (size_t)gridDim.x * BLOCK) {
+        const size_t i = t0 + threadIdx.x;
+        const bool live = i < nvec;
+        u32x4 b = {};
+        if (live) {
+            stage[threadIdx.x] = ld<true>(vin + i);
+            b = ld<true>(vio + i);
+        }
+        __syncthreads();
+        if (live) vio[i] = apply_vec<OP, T>(b, stage[threadIdx.x]);
+        __syncthreads();
+    }
+    const size_t nscalar = head + tail;
+    if (nscalar) {
+        const size_t body_end = head + nvec * EPV;
+        for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nscalar; s += (size_t)gridDim.x * BLOCK) {
+            const size_t e = s < head ? s : body_end + (s - head);
+            io[e] = Fn<OP>::apply(io[e], in[e]);
+        }
+    }
+}
+
 // ---- reference-order multi-input combine ----------------------------------------
 // One pass over up to 2*kMaxLeaves inputs that reproduces the association AND
 // the inout/in roles of the reference's multi-step schedules:
@@ -403,6 +439,22 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
     return hipGetLastError();
 }
 
+template <int OP, class T, int BLOCK>
+hipError_t run_combine_lds(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
+{
+    size_t head, nvec, tail;
+    split<T>(in, io, count, head, nvec, tail);
+    size_t grid = (nvec + BLOCK - 1) / BLOCK;
+    const size_t sc = (head + tail + BLOCK - 1) / BLOCK;
+    if (grid < sc) grid = sc;
+    if (grid == 0) return hipSuccess;
+    if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
+    if (grid > 0x7fffffffu) grid = 0x7fffffffu;
+    hipLaunchKernelGGL((k_combine_lds<OP, T, BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
+                       static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail);
+    return hipGetLastError();
+}
+
 // Default launch of every (op, type): one 16-B vector per lane per operand,
 // 256-thread workgroups (one-shot grid, 65536 workgroups at 256 MiB fp32),
 // non-temporal loads.  Measured on MI355X for the 256 MiB fp32 SUM
@@ -437,6 +489,7 @@ const Variant kF32SumVariants[] = {
     {"u1_b64_ntld", run_combine<O_SUM, float, float, 1, 64, true, false>},
     {"u1_b256_ntall", run_combine<O_SUM, float, float, 1, 256, true, true>},
     {"u1_b256_plain", run_combine<O_SUM, float, float, 1, 256, false, false>},
+    {"u1_b256_lds", run_combine_lds<O_SUM, float, 256>},
 };
 constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
 
