@@ -36,7 +36,12 @@ def main(out_path, scale):
     rank, p = r_.value, s_.value
     dev = torch.device("cuda", int(os.environ.get("MSX_DEVICE", "0")))
     torch.cuda.set_device(dev)
-    res = {"ranks": p, "transport_requested": os.environ.get("MSX_TRANSPORT", "ipc")}
+    # xGMI reference: 7 links x 153.6 GB/s bidirectional per MI355X = 76.8 GB/s
+    # per direction per link; busBW (bytes each GPU moves per direction) is
+    # compared with the 7-link per-direction aggregate
+    XGMI = 7 * 76.8
+    res = {"ranks": p, "transport_requested": os.environ.get("MSX_TRANSPORT", "ipc"),
+           "xgmi_aggregate_GB_s_per_direction": XGMI}
     logf = open(os.environ.get("MSX_BENCH_LOG", os.devnull), "a")
 
     def log(msg):
@@ -75,6 +80,7 @@ def main(out_path, scale):
         res["c3_allreduce_sum_f32"] = {
             "bytes_per_rank": S, "seconds": round(t, 5), "algbw_GB_s": round(S / t / 1e9, 2),
             "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 2),
+            "busbw_frac_xgmi": round(S / t / 1e9 * 2 * (p - 1) / p / XGMI, 3),
             "correct": bool(torch.equal(recv, exp))}
     del send, recv, exp
     torch.cuda.empty_cache()

@@ -792,6 +792,17 @@ int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "stage copy");
 }
 
+// Second engine stream (engine worker only): local copies that overlap xGMI work.
+hipStream_t aux_stream()
+{
+    static hipStream_t s = [] {
+        hipStream_t t = nullptr;
+        (void)hipStreamCreateWithFlags(&t, hipStreamNonBlocking);
+        return t;
+    }();
+    return s;
+}
+
 // A batch of byte ranges moved by one k_copy_segs launch (one grid row each).
 struct Segs {
     std::vector<const void*> src;
@@ -1180,6 +1191,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     // pieces (work balance only, 16-element granules); each element of a piece
     // is evaluated with the tree of its block's owner.
     const size_t ce = (size_t)p * qmax;
+    hipStream_t s2 = aux_stream();
     for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce) {
         const size_t len = std::min(ce, count - o);
         const size_t q = (len + p - 1) / p;
@@ -1193,6 +1205,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             scatter.add(mine + lo_of(r) * esz, w.sub(r, me), (hi_of(r) - lo_of(r)) * esz);
         if (rc == MPI_SUCCESS) rc = scatter.run(s, "allreduce scatter");
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce scatter");
+        if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");           // OUT(me) free
         if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // A
         if (rc != MPI_SUCCESS) break;
         const size_t plo = lo_of(me), phi = hi_of(me);
@@ -1215,9 +1228,11 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         if (rc == MPI_SUCCESS) rc = push.run(s, "allreduce push");
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
         if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // B
-        if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, w.out(me), len * esz, s);
+        // collect on a second stream: it overlaps the next chunk's scatter
+        // (local HBM copy vs xGMI writes); synced before the next barrier A
+        if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, w.out(me), len * esz, s2);
     }
-    if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce collect");
+    if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");
     trace("allreduce: done rc=%d", rc);
     return rc;
 }
