@@ -84,6 +84,20 @@ def run_collectives_child(world, rank, local, scale, transport="ipc"):
     return {}
 
 
+class stdout_to_stderr:
+    """fd-level redirect: gloo/RCCL print connection chatter on stdout, which
+    must carry nothing but rank 0's JSON line."""
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def rccl_native_allreduce(dist, torch, world, dev, scale):
     """xGMI reference point: RCCL's own fp32 SUM allreduce (its ring/tree order,
     NOT the reference's association) on c3's 1 GiB/rank, same GPUs."""
@@ -170,7 +184,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
+        with stdout_to_stderr():
+            dist.init_process_group("gloo", init_method="env://")
     # one rank per GPU; ranks beyond the visible GPUs share them round-robin
     # (lets the N>1 path run on a one-GPU box too)
     local = local % max(torch.cuda.device_count(), 1)
@@ -271,7 +286,8 @@ def main():
         coll = collect("ipc")
         if distinct:
             coll_rccl = collect("rccl")
-            rccl_native = rccl_native_allreduce(dist, torch, world, dev, args.coll_scale)
+            with stdout_to_stderr():
+                rccl_native = rccl_native_allreduce(dist, torch, world, dev, args.coll_scale)
 
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
