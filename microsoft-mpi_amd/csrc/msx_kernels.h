@@ -40,6 +40,8 @@ struct TreeSpec {
     unsigned pairmask = 0;
     bool chain = false;
     bool sys = false;   // sources/output shared with peers: system acquire/release
+    void* extra[31] = {};   // the result is also stored here (e.g. peers' windows)
+    int nextra = 0;
 };
 hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t count,
                             hipStream_t s);

@@ -277,8 +277,11 @@ __global__ __launch_bounds__(BLOCK) void k_combine_lds(const T* __restrict__ in,
 //   chain (chain == 1): ((s0 op s1) op s2) op ... op s[P-1] (pairwise exchange,
 //         reduce.cpp:1258-1318).
 constexpr int kMaxLeaves = 16;
+constexpr int kMaxExtraOut = 31;
 struct TreeArgs {
     const void* s[2 * kMaxLeaves];
+    void* extra[kMaxExtraOut];   // further destinations of the result (peer windows)
+    int nextra;
     int P;
     int nleaves;   // leaves present (<= P); the rest of the P-leaf tree is empty
     unsigned pairmask;
@@ -343,14 +346,18 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
     if (vec_ok) {
         for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < nvec; i += stride) {
             auto load = [&](int k) { return reinterpret_cast<const u32x4*>(a.s[k])[i]; };
-            reinterpret_cast<u32x4*>(out)[i] = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
+            const u32x4 r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
+            reinterpret_cast<u32x4*>(out)[i] = r;
+            for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
         }
     }
     const size_t first = vec_ok ? nvec * EPV : 0;
     const size_t nsc = vec_ok ? tail : tail + nvec * EPV;
     for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nsc; s += stride) {
         auto load = [&](int k) { return reinterpret_cast<const T*>(a.s[k])[first + s]; };
-        out[first + s] = tree_eval<Fn<OP>, T>(a, load);
+        const T r = tree_eval<Fn<OP>, T>(a, load);
+        out[first + s] = r;
+        for (int e = 0; e < a.nextra; ++e) static_cast<T*>(a.extra[e])[first + s] = r;
     }
     if (a.sys) release_system();
 }
@@ -541,6 +548,7 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
 {
     bool ok = ((uintptr_t)out & 15) == 0;
     for (int k = 0; k < nsrc; ++k) ok = ok && a.s[k] && (((uintptr_t)a.s[k] & 15) == 0);
+    for (int e = 0; e < a.nextra; ++e) ok = ok && (((uintptr_t)a.extra[e] & 15) == 0);
     constexpr size_t ES = sizeof(T);
     const size_t epv = 16 / ES;
     const size_t nvec = count / epv, tail = count - nvec * epv;
@@ -660,12 +668,15 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         }
         ns = 2 * t.P;
     }
+    if (t.nextra < 0 || t.nextra > kMaxExtraOut) return hipErrorInvalidValue;
+    a.nextra = t.nextra;
+    for (int e = 0; e < t.nextra; ++e) a.extra[e] = t.extra[e];
     a.P = t.P;
     a.nleaves = (t.nleaves > 0 && t.nleaves <= t.P) ? t.nleaves : t.P;
     a.pairmask = t.pairmask;
     a.chain = t.chain ? 1 : 0;
     a.sys = t.sys ? 1 : 0;
-    if (!t.chain && t.P == 1 && t.pairmask == 0) {
+    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0) {
         if (t.src[0] == out) return hipSuccess;
         return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
     }

@@ -659,10 +659,14 @@ int sync_stream(hipStream_t s, const char* what)
 // Evaluate RankTree `t` over [start, start+len) elements of the per-rank
 // source pointers `srcs` into `out`.
 int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>& srcs, size_t esz,
-                  size_t start, size_t len, char* out, hipStream_t s)
+                  size_t start, size_t len, char* out, hipStream_t s,
+                  const std::vector<char*>& extra_outs = {})
 {
     if (len == 0) return MPI_SUCCESS;
     TreeSpec spec;
+    if (extra_outs.size() > 31) { set_error("tree combine: too many destinations"); return MPI_ERR_INTERN; }
+    spec.nextra = (int)extra_outs.size();
+    for (size_t e = 0; e < extra_outs.size(); ++e) spec.extra[e] = extra_outs[e];
     spec.P = t.P;
     spec.nleaves = t.nleaves;
     spec.pairmask = t.pairmask;
@@ -1209,6 +1213,13 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // A
         if (rc != MPI_SUCCESS) break;
         const size_t plo = lo_of(me), phi = hi_of(me);
+        // reduce my piece from my IN area (local) and store the result straight
+        // into every receiver's OUT area: the push is fused into the tree
+        // kernel (remote stores over xGMI)
+        std::vector<int> dests;
+        if (want) dests.push_back(me);
+        for (int r = 0; r < p; ++r)
+            if (r != me && (root < 0 || r == root)) dests.push_back(r);
         for (size_t e0 = plo; e0 < phi && rc == MPI_SUCCESS;) {
             const size_t ge = o + e0;                                             // global element
             const size_t rs = count / (size_t)pof2;
@@ -1218,14 +1229,11 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             const size_t e1 = std::min(phi, bst + bl - o);
             const int owner = allreduce_block_owner(p, j);
             const RankTree t = is_reduce ? tree_reduce_rsag(p, owner) : tree_allreduce(p, owner);
-            rc = run_rank_tree(op.opidx, k, t, subs, esz, e0 - plo, e1 - e0, w.out(me) + e0 * esz, s);
+            std::vector<char*> extra;
+            for (size_t d = 1; d < dests.size(); ++d) extra.push_back(w.out(dests[d]) + e0 * esz);
+            rc = run_rank_tree(op.opidx, k, t, subs, esz, e0 - plo, e1 - e0, w.out(dests[0]) + e0 * esz, s, extra);
             e0 = e1;
         }
-        Segs push;
-        for (int r = 0; r < p; ++r)
-            if (r != me && (root < 0 || r == root))
-                push.add(w.out(me) + plo * esz, w.out(r) + plo * esz, (phi - plo) * esz);
-        if (rc == MPI_SUCCESS) rc = push.run(s, "allreduce push");
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
         if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // B
         // collect on a second stream: it overlaps the next chunk's scatter
