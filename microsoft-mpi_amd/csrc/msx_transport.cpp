@@ -1172,9 +1172,10 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             const size_t len = std::min(qmax, count - o);
             const char* mine = nullptr;
             rc = device_view(bs, src, o * esz, len * esz, stage, s, &mine);
-            Segs sg;
+            Segs sg;                      // my own contribution is read in place
             for (int r = 0; r < p; ++r)
-                if (root < 0 || r == root) sg.add(mine, w.sub(r, me), len * esz);
+                if (r != me && (root < 0 || r == root)) sg.add(mine, w.sub(r, me), len * esz);
+            subs[(size_t)me] = const_cast<char*>(mine);
             if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
             if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
             if (rc == MPI_SUCCESS) rc = tp->barrier();                              // A
@@ -1205,8 +1206,9 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         const char* mine = nullptr;
         rc = device_view(bs, src, o * esz, len * esz, stage, s, &mine);
         Segs scatter;
-        for (int r = 0; r < p; ++r)
-            scatter.add(mine + lo_of(r) * esz, w.sub(r, me), (hi_of(r) - lo_of(r)) * esz);
+        for (int r = 0; r < p; ++r)                  // my own piece is read in place
+            if (r != me) scatter.add(mine + lo_of(r) * esz, w.sub(r, me), (hi_of(r) - lo_of(r)) * esz);
+        subs[(size_t)me] = const_cast<char*>(mine) + lo_of(me) * esz;
         if (rc == MPI_SUCCESS) rc = scatter.run(s, "allreduce scatter");
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce scatter");
         if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");           // OUT(me) free
@@ -1314,7 +1316,8 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
             const char* v = nullptr;
             rc = device_view(bs, src, (disp[r] + o) * esz, len * esz, stage ? stage + (size_t)r * qe * esz : nullptr,
                              s, &v);
-            scatter.add(v, w.sub(r, me), len * esz);
+            if (r == me) subs[(size_t)me] = const_cast<char*>(v);   // read in place
+            else scatter.add(v, w.sub(r, me), len * esz);
         }
         if (rc == MPI_SUCCESS) rc = scatter.run(s, "reduce_scatter scatter");
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "reduce_scatter scatter");
