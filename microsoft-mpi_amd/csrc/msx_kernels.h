@@ -11,6 +11,8 @@ namespace msx {
 struct LaunchCfg {
     int variant = 0;      // fp32-SUM tuning variant (0 = default); other pairs ignore it
     int grid_cap = 0;     // 0 = one tile per workgroup (no grid-stride), else max workgroups
+    bool pcie = false;    // operands are pinned host memory read over PCIe (zero-copy):
+                          // launched as k_combine_pcie so profiles keep the HBM kernel apart
 };
 
 // inout[i] = op(inout[i], in[i]) for i in [0, count), stream-ordered on `s`.

@@ -190,8 +190,8 @@ __device__ __forceinline__ void st(u32x4* p, u32x4 v)
 // VT = lane type used inside a 16-byte vector (== T except bitwise ops, which
 //      run on 32-bit words regardless of the MPI element type).
 template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
-__global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* __restrict__ io,
-                                                   size_t head, size_t nvec, size_t tail)
+__device__ __forceinline__ void combine_body(const T* __restrict__ in, T* __restrict__ io, size_t head,
+                                             size_t nvec, size_t tail)
 {
     constexpr size_t EPV = 16 / sizeof(T);
     constexpr size_t TILE = (size_t)BLOCK * UNROLL;
@@ -228,6 +228,22 @@ __global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* 
             io[e] = Fn<OP>::apply(io[e], in[e]);
         }
     }
+}
+
+template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
+__global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* __restrict__ io,
+                                                   size_t head, size_t nvec, size_t tail)
+{
+    combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
+}
+
+// Same body with both operands in pinned host memory (zero-copy over PCIe):
+// a separate symbol so rocprof statistics of the HBM kernel stay clean.
+template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
+__global__ __launch_bounds__(BLOCK) void k_combine_pcie(const T* __restrict__ in, T* __restrict__ io,
+                                                        size_t head, size_t nvec, size_t tail)
+{
+    combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
 }
 
 // ---- LDS-staged variant (measurement only) ---------------------------------------
@@ -440,9 +456,14 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
     if (grid == 0) return hipSuccess;
     if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
     if (grid > 0x7fffffffu) grid = 0x7fffffffu;
-    hipLaunchKernelGGL((k_combine<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
-                       dim3(BLOCK), 0, s, static_cast<const T*>(in), static_cast<T*>(io), head,
-                       nvec, tail);
+    if (cfg.pcie)
+        hipLaunchKernelGGL((k_combine_pcie<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
+                           dim3(BLOCK), 0, s, static_cast<const T*>(in), static_cast<T*>(io), head,
+                           nvec, tail);
+    else
+        hipLaunchKernelGGL((k_combine<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
+                           dim3(BLOCK), 0, s, static_cast<const T*>(in), static_cast<T*>(io), head,
+                           nvec, tail);
     return hipGetLastError();
 }
 
@@ -615,7 +636,7 @@ hipError_t launch_combine(int opidx, Kind k, const void* in, void* io, size_t n,
     if (n == 0) return hipSuccess;
     switch (opidx) {
     case O_SUM:
-        if (k == K_F32 && c.variant > 0 && c.variant < kNumVariants)
+        if (k == K_F32 && c.variant > 0 && c.variant < kNumVariants && !c.pcie)
             return kF32SumVariants[c.variant].fn(in, io, n, s, c);
         return dispatch_arith<O_SUM>(k, in, io, n, s, c);
     case O_MAX:  return dispatch_arith<O_MAX>(k, in, io, n, s, c);

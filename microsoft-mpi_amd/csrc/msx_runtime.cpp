@@ -213,8 +213,10 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
     const bool direct = (bi.place == Place::Device && bo.place == Place::Device) ||
                         (g_host_mode.load() == 0 && bi.dev && bo.dev);
     if (direct) {
-        rc = reduce_local_device(opidx, k, bi.dev, bo.dev, count, s.stream);   // device aliases
-        if (rc != MPI_SUCCESS) return rc;
+        LaunchCfg cfg = g_cfg;
+        cfg.pcie = bi.place != Place::Device || bo.place != Place::Device;
+        hipError_t le = launch_combine(opidx, k, bi.dev, bo.dev, count, s.stream, cfg);   // device aliases
+        if (le != hipSuccess) return hip_fail(le, "combine kernel launch");
         hipError_t e = hipStreamSynchronize(s.stream);
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "combine kernel");
     }

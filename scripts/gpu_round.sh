@@ -23,7 +23,7 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --sweep
-    step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o trace --output-format csv -- python bench.py --steps 20 --warmup 5 --cpu-seconds 1 --no-host-path
+    step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o trace --output-format csv -- python bench.py
     step rocprof_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof_pmc" -o pmc_fetch --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0.5 --no-host-path
     step rocprof_pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof_pmc" -o pmc_write --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0.5 --no-host-path
 fi
