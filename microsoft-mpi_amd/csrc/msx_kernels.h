@@ -11,8 +11,9 @@ namespace msx {
 struct LaunchCfg {
     int variant = 0;      // fp32-SUM tuning variant (0 = default); other pairs ignore it
     int grid_cap = 0;     // 0 = one tile per workgroup (no grid-stride), else max workgroups
-    bool pcie = false;    // operands are pinned host memory read over PCIe (zero-copy):
-                          // launched as k_combine_pcie so profiles keep the HBM kernel apart
+    bool host = false;    // launched by the host-memory path of MPI_Reduce_local (zero-copy
+                          // over PCIe, or a staged chunk): the k_combine_host symbol, so
+                          // profiles keep the device-resident kernel's statistics apart
 };
 
 // inout[i] = op(inout[i], in[i]) for i in [0, count), stream-ordered on `s`.

@@ -237,10 +237,11 @@ __global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* 
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
 }
 
-// Same body with both operands in pinned host memory (zero-copy over PCIe):
-// a separate symbol so rocprof statistics of the HBM kernel stay clean.
+// Same body, launched by the host-memory path of MPI_Reduce_local (pinned
+// operands read over PCIe, or HBM staging chunks): a separate symbol so the
+// rocprof statistics of the device-resident kernel stay clean.
 template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
-__global__ __launch_bounds__(BLOCK) void k_combine_pcie(const T* __restrict__ in, T* __restrict__ io,
+__global__ __launch_bounds__(BLOCK) void k_combine_host(const T* __restrict__ in, T* __restrict__ io,
                                                         size_t head, size_t nvec, size_t tail)
 {
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
@@ -456,8 +457,8 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
     if (grid == 0) return hipSuccess;
     if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
     if (grid > 0x7fffffffu) grid = 0x7fffffffu;
-    if (cfg.pcie)
-        hipLaunchKernelGGL((k_combine_pcie<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
+    if (cfg.host)
+        hipLaunchKernelGGL((k_combine_host<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
                            dim3(BLOCK), 0, s, static_cast<const T*>(in), static_cast<T*>(io), head,
                            nvec, tail);
     else
@@ -636,7 +637,7 @@ hipError_t launch_combine(int opidx, Kind k, const void* in, void* io, size_t n,
     if (n == 0) return hipSuccess;
     switch (opidx) {
     case O_SUM:
-        if (k == K_F32 && c.variant > 0 && c.variant < kNumVariants && !c.pcie)
+        if (k == K_F32 && c.variant > 0 && c.variant < kNumVariants && !c.host)
             return kF32SumVariants[c.variant].fn(in, io, n, s, c);
         return dispatch_arith<O_SUM>(k, in, io, n, s, c);
     case O_MAX:  return dispatch_arith<O_MAX>(k, in, io, n, s, c);

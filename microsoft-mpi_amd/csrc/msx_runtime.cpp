@@ -214,7 +214,7 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
                         (g_host_mode.load() == 0 && bi.dev && bo.dev);
     if (direct) {
         LaunchCfg cfg = g_cfg;
-        cfg.pcie = bi.place != Place::Device || bo.place != Place::Device;
+        cfg.host = bi.place != Place::Device || bo.place != Place::Device;
         hipError_t le = launch_combine(opidx, k, bi.dev, bo.dev, count, s.stream, cfg);   // device aliases
         if (le != hipSuccess) return hip_fail(le, "combine kernel launch");
         hipError_t e = hipStreamSynchronize(s.stream);
@@ -223,6 +223,8 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
 
     // At least one operand in host memory: chunked, double-buffered staging.
     std::lock_guard<std::mutex> g(s.stage_mu);
+    LaunchCfg host_cfg = g_cfg;
+    host_cfg.host = true;
     rc = ensure_staging(s);
     if (rc != MPI_SUCCESS) return rc;
     const size_t esz = (size_t)kind_size(k);
@@ -251,7 +253,7 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
                 e = hipMemcpyAsync(s.stage_io[slot], src_io, bytes, hipMemcpyHostToDevice, st);
             dio = s.stage_io[slot];
         }
-        if (e == hipSuccess) e = launch_combine(opidx, k, din, dio, n, st, g_cfg);
+        if (e == hipSuccess) e = launch_combine(opidx, k, din, dio, n, st, host_cfg);
         if (e == hipSuccess && bo.place == Place::Host)
             e = hipMemcpyAsync(src_io, dio, bytes, hipMemcpyDeviceToHost, st);
         off += n;
