@@ -196,3 +196,24 @@ def test_rma_window_validation(msxlib):
     assert L.MPI_Win_free(ctypes.byref(win)) == 0 and win.value == C.MPI_WIN_NULL
     bad = ctypes.c_int(0xA0000000 | 77)
     assert L.MPI_Win_fence(0, bad) == C.MPI_ERR_WIN
+
+
+def _build_c_demo(tmp_path):
+    exe = str(tmp_path / "reduce_local_demo")
+    libdir = os.path.join(msx.REPO_ROOT, "microsoft-mpi_amd", "lib")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(msx.REPO_ROOT, "include"),
+                    os.path.join(msx.REPO_ROOT, "examples", "reduce_local_demo.c"), "-L", libdir,
+                    "-lmsmpi_mi355x", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    return exe
+
+
+def test_plain_c_program_builds_against_the_headers(tmp_path):
+    """Link-level drop-in: a C MPI program compiles with gcc against include/mpi.h
+    and links the library; without a GPU its first reduction aborts loudly with
+    the MPI error class (MPI_ERR_OTHER), never a silent CPU result."""
+    exe = _build_c_demo(tmp_path)
+    if msx.lib().msx_device_count() > 0:
+        pytest.skip("GPU present: covered by tests/test_gpu_local.py")
+    r = subprocess.run([exe], capture_output=True, text=True, env={**os.environ, "MSX_SIZE": "1"})
+    assert r.returncode == C.MPI_ERR_OTHER
+    assert "no usable MI355X" in r.stderr

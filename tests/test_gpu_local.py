@@ -298,3 +298,15 @@ def test_nan_payload_propagation_matches_reference_cpu(L, dt, op):
         bc = np.empty(b.size, ct); bc.real, bc.imag = b, a[::-1]
         a, b = ac, bc
     _check_dev(L, op, dt, a, b)
+
+
+def test_plain_c_program_runs_on_the_gpu(tmp_path):
+    """examples/reduce_local_demo.c (BASELINE configs[0] through the C ABI):
+    gcc-built, linked with the library, bit-exact against the C loop."""
+    import subprocess
+    from test_abi import _build_c_demo
+    exe = _build_c_demo(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "MSX_SIZE": "1", "MSX_RANK": "0"})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("OK ")
