@@ -168,10 +168,28 @@ def cpu_baseline(seconds, elems):
         if el >= seconds:
             break
     gib = calls * n * BYTES_PER_ELEM / el / 2**30
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{calls} calls of oracle Op<float>::Sum over 2 x {n * 4 >> 20} MiB host buffers "
-                      f"({el:.1f} s, 1 thread = one MS-MPI rank)",
-            "payload_GiB_s": round(calls * n * 4 / el / 2**30, 3)}
+    out = {"value": round(gib, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+           "sample": f"{calls} calls of oracle Op<float>::Sum over 2 x {n * 4 >> 20} MiB host buffers "
+                     f"({el:.1f} s, 1 thread = one MS-MPI rank)",
+           "payload_GiB_s": round(calls * n * 4 / el / 2**30, 3)}
+    # every host core of this job, elements sharded across
+    # threads (the box allots 16 cores to a one-GPU job)
+    try:
+        cores = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        cores = min(16, os.cpu_count() or 1)
+    if cores > 1:
+        oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=cores)
+        calls, t0 = 0, time.perf_counter()
+        while True:
+            oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=cores)
+            calls += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 3:
+                break
+        out["all_cores"] = {"value": round(calls * n * BYTES_PER_ELEM / el / 2**30, 3), "unit": "GiB/s",
+                            "cores": cores, "sample": f"{calls} calls, {el:.1f} s, {cores} threads"}
+    return out
 
 
 def main():
