@@ -727,6 +727,39 @@ int host_user_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t coun
     return copy_any(recvbuf, v[src].data(), bytes);
 }
 
+// Evaluate RankTree `t` on host with a user function (same association and
+// inout/in roles as k_tree: the left operand is `inout`).  x[r] = rank r's
+// contribution (count elements).
+void eval_tree_host(const RankTree& t, const std::vector<const char*>& x, char* out, size_t count,
+                    MPI_Datatype dt, const OpRef& op)
+{
+    const size_t esz = (size_t)type_size(dt), bytes = count * esz;
+    auto call = [&](const char* in, char* io) {
+        for (size_t off = 0; off < count;) {
+            size_t n = std::min(count - off, (size_t)0x7fffffff);
+            int len = (int)n;
+            MPI_Datatype d = dt;
+            op.user_fn(const_cast<char*>(in) + off * esz, io + off * esz, &len, &d);
+            off += n;
+        }
+    };
+    if (t.chain) {
+        memcpy(out, x[(size_t)t.src[0]], bytes);
+        for (int k = 1; k < t.P; ++k) call(x[(size_t)t.src[k]], out);
+        return;
+    }
+    const int nl = t.nleaves ? t.nleaves : t.P;
+    std::vector<std::vector<char>> v((size_t)nl);
+    for (int k = 0; k < nl; ++k) {
+        v[(size_t)k].assign(x[(size_t)t.src[2 * k]], x[(size_t)t.src[2 * k]] + bytes);
+        if ((t.pairmask >> k) & 1u) call(x[(size_t)t.src[2 * k + 1]], v[(size_t)k].data());
+    }
+    for (int w = 1; w < t.P; w *= 2)
+        for (int k = 0; k + w < t.P; k += 2 * w)
+            if (k + w < nl) call(v[(size_t)(k + w)].data(), v[(size_t)k].data());
+    memcpy(out, v[0].data(), bytes);
+}
+
 // Engine-private device scratch (grows, never shrinks; engine worker only).
 char* dev_scratch(size_t bytes)
 {
@@ -1265,10 +1298,31 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
     const char* src = static_cast<const char*>(in_place ? recvbuf : sendbuf);
 
     if (op.opidx == O_NULL) {
-        // user op: full allreduce on host, keep our block
-        std::vector<char> full(total * esz), res(total * esz);
+        std::vector<char> full(total * esz);
         int rc = copy_any(full.data(), src, total * esz);
-        if (rc == MPI_SUCCESS) rc = host_user_allreduce(c, full.data(), res.data(), total, dt, op);
+        if (rc != MPI_SUCCESS) return rc;
+        if (op.commutative) {
+            // commutative user op: the builtin schedules (recursive halving or
+            // pairwise, same 32-bit gate) evaluated on host with the user's
+            // function, reduce.cpp:917-1334
+            std::vector<char> all((size_t)p * total * esz);
+            if ((rc = c->tp->allgather(full.data(), total * esz, all.data())) != MPI_SUCCESS) return rc;
+            const int algo = reduce_scatter_algo(p, total, (int)esz, true);
+            const int n = newrank_of(me, p);
+            const RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
+                                                       : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
+            const size_t mycnt = (size_t)recvcounts[me];
+            std::vector<const char*> x((size_t)p);
+            for (int r = 0; r < p; ++r) x[(size_t)r] = all.data() + ((size_t)r * total + disp[me]) * esz;
+            std::vector<char> res(mycnt * esz);
+            eval_tree_host(t, x, res.data(), mycnt, dt, op);
+            return mycnt ? copy_any(recvbuf, res.data(), mycnt * esz) : MPI_SUCCESS;
+        }
+        // non-commutative: recursive doubling (MPIR_Reduce_scatter_non_commutative,
+        // reduce.cpp:1340-1630) -- for a power-of-two p each block is exactly the
+        // recursive-doubling allreduce value; other p share its lower-first order
+        std::vector<char> res(total * esz);
+        rc = host_user_allreduce(c, full.data(), res.data(), total, dt, op);
         if (rc == MPI_SUCCESS && recvcounts[me])
             rc = copy_any(recvbuf, res.data() + disp[me] * esz, (size_t)recvcounts[me] * esz);
         return rc;
@@ -1360,20 +1414,61 @@ int engine_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int
         .get();
 }
 
+namespace {
+
+// MPI_Reduce with a user function (host code): every contribution is gathered
+// to host memory and the reference's binomial tree is evaluated with the
+// user's function (reduce.cpp:440-540): relative ranks from lroot = root for
+// commutative ops, else from 0 with the result sent to root; the parent
+// combines a child's buffer as `in` (commutative) or as `inout` with its own
+// as `in` (non-commutative, "the sender is above us").
+int host_user_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                     const OpRef& op, int root)
+{
+    const int p = c->size, me = c->rank, esz = type_size(dt);
+    const size_t bytes = count * (size_t)esz;
+    std::vector<char> mine(bytes), all((size_t)p * bytes);
+    int rc = copy_any(mine.data(), sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, bytes);
+    if (rc == MPI_SUCCESS) rc = c->tp->allgather(mine.data(), bytes, all.data());
+    if (rc != MPI_SUCCESS || me != root) return rc;
+    auto call = [&](const char* in, char* io) {
+        for (size_t off = 0; off < count;) {
+            size_t n = std::min(count - off, (size_t)0x7fffffff);
+            int len = (int)n;
+            MPI_Datatype d = dt;
+            op.user_fn(const_cast<char*>(in) + off * esz, io + off * esz, &len, &d);
+            off += n;
+        }
+    };
+    const int lroot = op.commutative ? root : 0;
+    auto buf = [&](int rel) { return all.data() + (size_t)((rel + lroot) % p) * bytes; };
+    std::vector<char> tmp(bytes);
+    for (int mask = 1; mask < p; mask <<= 1) {
+        for (int rel = 0; rel < p; rel += 2 * mask) {     // receivers at this level
+            const int src = rel | mask;
+            if (src >= p) continue;
+            if (op.commutative) {
+                call(buf(src), buf(rel));
+            } else {
+                memcpy(tmp.data(), buf(src), bytes);
+                call(buf(rel), tmp.data());
+                memcpy(buf(rel), tmp.data(), bytes);
+            }
+        }
+    }
+    return copy_any(recvbuf, buf(0), bytes);
+}
+
+}  // namespace
+
 int engine_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                   const OpRef& op, int root)
 {
-    // The root receives the allreduce expression tree (identical to the
-    // reference's Rabenseifner / binomial reduce for root 0, reduce.cpp:226-299,
-    // 489-537); other ranks only contribute.  User ops: host allreduce.
+    // Builtin ops: the reference's binomial / Rabenseifner trees (do_allreduce
+    // in reduce mode); user ops: host_user_reduce.
     return worker()
         .submit([=]() -> int {
-            if (op.opidx == O_NULL) {
-                const size_t bytes = count * (size_t)type_size(dt);
-                std::vector<char> tmp(bytes);
-                int rc = host_user_allreduce(c, sendbuf, c->rank == root ? recvbuf : tmp.data(), count, dt, op);
-                return rc;
-            }
+            if (op.opidx == O_NULL) return host_user_reduce(c, sendbuf, recvbuf, count, dt, op, root);
             return do_allreduce(c, sendbuf, recvbuf, count, dt, op, root);
         })
         .get();

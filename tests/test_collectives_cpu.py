@@ -347,6 +347,23 @@ assert L.MPI_Wait(ctypes.byref(req), None) == 0 and req.value == C.MPI_REQUEST_N
 assert L.MPI_Iexscan(send.ctypes.data, exc2.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD, ctypes.byref(req)) == 0
 assert L.MPI_Wait(ctypes.byref(req), None) == 0
 assert (inc2 == inc).all() and (exc2 == exc).all()
+# MPI_Reduce with user ops: the reference's binomial tree (reduce.cpp:440-540)
+opc = ctypes.c_int()
+assert L.MPI_Op_create(fn, 1, ctypes.byref(opc)) == 0       # same function, flagged commutative
+x2 = np.array([10.0 * 2 ** r.value], np.float64)
+red = {}
+for name, o in (("noncomm", op.value), ("comm", opc.value)):
+    out = np.full(1, 7.0)
+    assert L.MPI_Reduce(x2.ctypes.data, out.ctypes.data, 1, C.MPI_DOUBLE, o, 2, C.MPI_COMM_WORLD) == 0
+    red[name] = out[0]
+# MPI_Reduce_scatter_block with the commutative-flagged user op: recursive
+# halving (32 B < 512 KiB), leaves x_{n ^ bitrev(k)}, left operand = inout
+rs_in = np.array([10.0 * 2 ** r.value + j for j in range(4)], np.float64)
+rs_out = np.zeros(1)
+assert L.MPI_Reduce_scatter_block(rs_in.ctypes.data, rs_out.ctypes.data, 1, C.MPI_DOUBLE, opc.value,
+                                  C.MPI_COMM_WORLD) == 0, msx.last_error()
+red["rs"] = rs_out[0]
+print("RED", r.value, red["noncomm"], red["comm"], red["rs"], flush=True)
 import time
 t0 = time.perf_counter()
 for _ in range(500):                       # node-local shared-memory barrier
@@ -365,10 +382,21 @@ def test_four_mpi_processes_user_op_scan_follows_reference_task_order():
     port = _free_port()
     outs = _spawn(SCAN_WORKER, 4, lambda r: {"MSX_SIZE": "4", "MSX_RANK": str(r),
                                              "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1"})
-    got = {}
+    got, red, rsv = {}, {}, {}
     for rc, o, e in outs:
         assert rc == 0, e[-3000:]
         _, rk, inc, exc = [l for l in o.splitlines() if l.startswith("OUT")][0].split()
         got[int(rk)] = (float(inc), float(exc))
+        _, rk, nc, cm, rs = [l for l in o.splitlines() if l.startswith("RED")][0].split()
+        red[int(rk)] = (float(nc), float(cm))
+        rsv[int(rk)] = float(rs)
+    # MPI_Reduce at root 2 of x = [10, 20, 40, 80] with a op b = a - b:
+    # non-commutative -> tree rooted at 0: (x0-x1)-(x2-x3) = 30;
+    # flagged commutative -> relative ranks from root 2: (x1-x0)-(x3-x2) = -30
+    assert red[2] == (30.0, -30.0)
+    assert all(red[k] == (7.0, 7.0) for k in (0, 1, 3))
+    # reduce_scatter (recursive halving): rank 0 = (x3-x1)-(x2-x0) = 30 with
+    # x = [10, 20, 40, 80]; rank 1 over x+1 with leaves [x1,x3,x0,x2] = -30
+    assert rsv[0] == 30.0 and rsv[1] == -30.0
     assert [got[k][0] for k in range(4)] == [10.0, -10.0, -40.0, 0.0]
     assert [got[k][1] for k in range(4)] == [7.0, 10.0, -10.0, -40.0]
