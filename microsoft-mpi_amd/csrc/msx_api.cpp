@@ -691,7 +691,8 @@ MSX_EXPORT int MPI_Waitall(int count, MPI_Request reqs[], MPI_Status statuses[])
     MSX_REQUIRE_INIT("MPI_Waitall");
     int rc = MPI_SUCCESS;
     for (int i = 0; i < count; ++i) {
-        MPI_Status* st = (statuses == MPI_STATUSES_IGNORE) ? MPI_STATUS_IGNORE : &statuses[i];
+        MPI_Status* st = (statuses == MPI_STATUSES_IGNORE || statuses == nullptr) ? MPI_STATUS_IGNORE
+                                                                                  : &statuses[i];
         int r = request_wait(&reqs[i], st);
         if (r != MPI_SUCCESS && rc == MPI_SUCCESS) rc = r;
     }

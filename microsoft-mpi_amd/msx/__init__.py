@@ -85,6 +85,8 @@ def lib():
         "MPI_Iallreduce": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
         "MPI_Ireduce": (i, [p, p, i, i, i, i, i, ctypes.POINTER(i)]),
         "MPI_Ireduce_scatter_block": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Ireduce_scatter": (i, [p, p, p, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Waitall": (i, [i, ctypes.POINTER(i), p]),
         "MPI_Scan": (i, [p, p, i, i, i, i]),
         "MPI_Exscan": (i, [p, p, i, i, i, i]),
         "MPI_Iscan": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),

@@ -153,6 +153,45 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
         elif not (excl and rank == 0):
             check(f"iscan {opn} {dtn} excl={excl}", fromdev(rb2, xs[rank]), exp[rank])
 
+# MPI_Ireduce / MPI_Ireduce_scatter_block / MPI_Ireduce_scatter in flight together,
+# completed by one MPI_Waitall (issue order = execution order on every rank)
+cnt = 30001
+xr = inputs("MPI_SUM", "MPI_FLOAT", cnt, 6000)
+er = raw(np.zeros_like(xr[0]))
+assert oracle.reduce(C.MPI_SUM, C.MPI_FLOAT, p - 1, xr, er) == 0
+per = 5003
+xs_b = inputs("MPI_MAX", "MPI_DOUBLE", per * p, 6001)
+es_b = [raw(np.zeros(per, xs_b[0].dtype)) for _ in range(p)]
+assert oracle.reduce_scatter(C.MPI_MAX, C.MPI_DOUBLE, [per] * p, xs_b, es_b) == 0
+counts_v = [1000 + 7 * k for k in range(p)]
+xs_v = inputs("MPI_BXOR", "MPI_INT", sum(counts_v), 6002)
+es_v = [raw(np.zeros(c, xs_v[0].dtype)) for c in counts_v]
+assert oracle.reduce_scatter(C.MPI_BXOR, C.MPI_INT, counts_v, xs_v, es_v) == 0
+d_r, o_r = todev(xr[rank]), torch.zeros(xr[rank].nbytes, dtype=torch.uint8, device="cuda")
+d_b, o_b = todev(xs_b[rank]), torch.zeros(per * 8, dtype=torch.uint8, device="cuda")
+d_v, o_v = todev(xs_v[rank]), torch.zeros(counts_v[rank] * 4, dtype=torch.uint8, device="cuda")
+reqs = (ctypes.c_int * 3)()
+cv = (ctypes.c_int * p)(*counts_v)
+rcs = [L.MPI_Ireduce(d_r.data_ptr(), o_r.data_ptr(), cnt, C.MPI_FLOAT, C.MPI_SUM, p - 1, C.MPI_COMM_WORLD,
+                     ctypes.cast(ctypes.addressof(reqs) + 0, ctypes.POINTER(ctypes.c_int))),
+       L.MPI_Ireduce_scatter_block(d_b.data_ptr(), o_b.data_ptr(), per, C.MPI_DOUBLE, C.MPI_MAX, C.MPI_COMM_WORLD,
+                                   ctypes.cast(ctypes.addressof(reqs) + 4, ctypes.POINTER(ctypes.c_int))),
+       L.MPI_Ireduce_scatter(d_v.data_ptr(), o_v.data_ptr(), cv, C.MPI_INT, C.MPI_BXOR, C.MPI_COMM_WORLD,
+                             ctypes.cast(ctypes.addressof(reqs) + 8, ctypes.POINTER(ctypes.c_int)))]
+if any(rcs):
+    fails.append(f"nbc start rc={rcs} {msx.last_error()}")
+else:
+    rc = L.MPI_Waitall(3, reqs, None)
+    if rc:
+        fails.append(f"waitall rc={rc} {msx.last_error()}")
+    else:
+        if rank == p - 1:
+            check("ireduce", fromdev(o_r, xr[rank]), er)
+        check("ireduce_scatter_block", fromdev(o_b, es_b[rank]), es_b[rank])
+        check("ireduce_scatter", fromdev(o_v, es_v[rank]), es_v[rank])
+        if list(reqs) != [C.MPI_REQUEST_NULL] * 3:
+            fails.append(f"waitall left requests {list(reqs)}")
+
 # MPI_Iallreduce BAND u64 (config 5 op/type) overlapped with host compute
 xs = inputs("MPI_BAND", "MPI_UINT64_T", 1 << 18, 4000)
 exp = [raw(x.copy()) for x in xs]
