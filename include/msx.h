@@ -41,6 +41,10 @@ int msx_device_count(void);
  * send/recv over xGMI, MSX_TRANSPORT=rccl and one GPU per rank), "ipc" (IPC
  * windows + remote writes) or "self" (one rank) */
 const char* msx_engine_transport(void);
+/* phase timers of the window allreduce since the last reset (seconds):
+ * out[0] stage+scatter, [1] collect wait + barrier A, [2] reduce + push,
+ * [3] barrier B, [4] final collect, [5] chunks, [6] calls; returns 7 */
+int msx_engine_stats(double* out, int n, int reset);
 /* text of the last error raised on the calling thread ("" if none) */
 const char* msx_last_error(void);
 

@@ -1030,6 +1030,11 @@ MSX_EXPORT const char* msx_engine_transport(void)
     Comm* c = world();
     return engine_transport_name(c ? c->tp : nullptr);
 }
+MSX_EXPORT int msx_engine_stats(double* out, int n, int reset)
+{
+    if (!out || n < 0) return -1;
+    return engine_stats(out, n, reset);
+}
 MSX_EXPORT int msx_device_count(void) { return device_count_noinit(); }
 MSX_EXPORT const char* msx_last_error(void) { return last_error(); }
 

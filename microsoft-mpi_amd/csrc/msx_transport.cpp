@@ -829,6 +829,15 @@ int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "stage copy");
 }
 
+// Phase timers of the window allreduce (host clock, engine worker only):
+// t[0] stage + scatter, t[1] collect wait + barrier A, t[2] reduce + push,
+// t[3] barrier B, t[4] last collect.  Read by msx_engine_stats().
+struct EngineStats {
+    double t[5] = {0, 0, 0, 0, 0};
+    long chunks = 0, calls = 0;
+};
+EngineStats g_stats;
+
 // Second engine stream (engine worker only): local copies that overlap xGMI work.
 hipStream_t aux_stream()
 {
@@ -1231,6 +1240,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     const size_t ce = (size_t)p * qmax;
     hipStream_t s2 = aux_stream();
     for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce) {
+        const double t0 = now_s();
         const size_t len = std::min(ce, count - o);
         const size_t q = (len + p - 1) / p;
         const size_t qv = (q + 15) & ~(size_t)15;
@@ -1244,8 +1254,13 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         subs[(size_t)me] = const_cast<char*>(mine) + lo_of(me) * esz;
         if (rc == MPI_SUCCESS) rc = scatter.run(s, "allreduce scatter");
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce scatter");
-        if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");           // OUT(me) free
+        const double t1 = now_s();
+        const double tc = now_s();
+    if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");
+    g_stats.t[4] += now_s() - tc;
+    g_stats.calls += 1;           // OUT(me) free
         if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // A
+        const double t2 = now_s();
         if (rc != MPI_SUCCESS) break;
         const size_t plo = lo_of(me), phi = hi_of(me);
         // reduce my piece from my IN area (local) and store the result straight
@@ -1270,7 +1285,14 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             e0 = e1;
         }
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
+        const double t3 = now_s();
         if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // B
+        const double t4 = now_s();
+        g_stats.chunks += 1;
+        g_stats.t[0] += t1 - t0;
+        g_stats.t[1] += t2 - t1;
+        g_stats.t[2] += t3 - t2;
+        g_stats.t[3] += t4 - t3;
         // collect on a second stream: it overlaps the next chunk's scatter
         // (local HBM copy vs xGMI writes); synced before the next barrier A
         if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, w.out(me), len * esz, s2);
@@ -1856,6 +1878,17 @@ int engine_rma_fence(RmaWin* w)
 {
     if (w->comm->size == 1 || !w->comm->tp) return MPI_SUCCESS;   // all operations were local
     return worker().submit([w] { return do_rma_fence(w); }).get();
+}
+
+int engine_stats(double* out, int n, int reset)
+{
+    return worker().submit([out, n, reset]() -> int {
+        const double v[7] = {g_stats.t[0], g_stats.t[1], g_stats.t[2], g_stats.t[3], g_stats.t[4],
+                             (double)g_stats.chunks, (double)g_stats.calls};
+        for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+        if (reset) g_stats = EngineStats();
+        return 7;
+    }).get();
 }
 
 const char* engine_transport_name(Transport* tp)

@@ -37,6 +37,9 @@ public:
 };
 
 int transport_create(int rank, int size, Transport** out);
+// window-allreduce phase timers (seconds): stage+scatter, collect wait+barrier A,
+// reduce+push, barrier B, last collect, chunks, calls; returns 7
+int engine_stats(double* out, int n, int reset);
 // data plane the engine uses for `tp`: "rccl", "ipc" or "self" (size 1)
 const char* engine_transport_name(Transport* tp);
 void transport_destroy(Transport* t);

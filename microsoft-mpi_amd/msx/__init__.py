@@ -103,6 +103,7 @@ def lib():
         "MPI_Fetch_and_op": (i, [p, p, i, i, i64, i, i]),
         "MPI_Compare_and_swap": (i, [p, p, p, i, i, i64, i]),
         "msx_engine_transport": (ctypes.c_char_p, []),
+        "msx_engine_stats": (i, [ctypes.POINTER(ctypes.c_double), i, i]),
         "MPI_Wait": (i, [ctypes.POINTER(i), p]),
         "MPI_Test": (i, [ctypes.POINTER(i), ctypes.POINTER(i), p]),
         "MPI_Wtime": (ctypes.c_double, []),
