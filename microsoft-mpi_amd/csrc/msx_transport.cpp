@@ -1255,10 +1255,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         if (rc == MPI_SUCCESS) rc = scatter.run(s, "allreduce scatter");
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce scatter");
         const double t1 = now_s();
-        const double tc = now_s();
-    if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");
-    g_stats.t[4] += now_s() - tc;
-    g_stats.calls += 1;           // OUT(me) free
+        if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");           // OUT(me) free
         if (rc == MPI_SUCCESS) rc = tp->barrier();                                  // A
         const double t2 = now_s();
         if (rc != MPI_SUCCESS) break;
@@ -1297,7 +1294,10 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // (local HBM copy vs xGMI writes); synced before the next barrier A
         if (rc == MPI_SUCCESS && want) rc = copy_async(dst + o * esz, w.out(me), len * esz, s2);
     }
+    const double tc = now_s();
     if (rc == MPI_SUCCESS) rc = sync_stream(s2, "allreduce collect");
+    g_stats.t[4] += now_s() - tc;
+    g_stats.calls += 1;
     trace("allreduce: done rc=%d", rc);
     return rc;
 }
