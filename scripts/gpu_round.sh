@@ -19,7 +19,7 @@ rocm-smi --showproductname > "$OUT/rocm_smi.log" 2>&1
 lscpu > "$OUT/lscpu.log" 2>&1; nproc >> "$OUT/lscpu.log"
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
     step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-    step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+    step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --sweep
