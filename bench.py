@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--no-collectives", action="store_true",
                     help="skip the N>1 collective configs (c3-c5, bench_collectives.py)")
     ap.add_argument("--coll-scale", type=float, default=1.0, help="size factor for c3-c5")
+    ap.add_argument("--no-per-op", action="store_true", help="skip the per-(op, type) roofline table")
     return ap.parse_args()
 
 
@@ -189,6 +190,101 @@ def cpu_baseline(seconds, elems):
                 break
         out["all_cores"] = {"value": round(calls * n * BYTES_PER_ELEM / el / 2**30, 3), "unit": "GiB/s",
                             "cores": cores, "sample": f"{calls} calls, {el:.1f} s, {cores} threads"}
+    return out
+
+
+# Per-(op, type) roofline at the same 256 MiB per operand (reported beside
+# `value`, never part of it): the ops of configs 4 and 5 (MAX over DOUBLE,
+# BAND over UINT64_T) plus one representative of every kernel family
+# (integer wrap, complex arithmetic, logical, loc structs).
+PER_OP = [
+    ("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_DOUBLE"), ("MPI_SUM", "MPI_INT"),
+    ("MPI_SUM", "MPI_INT8_T"), ("MPI_SUM", "MPI_INT64_T"), ("MPI_PROD", "MPI_FLOAT"),
+    ("MPI_PROD", "MPI_INT16_T"), ("MPI_SUM", "MPI_C_FLOAT_COMPLEX"),
+    ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX"), ("MPI_MAX", "MPI_DOUBLE"), ("MPI_MIN", "MPI_FLOAT"),
+    ("MPI_MAX", "MPI_UNSIGNED_CHAR"), ("MPI_BAND", "MPI_UINT64_T"), ("MPI_BXOR", "MPI_BYTE"),
+    ("MPI_LAND", "MPI_INT"), ("MPI_LXOR", "MPI_C_BOOL"), ("MPI_MAXLOC", "MPI_2INT"),
+    ("MPI_MINLOC", "MPI_DOUBLE_INT"), ("MPI_MAXLOC", "MPI_SHORT_INT"), ("MPI_MINLOC", "MPI_2DOUBLE_PRECISION"),
+]
+
+
+def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
+    """GB/s of HBM traffic (2 reads + 1 write per element) per (op, type), from
+    HIP events on the launch stream around 10 launches (median of 3 rounds).
+    Operands are random bytes interpreted as the MPI type, except floating
+    types, which get finite uniform values (no NaN slow path)."""
+    import ctypes
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    out = {}
+    for opn, dtn in PER_OP:
+        op, dt = getattr(C, opn), getattr(C, dtn)
+        sz = ctypes.c_int(0)
+        L.MPI_Type_size(dt, ctypes.byref(sz))
+        n = nbytes // sz.value
+        with torch.cuda.stream(stream):
+            a.random_(0, 256)
+            b.random_(0, 256)
+            if dtn in ("MPI_FLOAT", "MPI_C_FLOAT_COMPLEX"):
+                a.view(torch.float32).uniform_(-1, 1)
+                b.view(torch.float32).uniform_(-1, 1)
+            elif dtn in ("MPI_DOUBLE", "MPI_C_DOUBLE_COMPLEX", "MPI_2DOUBLE_PRECISION"):
+                a.view(torch.float64).uniform_(-1, 1)
+                b.view(torch.float64).uniform_(-1, 1)
+            elif dtn == "MPI_DOUBLE_INT":                      # {f64, i32, pad}
+                a.view(torch.float64)[0::2].uniform_(-1, 1)
+                b.view(torch.float64)[0::2].uniform_(-1, 1)
+        ts = []
+        for _ in range(3):
+            for _ in range(2):
+                L.msx_reduce_local_dev(a.data_ptr(), b.data_ptr(), n, dt, op, sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(10):
+                rc = L.msx_reduce_local_dev(a.data_ptr(), b.data_ptr(), n, dt, op, sp)
+                if rc:
+                    raise RuntimeError(f"{opn}/{dtn}: rc={rc}")
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 10)
+        ms = sorted(ts)[1]
+        gbs = 3 * n * sz.value / ms / 1e6
+        out[f"{opn}/{dtn}"] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1),
+                               "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    # the collective combine (k_tree): p = 8 contributions of 32 MiB reduced in
+    # the reference's tree order into one output, (p + 1) x 32 MiB of traffic
+    p, m = 8, nbytes // 8 // 4
+    srcs = (ctypes.c_void_p * p)(*[a.data_ptr() + r * m * 4 for r in range(p)])
+    a.view(torch.float32).uniform_(-1, 1)
+
+    def time_tree():
+        ts = []
+        for _ in range(3):
+            L.msx_reduce_tree_dev(srcs, p, b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(10):
+                rc = L.msx_reduce_tree_dev(srcs, p, b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, sp)
+                if rc:
+                    raise RuntimeError(f"tree: rc={rc}")
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 10)
+        return sorted(ts)[1]
+
+    def entry(ms):
+        gbs = (p + 1) * m * 4 / ms / 1e6
+        return {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+    out["tree8/MPI_SUM/MPI_FLOAT"] = entry(time_tree())
+    if tree_sweep:
+        for mode, name in enumerate(("interleaved", "upfront", "upfront_nt", "interleaved_nt")):
+            for cap in (1024, 2048, 4096, 8192, 65536):
+                L.msx_tune_tree(mode, cap)
+                out[f"tree8_sweep/{name}/cap{cap}"] = entry(time_tree())
+        L.msx_tune_tree(0, 0)
+    del a, b
     return out
 
 
@@ -336,6 +432,10 @@ def main():
         dt_b = (time.perf_counter() - t1) / reps
         host["device_blocking_MPI_Reduce_local_GiB_s"] = round(n * BYTES_PER_ELEM / dt_b / 2**30, 1)
 
+    per_op = None
+    if rank == 0 and world == 1 and not args.no_per_op:
+        per_op = per_op_roofline(L, C, torch, dev, stream, n * 4, tree_sweep=args.sweep)
+
     if rank == 0:
         total_bytes = world * args.steps * n * BYTES_PER_ELEM
         value = total_bytes / elapsed / 2**30
@@ -376,6 +476,8 @@ def main():
             out["collectives_rccl_transport"] = coll_rccl
         if rccl_native is not None:
             out["rccl_native_allreduce_f32"] = rccl_native
+        if per_op is not None:
+            out["per_op_roofline_hbm"] = per_op
         if sweep:
             out["variant_sweep_GB_s"] = sweep
         if world == 1:

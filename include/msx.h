@@ -69,6 +69,11 @@ int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count
  * a cap on workgroups (0 = one tile per workgroup). */
 int msx_tune_set(int variant, int grid_cap);
 int msx_tune_variant_count(void);
+/* collective tree combine (msx_reduce_tree_dev and the engine), fp32 SUM only:
+ * mode 0 = default (loads interleaved with the combines), 1 = all sources
+ * loaded up front, 2 = up front + non-temporal, 3 = interleaved +
+ * non-temporal; grid_cap 0 = default. */
+int msx_tune_tree(int mode, int grid_cap);
 const char* msx_tune_variant_name(int variant);
 
 /* host staging chunk size (bytes) for MPI_Reduce_local on host buffers */

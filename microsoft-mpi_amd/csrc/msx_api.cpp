@@ -1091,6 +1091,11 @@ MSX_EXPORT int msx_tune_set(int variant, int grid_cap)
     return MPI_SUCCESS;
 }
 
+MSX_EXPORT int msx_tune_tree(int mode, int grid_cap)
+{
+    return tree_tune_set(mode, grid_cap) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
+}
+
 MSX_EXPORT int msx_tune_variant_count(void) { return combine_variant_count(); }
 MSX_EXPORT const char* msx_tune_variant_name(int v) { return combine_variant_name(v); }
 

@@ -54,6 +54,14 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
 hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size_t* nbytes,
                             int nseg, bool sys, hipStream_t s);
 
+// Tuning of the collective tree combine (fp32 SUM only; other pairs use the
+// default): mode 0 = default (loads interleaved with the combines, plain),
+// 1 = all sources loaded up front, 2 = up front + non-temporal,
+// 3 = interleaved + non-temporal;
+// grid_cap 0 = default cap.  Returns 0, or -1 for an invalid setting.
+struct TreeTune { int mode = 0; int grid_cap = 0; };
+int tree_tune_set(int mode, int grid_cap);
+
 // Number of tuning variants compiled for the fp32 SUM hot path.
 int combine_variant_count();
 const char* combine_variant_name(int v);

@@ -183,6 +183,15 @@ __device__ __forceinline__ void st(u32x4* p, u32x4 v)
     else *p = v;
 }
 
+// Both registers are inputs of one (empty) asm statement: their loads are
+// issued back to back and waited for together, and no use of either can be
+// scheduled between them.
+__device__ __forceinline__ void issued_together(u32x4& x, u32x4& y)
+{
+    asm volatile("" : "+v"(x), "+v"(y));
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // ---- the streaming combine -------------------------------------------------------
 // Elements [0, head) and [head + nvec*EPV, head + nvec*EPV + tail) are scalar;
 // the vector body starts at element `head`, 16-byte aligned for both operands.
@@ -207,6 +216,12 @@ __device__ __forceinline__ void combine_body(const T* __restrict__ in, T* __rest
                 a[u] = ld<NTLD>(vin + i0 + (size_t)u * BLOCK);
                 b[u] = ld<NTLD>(vio + i0 + (size_t)u * BLOCK);
             }
+            // Every load of the tile is issued before the first use: without
+            // this the compiler hoists work on the first operand (logical ops,
+            // complex, byte types) above the second load behind an
+            // s_waitcnt vmcnt(0), halving the bytes in flight (-7..10 %).
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) issued_together(a[u], b[u]);
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u)
                 st<NTST>(vio + i0 + (size_t)u * BLOCK, apply_vec<OP, VT>(b[u], a[u]));
@@ -214,7 +229,11 @@ __device__ __forceinline__ void combine_body(const T* __restrict__ in, T* __rest
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
                 const size_t i = i0 + (size_t)u * BLOCK;
-                if (i < nvec) vio[i] = apply_vec<OP, VT>(vio[i], vin[i]);
+                if (i < nvec) {
+                    u32x4 x = vin[i], y = vio[i];
+                    issued_together(x, y);
+                    vio[i] = apply_vec<OP, VT>(y, x);
+                }
             }
         }
     }
@@ -349,11 +368,56 @@ __device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
     return v[0];
 }
 
+// The same tree over 16-byte vectors, with every source vector loaded
+// (non-temporal: each is read once) before the first combine, so all of them
+// are in flight together.
+template <class F, bool NT>
+__device__ __forceinline__ u32x4 tree_vec(const TreeArgs& a, size_t i)
+{
+    auto ld_src = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
+    u32x4 v[kMaxLeaves], w[kMaxLeaves];
+    if (a.chain) {
+#pragma unroll
+        for (int k = 0; k < kMaxLeaves; ++k)
+            if (k < a.P) v[k] = ld_src(k);
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 r = v[0];
+#pragma unroll
+        for (int k = 1; k < kMaxLeaves; ++k)
+            if (k < a.P) r = F::apply(r, v[k]);
+        return r;
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxLeaves; ++k) {
+        if (k < a.nleaves) {
+            v[k] = ld_src(2 * k);
+            if ((a.pairmask >> k) & 1u) w[k] = ld_src(2 * k + 1);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < kMaxLeaves; ++k)
+        if (k < a.nleaves && ((a.pairmask >> k) & 1u)) v[k] = F::apply(v[k], w[k]);
+#pragma unroll
+    for (int d = 1; d < kMaxLeaves; d *= 2) {
+#pragma unroll
+        for (int k = 0; k + d < kMaxLeaves; k += 2 * d)
+            if (k + d < a.nleaves) v[k] = F::apply(v[k], v[k + d]);
+    }
+    return v[0];
+}
+
 template <int OP, class VT> struct VecFn {
     __device__ static u32x4 apply(u32x4 io, u32x4 in) { return apply_vec<OP, VT>(io, in); }
 };
 
-template <int OP, class T, class VT, int BLOCK>
+// UPFRONT: all source vectors loaded before the first combine (tree_vec), else
+// loads interleaved with the combines as the tree consumes them (tree_eval);
+// NT: non-temporal source loads.  The fp32 SUM tuning sweep times all four
+// (p = 8, 32 MiB each): interleaved plain loads 51.7 us (5.8 TB/s), up front
+// 57.1 us -- holding every source vector costs 146 VGPRs instead of 77, half
+// the waves per SIMD -- and non-temporal loads 3-8 % slower either way.
+template <int OP, class T, class VT, int BLOCK, bool UPFRONT = false, bool NT = false>
 __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out, size_t nvec,
                                                 size_t tail, int vec_ok)
 {
@@ -362,8 +426,13 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
     if (a.sys) acquire_system();
     if (vec_ok) {
         for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < nvec; i += stride) {
-            auto load = [&](int k) { return reinterpret_cast<const u32x4*>(a.s[k])[i]; };
-            const u32x4 r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
+            u32x4 r;
+            if constexpr (UPFRONT) {
+                r = tree_vec<VecFn<OP, VT>, NT>(a, i);
+            } else {
+                auto load = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
+                r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
+            }
             reinterpret_cast<u32x4*>(out)[i] = r;
             for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
         }
@@ -427,6 +496,7 @@ using namespace dev;
 
 constexpr int kBlock = 256;
 constexpr int kUnroll = 1;
+constexpr int kTreeGridCap = 4096;
 
 template <class T>
 inline void split(const void* in, const void* io, size_t count, size_t& head, size_t& nvec,
@@ -565,7 +635,9 @@ hipError_t dispatch_loc(Kind k, const void* in, void* io, size_t n, hipStream_t 
 }
 
 // ---- tree dispatch ----
-template <int OP, class T, class VT>
+TreeTune g_tree_tune;
+
+template <int OP, class T, class VT, bool UPFRONT = false, bool NT = false>
 hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     bool ok = ((uintptr_t)out & 15) == 0;
@@ -576,9 +648,10 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
     const size_t nvec = count / epv, tail = count - nvec * epv;
     const size_t work = ok ? nvec + tail : count;
     size_t grid = (work + kBlock - 1) / kBlock;
-    if (grid > 4096) grid = 4096;
+    const size_t cap = g_tree_tune.grid_cap > 0 ? (size_t)g_tree_tune.grid_cap : (size_t)kTreeGridCap;
+    if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_tree<OP, T, VT, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, s, a,
+    hipLaunchKernelGGL((k_tree<OP, T, VT, kBlock, UPFRONT, NT>), dim3((unsigned)grid), dim3(kBlock), 0, s, a,
                        static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
     return hipGetLastError();
 }
@@ -624,6 +697,14 @@ hipError_t tree_loc(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipS
 }
 
 }  // namespace
+
+int tree_tune_set(int mode, int grid_cap)
+{
+    if (mode < 0 || mode > 3 || grid_cap < 0) return -1;
+    g_tree_tune.mode = mode;
+    g_tree_tune.grid_cap = grid_cap;
+    return 0;
+}
 
 int combine_variant_count() { return kNumVariants; }
 const char* combine_variant_name(int v)
@@ -701,6 +782,14 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0) {
         if (t.src[0] == out) return hipSuccess;
         return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
+    }
+    if (opidx == O_SUM && k == K_F32 && g_tree_tune.mode != 0) {
+        switch (g_tree_tune.mode) {
+        case 1: return run_tree<O_SUM, float, float, true, false>(a, ns, out, n, s);
+        case 2: return run_tree<O_SUM, float, float, true, true>(a, ns, out, n, s);
+        case 3: return run_tree<O_SUM, float, float, false, true>(a, ns, out, n, s);
+        default: return hipErrorInvalidValue;
+        }
     }
     switch (opidx) {
     case O_SUM:  return tree_arith<O_SUM>(k, a, ns, out, n, s);
