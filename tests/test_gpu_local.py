@@ -310,3 +310,36 @@ def test_plain_c_program_runs_on_the_gpu(tmp_path):
                        env={**os.environ, "MSX_SIZE": "1", "MSX_RANK": "0"})
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("OK ")
+
+
+def test_maximum_count_int_max_fp32(L):
+    """Largest count the MPI API admits (count is an int, mpi.h:2352):
+    MPI_Reduce_local over 2^31-1 fp32 (8 GiB per operand) on device buffers,
+    checked in full against torch's fp32 add (one IEEE add per element) and
+    at the ragged last elements.  The kernels index in 64 bits."""
+    n = (1 << 31) - 1
+    g = torch.Generator(device="cuda").manual_seed(7)
+    a = torch.rand(n, device="cuda", generator=g)
+    b = torch.rand(n, device="cuda", generator=g) - 0.5
+    exp = a + b
+    assert L.MPI_Reduce_local(a.data_ptr(), b.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(b.view(torch.int32), exp.view(torch.int32))
+    del a, b, exp
+    torch.cuda.empty_cache()
+
+
+def test_device_entry_beyond_4gib_bytes(L):
+    """msx_reduce_local_dev takes a 64-bit count: 2^32 + 13 bytes of MPI_BXOR
+    over MPI_BYTE (crosses every 32-bit byte-offset boundary), plus an odd
+    start so the head/tail paths run too."""
+    n = (1 << 32) + 13
+    a = torch.empty(n + 1, dtype=torch.uint8, device="cuda").random_(0, 256)
+    b = torch.empty(n + 1, dtype=torch.uint8, device="cuda").random_(0, 256)
+    exp = b[1:] ^ a[1:]
+    rc = L.msx_reduce_local_dev(a.data_ptr() + 1, b.data_ptr() + 1, n, C.MPI_BYTE, C.MPI_BXOR, _stream())
+    assert rc == 0, msx.last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(b[1:], exp)
+    del a, b, exp
+    torch.cuda.empty_cache()
