@@ -303,6 +303,95 @@ MPI_METHOD MPI_Compare_and_swap(const void* origin_addr, const void* compare_add
                                 void* result_addr, MPI_Datatype datatype, int target_rank,
                                 MPI_Aint target_disp, MPI_Win win);
 
+/* ---- derived datatypes (mpi.h:1340-1822) and pack/unpack (mpi.h:1823-1887)
+ * Constructors, queries and MPI_Pack/MPI_Unpack; the bytes are moved by the
+ * gfx950 pack kernels.  Derived types are accepted by MPI_Pack/MPI_Unpack and
+ * the one-sided calls; the reduction collectives take predefined types. */
+#define MPI_ORDER_C         56
+#define MPI_ORDER_FORTRAN   57
+
+enum {                                  /* mpi.h:1758-1778 */
+    MPI_COMBINER_NAMED            = 1,
+    MPI_COMBINER_DUP              = 2,
+    MPI_COMBINER_CONTIGUOUS       = 3,
+    MPI_COMBINER_VECTOR           = 4,
+    MPI_COMBINER_HVECTOR_INTEGER  = 5,
+    MPI_COMBINER_HVECTOR          = 6,
+    MPI_COMBINER_INDEXED          = 7,
+    MPI_COMBINER_HINDEXED_INTEGER = 8,
+    MPI_COMBINER_HINDEXED         = 9,
+    MPI_COMBINER_INDEXED_BLOCK    = 10,
+    MPI_COMBINER_STRUCT_INTEGER   = 11,
+    MPI_COMBINER_STRUCT           = 12,
+    MPI_COMBINER_SUBARRAY         = 13,
+    MPI_COMBINER_DARRAY           = 14,
+    MPI_COMBINER_F90_REAL         = 15,
+    MPI_COMBINER_F90_COMPLEX      = 16,
+    MPI_COMBINER_F90_INTEGER      = 17,
+    MPI_COMBINER_RESIZED          = 18,
+    MPI_COMBINER_HINDEXED_BLOCK   = 19
+};
+
+MPI_METHOD MPI_Type_contiguous(int count, MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_vector(int count, int blocklength, int stride, MPI_Datatype oldtype,
+                           MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_hvector(int count, int blocklength, MPI_Aint stride,
+                                   MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_hvector(int count, int blocklength, MPI_Aint stride, MPI_Datatype oldtype,
+                            MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_indexed(int count, const int array_of_blocklengths[],
+                            const int array_of_displacements[], MPI_Datatype oldtype,
+                            MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_hindexed(int count, const int array_of_blocklengths[],
+                                    const MPI_Aint array_of_displacements[],
+                                    MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_hindexed(int count, const int array_of_blocklengths[],
+                             const MPI_Aint array_of_displacements[], MPI_Datatype oldtype,
+                             MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_indexed_block(int count, int blocklength,
+                                         const int array_of_displacements[],
+                                         MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_hindexed_block(int count, int blocklength,
+                                          const MPI_Aint array_of_displacements[],
+                                          MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_struct(int count, const int array_of_blocklengths[],
+                                  const MPI_Aint array_of_displacements[],
+                                  const MPI_Datatype array_of_types[], MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_struct(int count, const int array_of_blocklengths[],
+                           const MPI_Aint array_of_displacements[],
+                           const MPI_Datatype array_of_types[], MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_subarray(int ndims, const int array_of_sizes[],
+                                    const int array_of_subsizes[], const int array_of_starts[],
+                                    int order, MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_resized(MPI_Datatype oldtype, MPI_Aint lb, MPI_Aint extent,
+                                   MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_dup(MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_commit(MPI_Datatype* datatype);
+MPI_METHOD MPI_Type_free(MPI_Datatype* datatype);
+MPI_METHOD MPI_Type_size_x(MPI_Datatype datatype, MPI_Count* size);
+MPI_METHOD MPI_Type_get_extent(MPI_Datatype datatype, MPI_Aint* lb, MPI_Aint* extent);
+MPI_METHOD MPI_Type_get_extent_x(MPI_Datatype datatype, MPI_Count* lb, MPI_Count* extent);
+MPI_METHOD MPI_Type_get_true_extent(MPI_Datatype datatype, MPI_Aint* true_lb,
+                                    MPI_Aint* true_extent);
+MPI_METHOD MPI_Type_get_true_extent_x(MPI_Datatype datatype, MPI_Count* true_lb,
+                                      MPI_Count* true_extent);
+MPI_METHOD MPI_Type_extent(MPI_Datatype datatype, MPI_Aint* extent);
+MPI_METHOD MPI_Type_lb(MPI_Datatype datatype, MPI_Aint* displacement);
+MPI_METHOD MPI_Type_ub(MPI_Datatype datatype, MPI_Aint* displacement);
+MPI_METHOD MPI_Type_get_envelope(MPI_Datatype datatype, int* num_integers, int* num_addresses,
+                                 int* num_datatypes, int* combiner);
+MPI_METHOD MPI_Type_get_contents(MPI_Datatype datatype, int max_integers, int max_addresses,
+                                 int max_datatypes, int array_of_integers[],
+                                 MPI_Aint array_of_addresses[],
+                                 MPI_Datatype array_of_datatypes[]);
+MPI_METHOD MPI_Get_address(const void* location, MPI_Aint* address);
+MPI_METHOD MPI_Address(void* location, MPI_Aint* address);
+MPI_METHOD MPI_Pack(const void* inbuf, int incount, MPI_Datatype datatype, void* outbuf,
+                    int outsize, int* position, MPI_Comm comm);
+MPI_METHOD MPI_Unpack(const void* inbuf, int insize, int* position, void* outbuf, int outcount,
+                      MPI_Datatype datatype, MPI_Comm comm);
+MPI_METHOD MPI_Pack_size(int incount, MPI_Datatype datatype, MPI_Comm comm, int* size);
+
 /* ---- profiling interface aliases (msmpi.def:101-102,422-423,478-483,...) -- */
 MPI_METHOD PMPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
                              MPI_Datatype datatype, MPI_Op op);

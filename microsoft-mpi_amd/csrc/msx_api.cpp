@@ -195,6 +195,20 @@ int v_op(MPI_Op op, MPI_Datatype dt, OpRef* out)
 
 }  // namespace
 
+// ---- entry-point helpers shared with msx_dtype_api.cpp -----------------------
+namespace msx {
+void api_require_init(const char* fn)
+{
+    if (!is_initialized() || is_finalized()) not_initialized_exit(fn);
+}
+int api_err_return(const char* fn, int code) { return err_return(nullptr, fn, code); }
+int api_comm_valid(MPI_Comm comm)
+{
+    Comm* c;
+    return v_comm(comm, &c);
+}
+}  // namespace msx
+
 // ===========================================================================
 // environment
 // ===========================================================================
@@ -325,17 +339,6 @@ MSX_EXPORT int MPI_Error_string(int errorcode, char* str, int* len)
     if (!str || !len) return MPI_ERR_ARG;
     int n = snprintf(str, MPI_MAX_ERROR_STRING, "%s", class_string(errorcode & 0x7f));
     *len = n < MPI_MAX_ERROR_STRING ? n : MPI_MAX_ERROR_STRING - 1;
-    return MPI_SUCCESS;
-}
-
-MSX_EXPORT int MPI_Type_size(MPI_Datatype dt, int* size)
-{
-    MSX_REQUIRE_INIT("MPI_Type_size");
-    int rc = MPI_SUCCESS;
-    if (dt == MPI_DATATYPE_NULL || !dtype_known(dt)) { set_error("invalid datatype"); rc = MPI_ERR_TYPE; }
-    else if (!size) rc = MPI_ERR_ARG;
-    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Type_size", rc);
-    *size = type_size(dt);
     return MPI_SUCCESS;
 }
 

@@ -1,0 +1,294 @@
+// msx_pack.hip — gfx950 kernels of the derived-datatype engine (msx_dtype.h).
+//
+// The reference interprets a dataloop tree on the CPU, one contiguous piece at
+// a time (MPID_Segment_pack / unpack, mpid/segment.cpp; the accumulate walk of
+// packethandling.cpp:2969-3004).  Here a committed type is a flat list of byte
+// runs, and every work item maps one packed granule straight to its typed
+// address:
+//
+//   packed byte p of instance i  ->  typed[i*extent + disp[k] + (p - poff[k])]
+//
+// with k found by a magic-number division for regular layouts (vector,
+// hvector, subarray rows: run k = first + k*stride) and by a binary search
+// over the run offsets otherwise.  The granule G is the largest power of two
+// <= 16 that divides every run offset / length, the size, the extent and both
+// pointers, so a granule never straddles two runs and every access is a
+// naturally aligned G-byte load or store.  The kernels are HBM-bound byte
+// movers (no arithmetic beyond the address map); a pack moves 2*size bytes per
+// instance.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "msx_dev_ops.h"
+#include "msx_dtype.h"
+#include "msx_kernels.h"
+
+namespace msx {
+namespace dev {
+
+// q = n / d for any 32-bit n (Granlund-Montgomery round-up method).
+struct FastDiv {
+    uint32_t d = 1, m = 0, s = 0;
+    FastDiv() = default;
+    explicit FastDiv(uint32_t div) : d(div)
+    {
+        s = 0;
+        while ((1ull << s) < div) ++s;
+        m = (uint32_t)((((1ull << 32) * ((1ull << s) - div)) / div) + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const
+    {
+        return (uint32_t)(((uint64_t)__umulhi(n, m) + n) >> s);
+    }
+};
+
+struct CopyArgs {
+    char* typed;
+    char* packed;
+    int64_t ngran;           // granules in the packed stream (count * size / G)
+    int64_t extent;          // bytes
+    int64_t size;            // bytes per instance
+    // regular layout, in granules where noted
+    int64_t first;           // bytes
+    int64_t stride;          // bytes
+    int64_t gsize, gblen;    // granules
+    FastDiv fd_size, fd_blen;
+    // general layout
+    const int64_t* disp;
+    const int64_t* poff;
+    int64_t nruns;
+};
+
+constexpr int kPackBlock = 256;
+
+template <int G> struct GranT;
+template <> struct GranT<1> { typedef uint8_t T; };
+template <> struct GranT<2> { typedef uint16_t T; };
+template <> struct GranT<4> { typedef uint32_t T; };
+template <> struct GranT<8> { typedef uint64_t T; };
+template <> struct GranT<16> { typedef u32x4 T; };
+
+// Largest k with poff[k] <= q (poff[0] = 0, poff[nruns] = size > q).
+__device__ __forceinline__ int64_t find_run(const int64_t* __restrict__ poff, int64_t nruns, int64_t q)
+{
+    int64_t lo = 0, hi = nruns;      // invariant: poff[lo] <= q < poff[hi]
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (poff[mid] <= q) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Byte offset (from the typed base) of packed granule g.
+template <int G, bool REG, bool NARROW>
+__device__ __forceinline__ int64_t typed_off(const CopyArgs& a, int64_t g)
+{
+    int64_t i, q;
+    if constexpr (NARROW) {
+        const uint32_t gi = (uint32_t)a.fd_size.div((uint32_t)g);
+        i = gi;
+        q = g - (int64_t)gi * a.gsize;
+    } else {
+        i = g / a.gsize;
+        q = g - i * a.gsize;
+    }
+    if constexpr (REG) {
+        int64_t k;
+        if constexpr (NARROW) k = a.fd_blen.div((uint32_t)q);
+        else k = q / a.gblen;
+        const int64_t off = q - k * a.gblen;
+        return i * a.extent + a.first + k * a.stride + off * G;
+    } else {
+        const int64_t qb = q * G;
+        const int64_t k = find_run(a.poff, a.nruns, qb);
+        return i * a.extent + a.disp[k] + (qb - a.poff[k]);
+    }
+}
+
+template <int G, bool REG, bool NARROW, bool UNPACK>
+__global__ __launch_bounds__(kPackBlock) void k_dt_pack(CopyArgs a)
+{
+    typedef typename GranT<G>::T T;
+    const int64_t stride = (int64_t)gridDim.x * kPackBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kPackBlock + threadIdx.x; g < a.ngran; g += stride) {
+        T* t = reinterpret_cast<T*>(a.typed + typed_off<G, REG, NARROW>(a, g));
+        T* p = reinterpret_cast<T*>(a.packed) + g;
+        if constexpr (UNPACK) *t = __builtin_nontemporal_load(p);
+        else __builtin_nontemporal_store(*t, p);
+    }
+}
+
+// typed element (op)= packed element.  E = element bytes; granules are whole
+// elements.  ALIGNED: every element address is a multiple of alignof(T);
+// otherwise the element moves through byte copies.
+template <int OP, class T, bool REG, bool ALIGNED>
+__global__ __launch_bounds__(kPackBlock) void k_dt_acc(CopyArgs a)
+{
+    constexpr int E = (int)sizeof(T);
+    const int64_t stride = (int64_t)gridDim.x * kPackBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kPackBlock + threadIdx.x; g < a.ngran; g += stride) {
+        char* t = a.typed + typed_off<E, REG, false>(a, g);
+        const char* p = a.packed + g * E;
+        if constexpr (ALIGNED) {
+            T* tt = reinterpret_cast<T*>(t);
+            *tt = Fn<OP>::apply(*tt, *reinterpret_cast<const T*>(p));
+        } else {
+            T x, y;
+            __builtin_memcpy(&x, t, E);
+            __builtin_memcpy(&y, p, E);
+            x = Fn<OP>::apply(x, y);
+            __builtin_memcpy(t, &x, E);
+        }
+    }
+}
+
+// ---- host side ---------------------------------------------------------------
+int grid_for(int64_t n)
+{
+    // a few waves of workgroups over 256 CUs; the loops are grid-stride
+    const int64_t want = (n + kPackBlock - 1) / kPackBlock;
+    return (int)(want < 8192 ? (want > 0 ? want : 1) : 8192);
+}
+
+CopyArgs make_args(const DevLayout& L, int64_t count, void* typed, void* packed, int G)
+{
+    CopyArgs a{};
+    a.typed = static_cast<char*>(typed);
+    a.packed = static_cast<char*>(packed);
+    a.extent = L.extent;
+    a.size = L.size;
+    a.gsize = L.size / G;
+    a.ngran = count * a.gsize;
+    if (L.regular) {
+        a.first = L.first;
+        a.stride = L.stride;
+        a.gblen = L.blen / G;
+    } else {
+        a.disp = L.disp;
+        a.poff = L.poff;
+        a.nruns = L.nruns;
+    }
+    a.fd_size = FastDiv((uint32_t)(a.gsize < 0xffffffffll ? a.gsize : 1));
+    a.fd_blen = FastDiv((uint32_t)(a.gblen > 0 && a.gblen < 0xffffffffll ? a.gblen : 1));
+    return a;
+}
+
+template <int G, bool UNPACK>
+hipError_t run_copy(const CopyArgs& a, bool reg, hipStream_t s)
+{
+    const bool narrow = a.ngran < (int64_t)0xffffffffll;
+    const dim3 grid(grid_for(a.ngran)), block(kPackBlock);
+    if (reg && narrow) hipLaunchKernelGGL((k_dt_pack<G, true, true, UNPACK>), grid, block, 0, s, a);
+    else if (reg) hipLaunchKernelGGL((k_dt_pack<G, true, false, UNPACK>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_dt_pack<G, false, false, UNPACK>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+template <bool UNPACK>
+hipError_t copy_g(int G, const CopyArgs& a, bool reg, hipStream_t s)
+{
+    switch (G) {
+    case 16: return run_copy<16, UNPACK>(a, reg, s);
+    case 8: return run_copy<8, UNPACK>(a, reg, s);
+    case 4: return run_copy<4, UNPACK>(a, reg, s);
+    case 2: return run_copy<2, UNPACK>(a, reg, s);
+    default: return run_copy<1, UNPACK>(a, reg, s);
+    }
+}
+
+// Which (op, element) pairs have a kernel: the builtin ops' tables (op.cpp:739-1883).
+template <int OP, class T> struct AccLegal {
+    static constexpr bool arith = std::is_arithmetic<T>::value;
+    static constexpr bool value =
+        ((OP == O_MAX || OP == O_MIN || OP == O_LAND || OP == O_LOR || OP == O_LXOR) && arith) ||
+        ((OP == O_SUM || OP == O_PROD) && (arith || std::is_same<T, c32>::value || std::is_same<T, c64>::value)) ||
+        ((OP == O_BAND || OP == O_BOR || OP == O_BXOR) && std::is_integral<T>::value) ||
+        ((OP == O_MAXLOC || OP == O_MINLOC) &&
+         (std::is_same<T, loc_ii>::value || std::is_same<T, loc_fi>::value || std::is_same<T, loc_si>::value ||
+          std::is_same<T, loc_di>::value || std::is_same<T, loc_ff>::value || std::is_same<T, loc_dd>::value));
+};
+
+template <int OP, class T>
+hipError_t run_acc(const DevLayout& L, int64_t count, const void* packed, void* typed, hipStream_t s)
+{
+    if constexpr (!AccLegal<OP, T>::value) {
+        return hipErrorInvalidValue;
+    } else {
+        constexpr int E = (int)sizeof(T);
+        // every run offset / length must hold whole elements for the element map
+        if (L.size % E) return hipErrorInvalidValue;
+        CopyArgs a = make_args(L, count, typed, const_cast<void*>(packed), E);
+        if (L.regular && (L.blen % E)) return hipErrorInvalidValue;
+        const bool aligned = L.align >= (int)alignof(T);
+        const bool reg = L.regular != 0;
+        const dim3 grid(grid_for(a.ngran)), block(kPackBlock);
+        if (reg && aligned) hipLaunchKernelGGL((k_dt_acc<OP, T, true, true>), grid, block, 0, s, a);
+        else if (reg) hipLaunchKernelGGL((k_dt_acc<OP, T, true, false>), grid, block, 0, s, a);
+        else if (aligned) hipLaunchKernelGGL((k_dt_acc<OP, T, false, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_dt_acc<OP, T, false, false>), grid, block, 0, s, a);
+        return hipGetLastError();
+    }
+}
+
+template <int OP>
+hipError_t acc_kind(Kind k, const DevLayout& L, int64_t count, const void* packed, void* typed, hipStream_t s)
+{
+    switch (k) {
+    case K_I8: return run_acc<OP, int8_t>(L, count, packed, typed, s);
+    case K_U8: case K_BOOL: return run_acc<OP, uint8_t>(L, count, packed, typed, s);
+    case K_I16: return run_acc<OP, int16_t>(L, count, packed, typed, s);
+    case K_U16: return run_acc<OP, uint16_t>(L, count, packed, typed, s);
+    case K_I32: return run_acc<OP, int32_t>(L, count, packed, typed, s);
+    case K_U32: return run_acc<OP, uint32_t>(L, count, packed, typed, s);
+    case K_I64: return run_acc<OP, int64_t>(L, count, packed, typed, s);
+    case K_U64: return run_acc<OP, uint64_t>(L, count, packed, typed, s);
+    case K_F32: return run_acc<OP, float>(L, count, packed, typed, s);
+    case K_F64: return run_acc<OP, double>(L, count, packed, typed, s);
+    case K_C32: return run_acc<OP, c32>(L, count, packed, typed, s);
+    case K_C64: return run_acc<OP, c64>(L, count, packed, typed, s);
+    case K_LOC_II: return run_acc<OP, loc_ii>(L, count, packed, typed, s);
+    case K_LOC_FI: return run_acc<OP, loc_fi>(L, count, packed, typed, s);
+    case K_LOC_SI: return run_acc<OP, loc_si>(L, count, packed, typed, s);
+    case K_LOC_DI: return run_acc<OP, loc_di>(L, count, packed, typed, s);
+    case K_LOC_FF: return run_acc<OP, loc_ff>(L, count, packed, typed, s);
+    case K_LOC_DD: return run_acc<OP, loc_dd>(L, count, packed, typed, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace dev
+
+hipError_t launch_dt_copy(const DevLayout& L, int64_t count, void* typed, void* packed, bool unpack,
+                          hipStream_t s)
+{
+    if (count <= 0 || L.size == 0) return hipSuccess;
+    const int G = L.align;
+    if (G < 1 || G > 16 || (G & (G - 1)) || L.size % G || (L.regular && L.blen % G))
+        return hipErrorInvalidValue;
+    dev::CopyArgs a = dev::make_args(L, count, typed, packed, G);
+    return unpack ? dev::copy_g<true>(G, a, L.regular != 0, s) : dev::copy_g<false>(G, a, L.regular != 0, s);
+}
+
+hipError_t launch_dt_acc(int opidx, Kind k, const DevLayout& L, int64_t count, const void* packed,
+                         void* typed, hipStream_t s)
+{
+    if (count <= 0 || L.size == 0) return hipSuccess;
+    switch (opidx) {
+    case O_MAX: return dev::acc_kind<O_MAX>(k, L, count, packed, typed, s);
+    case O_MIN: return dev::acc_kind<O_MIN>(k, L, count, packed, typed, s);
+    case O_SUM: return dev::acc_kind<O_SUM>(k, L, count, packed, typed, s);
+    case O_PROD: return dev::acc_kind<O_PROD>(k, L, count, packed, typed, s);
+    case O_LAND: return dev::acc_kind<O_LAND>(k, L, count, packed, typed, s);
+    case O_BAND: return dev::acc_kind<O_BAND>(k, L, count, packed, typed, s);
+    case O_LOR: return dev::acc_kind<O_LOR>(k, L, count, packed, typed, s);
+    case O_BOR: return dev::acc_kind<O_BOR>(k, L, count, packed, typed, s);
+    case O_LXOR: return dev::acc_kind<O_LXOR>(k, L, count, packed, typed, s);
+    case O_BXOR: return dev::acc_kind<O_BXOR>(k, L, count, packed, typed, s);
+    case O_MINLOC: return dev::acc_kind<O_MINLOC>(k, L, count, packed, typed, s);
+    case O_MAXLOC: return dev::acc_kind<O_MAXLOC>(k, L, count, packed, typed, s);
+    case O_REPLACE: return launch_dt_copy(L, count, typed, const_cast<void*>(packed), true, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace msx

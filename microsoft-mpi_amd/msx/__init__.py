@@ -25,8 +25,13 @@ def _parse_header_constants(path):
     """#define NAME value / ((T)0x...) from include/mpi.h -> dict (ints only)."""
     out = {}
     pat = re.compile(r"^#define\s+(MPI_\w+)\s+(.+?)\s*(?:/\*.*)?$")
+    enum = re.compile(r"^(MPI_\w+)\s*=\s*(\d+),?$")
     with open(path) as f:
         for line in f:
+            e = enum.match(line.strip())
+            if e:
+                out[e.group(1)] = int(e.group(2))
+                continue
             m = pat.match(line.strip())
             if not m:
                 continue
@@ -102,6 +107,37 @@ def lib():
         "MPI_Get_accumulate": (i, [p, i, i, p, i, i, i, i64, i, i, i, i]),
         "MPI_Fetch_and_op": (i, [p, p, i, i, i64, i, i]),
         "MPI_Compare_and_swap": (i, [p, p, p, i, i, i64, i]),
+        # derived datatypes + pack (msx_dtype_api.cpp); arrays / outputs as void*
+        "MPI_Type_contiguous": (i, [i, i, p]),
+        "MPI_Type_vector": (i, [i, i, i, i, p]),
+        "MPI_Type_create_hvector": (i, [i, i, i64, i, p]),
+        "MPI_Type_hvector": (i, [i, i, i64, i, p]),
+        "MPI_Type_indexed": (i, [i, p, p, i, p]),
+        "MPI_Type_create_hindexed": (i, [i, p, p, i, p]),
+        "MPI_Type_hindexed": (i, [i, p, p, i, p]),
+        "MPI_Type_create_indexed_block": (i, [i, i, p, i, p]),
+        "MPI_Type_create_hindexed_block": (i, [i, i, p, i, p]),
+        "MPI_Type_create_struct": (i, [i, p, p, p, p]),
+        "MPI_Type_struct": (i, [i, p, p, p, p]),
+        "MPI_Type_create_subarray": (i, [i, p, p, p, i, i, p]),
+        "MPI_Type_create_resized": (i, [i, i64, i64, p]),
+        "MPI_Type_dup": (i, [i, p]),
+        "MPI_Type_commit": (i, [p]),
+        "MPI_Type_free": (i, [p]),
+        "MPI_Type_size_x": (i, [i, p]),
+        "MPI_Type_get_extent": (i, [i, p, p]),
+        "MPI_Type_get_extent_x": (i, [i, p, p]),
+        "MPI_Type_get_true_extent": (i, [i, p, p]),
+        "MPI_Type_get_true_extent_x": (i, [i, p, p]),
+        "MPI_Type_extent": (i, [i, p]),
+        "MPI_Type_lb": (i, [i, p]),
+        "MPI_Type_ub": (i, [i, p]),
+        "MPI_Type_get_envelope": (i, [i, p, p, p, p]),
+        "MPI_Type_get_contents": (i, [i, i, i, i, p, p, p]),
+        "MPI_Get_address": (i, [p, p]),
+        "MPI_Pack": (i, [p, i, i, p, i, p, i]),
+        "MPI_Unpack": (i, [p, i, p, p, i, i, i]),
+        "MPI_Pack_size": (i, [i, i, i, p]),
         "msx_engine_transport": (ctypes.c_char_p, []),
         "msx_engine_stats": (i, [ctypes.POINTER(ctypes.c_double), i, i]),
         "MPI_Wait": (i, [ctypes.POINTER(i), p]),

@@ -1,0 +1,220 @@
+"""GPU parity of the derived-datatype engine (msx_pack.hip) against the oracle.
+
+MPI_Pack / MPI_Unpack move bytes with the gfx950 granule-map kernels; the
+oracle (oracle/msx_dtype_oracle.py) gathers / scatters the MPI type map element
+by element.  Byte movement is exact, so every check is bit-exact.  Covered:
+every constructor nested at random (seeded), negative displacements and
+strides, lb shifts, holes that unpack must preserve, host (pageable) and device
+buffers, odd base addresses (1-byte granules), and size-independent properties
+at large sizes (pack of a subarray == torch's slice; unpack(pack(x)) == x on
+the type map).
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import msx
+from oracle import msx_dtype_oracle as O
+from test_dtype_cpu import build_lib, build_oracle, free_all, random_recipe
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+C = msx.C
+c_int = ctypes.c_int
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lib = msx.init(errors_return=True)
+    assert lib.msx_device_count() > 0
+    return lib
+
+
+def _commit(L, r, keep):
+    h = build_lib(L, r, keep)
+    x = c_int(h)
+    assert L.MPI_Type_commit(ctypes.byref(x)) == 0
+    return h
+
+
+def _layout(t, count, misalign):
+    lo, hi = O.span(t, count)
+    base = -lo + misalign            # byte index of the buffer address inside the array
+    return base, hi - lo + misalign + 16
+
+
+def _overlaps(t, count):
+    """A receive type map with overlapping entries is erroneous in MPI (the
+    last write is unspecified); such types are checked on pack only."""
+    seen = set()
+    for i in range(count):
+        for d, sz in t.typemap:
+            for b in range(i * t.extent + d, i * t.extent + d + sz):
+                if b in seen:
+                    return True
+                seen.add(b)
+    return False
+
+
+def _recipes(n, seed0):
+    out = []
+    seed = seed0
+    while len(out) < n:
+        rng = random.Random(seed)
+        seed += 1
+        r = random_recipe(rng)
+        if r[0] == "basic":
+            r = ("vector", 3, 2, 3, r)
+        t = build_oracle(r)
+        if t.size == 0:
+            continue
+        out.append((r, rng.randint(1, 5), rng.choice([0, 0, 1, 3, 8])))
+    return out
+
+
+@pytest.mark.parametrize("case", _recipes(40, 1000))
+def test_pack_unpack_host_buffers(L, case):
+    r, count, mis = case
+    keep = []
+    h = _commit(L, r, keep)
+    t = build_oracle(r)
+    base, nbytes = _layout(t, count, mis)
+    rng = np.random.default_rng(len(keep) * 7919 + count)
+    typed = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    want = O.pack(t, count, typed, base)
+    out = np.zeros(want.size + 8, np.uint8)
+    pos = c_int(3)                    # pack at a non-zero position
+    rc = L.MPI_Pack(typed.ctypes.data + base, count, h, out.ctypes.data, out.size, ctypes.byref(pos),
+                    C.MPI_COMM_WORLD)
+    assert rc == 0, msx.last_error()
+    assert pos.value == 3 + want.size
+    assert np.array_equal(out[3:3 + want.size], want), r
+    if _overlaps(t, count):
+        free_all(L, keep)
+        return
+    # unpack random bytes into a buffer whose holes must survive
+    src = rng.integers(0, 256, want.size + 3, dtype=np.uint8)
+    dst = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    exp = dst.copy()
+    O.unpack(t, count, src[3:], exp, base)
+    pos = c_int(3)
+    rc = L.MPI_Unpack(src.ctypes.data, src.size, ctypes.byref(pos), dst.ctypes.data + base, count, h,
+                      C.MPI_COMM_WORLD)
+    assert rc == 0, msx.last_error()
+    assert pos.value == src.size
+    assert np.array_equal(dst, exp), r
+    free_all(L, keep)
+
+
+@pytest.mark.parametrize("case", _recipes(25, 5000))
+def test_pack_unpack_device_buffers(L, case):
+    r, count, mis = case
+    keep = []
+    h = _commit(L, r, keep)
+    t = build_oracle(r)
+    base, nbytes = _layout(t, count, mis)
+    g = torch.Generator(device="cuda").manual_seed(count * 31 + mis)
+    typed = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+    want = O.pack(t, count, typed.cpu().numpy(), base)
+    out = torch.zeros(want.size, dtype=torch.uint8, device="cuda")
+    pos = c_int(0)
+    rc = L.MPI_Pack(typed.data_ptr() + base, count, h, out.data_ptr(), out.numel(), ctypes.byref(pos),
+                    C.MPI_COMM_WORLD)
+    assert rc == 0, msx.last_error()
+    assert np.array_equal(out.cpu().numpy(), want), r
+    if _overlaps(t, count):
+        free_all(L, keep)
+        return
+    dst = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+    exp = dst.cpu().numpy().copy()
+    src = torch.randint(0, 256, (want.size,), dtype=torch.uint8, device="cuda", generator=g)
+    O.unpack(t, count, src.cpu().numpy(), exp, base)
+    pos = c_int(0)
+    rc = L.MPI_Unpack(src.data_ptr(), src.numel(), ctypes.byref(pos), dst.data_ptr() + base, count, h,
+                      C.MPI_COMM_WORLD)
+    assert rc == 0, msx.last_error()
+    assert np.array_equal(dst.cpu().numpy(), exp), r
+    free_all(L, keep)
+
+
+def test_pair_and_resized_types(L):
+    """Pair types keep their padding out of the packed stream; a resized type
+    with a negative lb packs from before the buffer address."""
+    keep = []
+    for r, count in [(("contig", 5, ("basic", C.MPI_DOUBLE_INT)), 7),
+                     (("contig", 3, ("basic", C.MPI_SHORT_INT)), 4),
+                     (("resized", -8, 24, ("basic", C.MPI_DOUBLE)), 9),
+                     (("hvector", 4, 1, -24, ("basic", C.MPI_FLOAT_INT)), 3)]:
+        h = _commit(L, r, keep)
+        t = build_oracle(r)
+        base, nbytes = _layout(t, count, 0)
+        typed = np.random.default_rng(count).integers(0, 256, nbytes, dtype=np.uint8)
+        want = O.pack(t, count, typed, base)
+        out = np.zeros(want.size, np.uint8)
+        pos = c_int(0)
+        assert L.MPI_Pack(typed.ctypes.data + base, count, h, out.ctypes.data, out.size, ctypes.byref(pos),
+                          C.MPI_COMM_WORLD) == 0, msx.last_error()
+        assert np.array_equal(out, want), r
+    free_all(L, keep)
+
+
+def test_large_subarray_equals_torch_slice(L):
+    """Size-independent property at 1 GiB: a 3-D C-order subarray of fp32
+    packs to exactly torch's contiguous copy of the same slice, and unpacking
+    it into a zeroed array restores the slice and nothing else."""
+    n0, n1, n2 = 256, 1024, 1024                       # 1 GiB fp32
+    s0, s1, s2 = 100, 700, 513                         # ragged inner rows (2052 B)
+    st = (77, 300, 255)
+    x = torch.randn(n0, n1, n2, device="cuda")
+    keep = []
+    h = _commit(L, ("subarray", [n0, n1, n2], [s0, s1, s2], list(st), True, ("basic", C.MPI_FLOAT)), keep)
+    want = x[st[0]:st[0] + s0, st[1]:st[1] + s1, st[2]:st[2] + s2].contiguous()
+    out = torch.empty_like(want)
+    pos = c_int(0)
+    nb = want.numel() * 4
+    assert L.MPI_Pack(x.data_ptr(), 1, h, out.data_ptr(), nb, ctypes.byref(pos), C.MPI_COMM_WORLD) == 0
+    torch.cuda.synchronize()
+    assert pos.value == nb
+    assert torch.equal(out.view(torch.int32), want.view(torch.int32))
+    y = torch.zeros_like(x)
+    pos = c_int(0)
+    assert L.MPI_Unpack(out.data_ptr(), nb, ctypes.byref(pos), y.data_ptr(), 1, h, C.MPI_COMM_WORLD) == 0
+    torch.cuda.synchronize()
+    mask = torch.zeros_like(x, dtype=torch.bool)
+    mask[st[0]:st[0] + s0, st[1]:st[1] + s1, st[2]:st[2] + s2] = True
+    assert torch.equal(y[mask], x[mask])
+    assert not y[~mask].any()
+    free_all(L, keep)
+
+
+def test_large_vector_round_trip_general_layout(L):
+    """An indexed type with irregular blocks (the binary-search path), 2^20
+    instances on device buffers: unpack(pack(x)) touches exactly the type map."""
+    keep = []
+    r = ("indexed", [3, 1, 7, 2], [0, 5, 9, 20], ("basic", C.MPI_INT))
+    h = _commit(L, r, keep)
+    t = build_oracle(r)
+    count = 1 << 20
+    ext = t.extent
+    x = torch.randint(-2**31, 2**31 - 1, (count * ext // 4,), dtype=torch.int32, device="cuda")
+    packed = torch.empty(count * t.size // 4, dtype=torch.int32, device="cuda")
+    pos = c_int(0)
+    assert L.MPI_Pack(x.data_ptr(), count, h, packed.data_ptr(), packed.numel() * 4, ctypes.byref(pos),
+                      C.MPI_COMM_WORLD) == 0
+    idx = torch.tensor([d // 4 for d, _ in t.typemap], device="cuda")
+    rows = (torch.arange(count, device="cuda") * (ext // 4)).unsqueeze(1) + idx.unsqueeze(0)
+    assert torch.equal(packed, x[rows.reshape(-1)])
+    y = torch.zeros_like(x)
+    pos = c_int(0)
+    assert L.MPI_Unpack(packed.data_ptr(), packed.numel() * 4, ctypes.byref(pos), y.data_ptr(), count, h,
+                        C.MPI_COMM_WORLD) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y[rows.reshape(-1)], x[rows.reshape(-1)])
+    y[rows.reshape(-1)] = 0
+    assert not y.any()
+    free_all(L, keep)
