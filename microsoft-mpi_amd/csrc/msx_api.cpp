@@ -23,6 +23,7 @@
 
 #include "../../include/msx.h"
 #include "msx_comm.h"
+#include "msx_dtype.h"
 #include "msx_transport.h"
 #include "msx_kernels.h"
 #include "msx_runtime.h"
@@ -761,11 +762,26 @@ int err_win(RmaWin* w, const char* fn, int code)
     return err_return_h(w->errhandler, fn, code);
 }
 
+// MpiaDatatypeValidate (mpi_api.h:113-164) as the one-sided calls use it:
+// predefined and committed derived datatypes.
+int v_dtype_rma(const void* buf, long long count, MPI_Datatype dt)
+{
+    if (count == 0) return MPI_SUCCESS;
+    if (count < 0) { set_error("negative count %lld", count); return MPI_ERR_COUNT; }
+    if (dt == MPI_DATATYPE_NULL) { set_error("null datatype"); return MPI_ERR_TYPE; }
+    if (!dtype_is_derived(dt)) return v_dtype(buf, count, dt);
+    Dtype* t = dtype_lookup(dt);
+    if (!t) { set_error("invalid datatype 0x%x", dt); return MPI_ERR_TYPE; }
+    if (!t->committed) { set_error("datatype 0x%x is not committed", dt); return MPI_ERR_TYPE; }
+    if (buf == nullptr && t->true_lb == 0 && t->size > 0) { set_error("null buffer"); return MPI_ERR_BUFFER; }
+    return MPI_SUCCESS;
+}
+
 // target datatype checks (MpiaDatatypeValidate with MPI_IN_PLACE as buffer),
 // the displacement and the rank, in the order of mpi_rma.cpp:697-735
 int v_target(RmaWin* w, int target_count, MPI_Datatype target_dt, int target_rank, MPI_Aint target_disp)
 {
-    int rc = v_dtype(MPI_IN_PLACE, target_count, target_dt);
+    int rc = v_dtype_rma(MPI_IN_PLACE, target_count, target_dt);
     if (rc != MPI_SUCCESS) return rc;
     if (target_disp < 0) { set_error("negative target displacement"); return MPI_ERR_DISP; }
     if (target_rank != MPI_PROC_NULL && (target_rank < 0 || target_rank >= w->comm->size)) {
@@ -775,32 +791,110 @@ int v_target(RmaWin* w, int target_count, MPI_Datatype target_dt, int target_ran
     return MPI_SUCCESS;
 }
 
-// Predefined datatypes only: the signatures of origin and target must be the
-// same basic type and count (derived datatypes are out of scope).
+// Origin and target must describe the same data: predefined pairs the same
+// type and count; with a derived type on either side the same number of bytes
+// of the same basic element type (the type signatures of MPI-2.2 §11.3).
 int v_match(int ocount, MPI_Datatype odt, int tcount, MPI_Datatype tdt)
 {
-    if (odt != tdt) { set_error("origin and target datatypes differ (0x%x, 0x%x)", odt, tdt); return MPI_ERR_TYPE; }
-    if (ocount != tcount) { set_error("origin and target counts differ (%d, %d)", ocount, tcount); return MPI_ERR_COUNT; }
+    if (!dtype_is_derived(odt) && !dtype_is_derived(tdt)) {
+        if (odt != tdt) { set_error("origin and target datatypes differ (0x%x, 0x%x)", odt, tdt); return MPI_ERR_TYPE; }
+        if (ocount != tcount) { set_error("origin and target counts differ (%d, %d)", ocount, tcount); return MPI_ERR_COUNT; }
+        return MPI_SUCCESS;
+    }
+    const Dtype* o = dtype_lookup(odt);
+    const Dtype* t = dtype_lookup(tdt);
+    if ((int64_t)ocount * o->size != (int64_t)tcount * t->size) {
+        set_error("origin and target describe %lld and %lld bytes", (long long)((int64_t)ocount * o->size),
+                  (long long)((int64_t)tcount * t->size));
+        return MPI_ERR_TYPE;
+    }
+    if (o->eltype != t->eltype && o->size > 0) {
+        set_error("origin and target element types differ (0x%x, 0x%x)", o->eltype, t->eltype);
+        return MPI_ERR_TYPE;
+    }
     return MPI_SUCCESS;
+}
+
+// Device temporary holding `count` instances of `dt` from `src`, packed.
+int pack_to_device(const void* src, int64_t count, MPI_Datatype dt, void** out)
+{
+    *out = nullptr;
+    const Dtype* t = dtype_lookup(dt);
+    const size_t bytes = (size_t)(count * t->size);
+    if (bytes == 0) return MPI_SUCCESS;
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    if (hipMalloc(out, bytes) != hipSuccess) { *out = nullptr; set_error("rma temporary"); return MPI_ERR_NO_MEM; }
+    rc = dt_pack_any(t, count, src, *out);
+    if (rc != MPI_SUCCESS) { (void)hipFree(*out); *out = nullptr; }
+    return rc;
 }
 
 // Queue a remote operation, or apply it now when the target is this rank
 // (win.cpp:1570-1590: MPIDI_Win_local_accumulate / MPIR_Localcopy).
-int rma_issue(RmaWin* w, RmaKind kind, int target, MPI_Aint disp, int count, MPI_Datatype dt, int opidx,
-              const void* origin, void* result, const void* compare)
+// Derived origin / result types are packed / unpacked on the origin's GPU; a
+// derived target type travels as its flattened layout.
+int rma_issue(RmaWin* w, RmaKind kind, int target, MPI_Aint disp, int opidx, const void* origin, int ocount,
+              MPI_Datatype odt, void* result, int rcount, MPI_Datatype rdt, int tcount, MPI_Datatype tdt,
+              const void* compare)
 {
     RmaDesc d;
     d.kind = kind;
     d.target = target;
     d.opidx = opidx;
-    d.dt = dt;
-    d.count = count;
     d.tdisp = (int64_t)disp * w->disp_units[(size_t)target];    // the TARGET's disp_unit
+    const bool self = target == w->comm->rank;
+    const Dtype* T = nullptr;
+    if (dtype_is_derived(tdt)) {
+        T = dtype_lookup(tdt);
+        d.dt = T->eltype;
+        d.count = tcount;
+        d.usize = T->size;
+        d.uext = T->extent;
+        dt_span(T, tcount, &d.span_lo, &d.span_hi);
+        if (T->size == 0) return MPI_SUCCESS;
+        if (!self) {
+            d.layout = (int32_t)w->blob.size();
+            dtype_serialize(T, w->blob);
+        }
+    } else {
+        d.dt = tdt;
+        d.count = tcount;
+        d.usize = d.uext = type_size(tdt);
+    }
     RmaLocal l;
     l.origin = origin;
     l.result = result;
     l.compare = compare;
-    if (target == w->comm->rank) return rma_apply_self(w, d, l);
+    int rc = MPI_SUCCESS;
+    const bool sends = kind == RMA_PUT || ((kind == RMA_ACC || kind == RMA_GACC) && opidx != O_NOOP);
+    const bool fetches = kind == RMA_GET || kind == RMA_GACC;
+    // the typed kernels read the payload and write fetched bytes in device memory
+    if (sends && (dtype_is_derived(odt) || (T && classify(origin).place != Place::Device))) {
+        rc = pack_to_device(origin, ocount, odt, &l.tmp_origin);
+        l.origin = l.tmp_origin;
+    }
+    if (rc == MPI_SUCCESS && fetches && (dtype_is_derived(rdt) || (T && classify(result).place != Place::Device))) {
+        const size_t bytes = (size_t)(rcount * dtype_lookup(rdt)->size);
+        if (bytes && hipMalloc(&l.tmp_result, bytes) != hipSuccess) {
+            l.tmp_result = nullptr;
+            set_error("rma temporary");
+            rc = MPI_ERR_NO_MEM;
+        }
+        l.result = l.tmp_result;
+        l.result_user = result;
+        l.result_dt = rdt;
+        l.result_count = rcount;
+    }
+    if (rc != MPI_SUCCESS) {
+        rma_local_complete(l);
+        return rc;
+    }
+    if (self) {
+        rc = rma_apply_self(w, d, l, T);
+        const int r2 = rma_local_complete(l);
+        return rc != MPI_SUCCESS ? rc : r2;
+    }
     w->q.push_back(d);
     w->ql.push_back(l);
     return MPI_SUCCESS;
@@ -913,13 +1007,13 @@ MSX_EXPORT int MPI_Put(const void* origin_addr, int origin_count, MPI_Datatype o
     RmaWin* w;
     int rc = v_win(win, &w);
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Put", rc);
-    rc = v_dtype(origin_addr, origin_count, origin_datatype);
+    rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
         rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
-        rc = rma_issue(w, RMA_PUT, target_rank, target_disp, origin_count, origin_datatype, O_REPLACE, origin_addr,
-                       nullptr, nullptr);
+        rc = rma_issue(w, RMA_PUT, target_rank, target_disp, O_REPLACE, origin_addr, origin_count, origin_datatype,
+                       nullptr, 0, MPI_DATATYPE_NULL, target_count, target_datatype, nullptr);
     return err_win(w, "MPI_Put", rc);
 }
 
@@ -930,13 +1024,13 @@ MSX_EXPORT int MPI_Get(void* origin_addr, int origin_count, MPI_Datatype origin_
     RmaWin* w;
     int rc = v_win(win, &w);
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Get", rc);
-    rc = v_dtype(origin_addr, origin_count, origin_datatype);
+    rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
         rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
-        rc = rma_issue(w, RMA_GET, target_rank, target_disp, origin_count, origin_datatype, O_NOOP, nullptr,
-                       origin_addr, nullptr);
+        rc = rma_issue(w, RMA_GET, target_rank, target_disp, O_NOOP, nullptr, 0, MPI_DATATYPE_NULL, origin_addr,
+                       origin_count, origin_datatype, target_count, target_datatype, nullptr);
     return err_win(w, "MPI_Get", rc);
 }
 
@@ -949,14 +1043,14 @@ MSX_EXPORT int MPI_Accumulate(const void* origin_addr, int origin_count, MPI_Dat
     int rc = v_win(win, &w);
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Accumulate", rc);
     OpRef r;
-    rc = v_dtype(origin_addr, origin_count, origin_datatype);
+    rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
     if (rc == MPI_SUCCESS) rc = rma_op(op, &r, false);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
         rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
-        rc = rma_issue(w, RMA_ACC, target_rank, target_disp, origin_count, origin_datatype, r.opidx, origin_addr,
-                       nullptr, nullptr);
+        rc = rma_issue(w, RMA_ACC, target_rank, target_disp, r.opidx, origin_addr, origin_count, origin_datatype,
+                       nullptr, 0, MPI_DATATYPE_NULL, target_count, target_datatype, nullptr);
     return err_win(w, "MPI_Accumulate", rc);
 }
 
@@ -972,8 +1066,8 @@ MSX_EXPORT int MPI_Get_accumulate(const void* origin_addr, int origin_count, MPI
     OpRef r;
     rc = v_op_handle(op, &r);
     const bool noop = rc == MPI_SUCCESS && r.opidx == O_NOOP;
-    if (rc == MPI_SUCCESS && !noop) rc = v_dtype(origin_addr, origin_count, origin_datatype);
-    if (rc == MPI_SUCCESS) rc = v_dtype(result_addr, result_count, result_datatype);
+    if (rc == MPI_SUCCESS && !noop) rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_rma(result_addr, result_count, result_datatype);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS) rc = rma_op(op, &r, true);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && result_count > 0) {
@@ -981,8 +1075,9 @@ MSX_EXPORT int MPI_Get_accumulate(const void* origin_addr, int origin_count, MPI
         if (rc == MPI_SUCCESS && !noop) rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
     }
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && target_count > 0)
-        rc = rma_issue(w, noop ? RMA_GET : RMA_GACC, target_rank, target_disp, target_count, target_datatype,
-                       r.opidx, origin_addr, result_addr, nullptr);
+        rc = rma_issue(w, noop ? RMA_GET : RMA_GACC, target_rank, target_disp, r.opidx, origin_addr, origin_count,
+                       origin_datatype, result_addr, result_count, result_datatype, target_count, target_datatype,
+                       nullptr);
     return err_win(w, "MPI_Get_accumulate", rc);
 }
 
@@ -1001,8 +1096,8 @@ MSX_EXPORT int MPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_
     if (rc == MPI_SUCCESS) rc = v_target(w, 1, datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS) rc = rma_op(op, &r, true);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL)
-        rc = rma_issue(w, noop ? RMA_GET : RMA_GACC, target_rank, target_disp, 1, datatype, r.opidx, origin_addr,
-                       result_addr, nullptr);
+        rc = rma_issue(w, noop ? RMA_GET : RMA_GACC, target_rank, target_disp, r.opidx, origin_addr, 1, datatype,
+                       result_addr, 1, datatype, 1, datatype, nullptr);
     return err_win(w, "MPI_Fetch_and_op", rc);
 }
 
@@ -1018,8 +1113,8 @@ MSX_EXPORT int MPI_Compare_and_swap(const void* origin_addr, const void* compare
     if (rc == MPI_SUCCESS) rc = v_dtype(result_addr, 1, datatype);
     if (rc == MPI_SUCCESS) rc = v_target(w, 1, datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL)
-        rc = rma_issue(w, RMA_CAS, target_rank, target_disp, 1, datatype, O_REPLACE, origin_addr, result_addr,
-                       compare_addr);
+        rc = rma_issue(w, RMA_CAS, target_rank, target_disp, O_REPLACE, origin_addr, 1, datatype, result_addr, 1,
+                       datatype, 1, datatype, compare_addr);
     return err_win(w, "MPI_Compare_and_swap", rc);
 }
 

@@ -744,6 +744,46 @@ void* stage_buffer(size_t bytes)
 
 }  // namespace
 
+void dtype_serialize(const Dtype* t, std::vector<int64_t>& out)
+{
+    out.push_back(t->size);
+    out.push_back(t->extent);
+    out.push_back((int64_t)t->eltype);
+    out.push_back((int64_t)t->runs.size());
+    for (const DtRun& r : t->runs) {
+        out.push_back(r.disp);
+        out.push_back(r.len);
+    }
+}
+
+Dtype* dtype_from_blob(const int64_t* b, int64_t avail)
+{
+    if (avail < 4 || b[3] < 0 || b[3] > kMaxRuns || avail < 4 + 2 * b[3]) return nullptr;
+    auto* t = new Dtype();
+    t->size = b[0];
+    t->extent = b[1];
+    t->eltype = (MPI_Datatype)b[2];
+    const TypeInfo* ti = type_info(t->eltype);
+    t->el_size = ti ? ti->size : -1;
+    t->committed = true;
+    t->runs.resize((size_t)b[3]);
+    int64_t sum = 0;
+    for (int64_t k = 0; k < b[3]; ++k) {
+        t->runs[(size_t)k] = {b[4 + 2 * k], b[5 + 2 * k]};
+        sum += b[5 + 2 * k];
+    }
+    if (sum != t->size) {
+        delete t;
+        return nullptr;
+    }
+    return t;
+}
+
+void dtype_delete(Dtype* t)
+{
+    if (t) destroy(t);
+}
+
 void dt_span(const Dtype* t, int64_t count, int64_t* lo, int64_t* hi)
 {
     if (t->runs.empty() || count <= 0) { *lo = *hi = 0; return; }

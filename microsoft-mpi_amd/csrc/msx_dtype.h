@@ -113,6 +113,12 @@ int dt_unpack_any(const Dtype* t, int64_t count, const void* packed, void* typed
 int dt_copy_any(const void* src, int64_t scount, MPI_Datatype sdt, void* dst, int64_t rcount,
                 MPI_Datatype rdt);
 
+// Serialized layout of a type (size, extent, eltype, nruns, runs...) and the
+// standalone (handle-less) type rebuilt from it at a one-sided target.
+void dtype_serialize(const Dtype* t, std::vector<int64_t>& out);
+Dtype* dtype_from_blob(const int64_t* blob, int64_t avail);   // nullptr when malformed
+void dtype_delete(Dtype* t);                                   // standalone types only
+
 // Byte span touched by `count` instances: [lo, hi) relative to the buffer.
 void dt_span(const Dtype* t, int64_t count, int64_t* lo, int64_t* hi);
 

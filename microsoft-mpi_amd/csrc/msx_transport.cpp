@@ -42,6 +42,7 @@
 
 #include <rccl/rccl.h>
 
+#include "msx_dtype.h"
 #include "msx_kernels.h"
 #include "msx_runtime.h"
 
@@ -1645,7 +1646,7 @@ namespace {
 int rma_combine(const RmaDesc& d, const char* payload, char* taddr, hipStream_t s)
 {
     if (d.opidx == O_NOOP || d.count == 0) return MPI_SUCCESS;
-    const size_t bytes = (size_t)d.count * (size_t)type_size(d.dt);
+    const size_t bytes = (size_t)d.count * (size_t)d.usize;
     if (d.opidx == O_REPLACE) return copy_async(taddr, payload, bytes, s);
     if (op_check_dtype(d.opidx, d.dt) != MPI_SUCCESS) return MPI_SUCCESS;
     const Kind k = type_info(d.dt)->kind;
@@ -1658,7 +1659,7 @@ int rma_combine(const RmaDesc& d, const char* payload, char* taddr, hipStream_t 
 // compare-and-swap of one element (bitwise compare, win.cpp:1909-1990)
 int rma_cas(const RmaDesc& d, const char* origin, const char* cmp, char* taddr, char* fetch, hipStream_t s)
 {
-    const size_t esz = (size_t)type_size(d.dt);
+    const size_t esz = (size_t)d.usize;
     int rc = sync_stream(s, "rma cas");
     char old[16], c[16];
     if (rc == MPI_SUCCESS) rc = copy_any(old, taddr, esz);
@@ -1668,11 +1669,50 @@ int rma_cas(const RmaDesc& d, const char* origin, const char* cmp, char* taddr, 
     return rc;
 }
 
-// One operation on window memory `taddr` of this rank.  `fetch` receives the
-// target's previous contents (GET / GACC / CAS).
-int rma_apply(const RmaDesc& d, const char* payload, const char* cmp, char* taddr, char* fetch, hipStream_t s)
+// A derived target datatype: the gfx950 pack / unpack / accumulate kernels
+// walk its layout at taddr (the reference's segment walk of
+// packethandling.cpp:2969-3004).  Window memory the GPU cannot address
+// (pageable host memory) is staged through HBM around the kernel.
+int rma_apply_typed(const RmaDesc& d, const Dtype* T, const char* payload, char* taddr, char* fetch,
+                    hipStream_t s)
 {
-    const size_t bytes = (size_t)d.count * (size_t)type_size(d.dt);
+    int64_t lo, hi;
+    dt_span(T, d.count, &lo, &hi);
+    const BufInfo bi = classify(taddr + lo);
+    char* tdev = taddr;
+    void* stage = nullptr;
+    int rc = MPI_SUCCESS;
+    if (bi.place == Place::Device) {
+        tdev = static_cast<char*>(bi.dev) - lo;
+    } else {
+        const size_t span = (size_t)(hi - lo);
+        const uintptr_t mis = (uintptr_t)(taddr + lo) & 15;
+        if (hipMalloc(&stage, span + 16) != hipSuccess) { set_error("rma staging allocation"); return MPI_ERR_NO_MEM; }
+        tdev = static_cast<char*>(stage) + mis - lo;
+        rc = copy_async(tdev + lo, taddr + lo, span, s);
+    }
+    // payload / fetch live in engine windows or device temporaries (device memory)
+    if (rc == MPI_SUCCESS && (d.kind == RMA_GET || d.kind == RMA_GACC))
+        rc = dt_pack_dev(T, d.count, tdev, fetch, s);
+    if (rc == MPI_SUCCESS && (d.kind == RMA_PUT || ((d.kind == RMA_ACC || d.kind == RMA_GACC))))
+        rc = d.kind == RMA_PUT ? dt_unpack_dev(T, d.count, payload, tdev, s)
+                               : dt_acc_dev(d.opidx, T, d.count, payload, tdev, s);
+    if (stage) {
+        if (rc == MPI_SUCCESS && d.kind != RMA_GET) rc = copy_async(taddr + lo, tdev + lo, (size_t)(hi - lo), s);
+        const int rs = sync_stream(s, "rma typed stage");
+        (void)hipFree(stage);
+        if (rc == MPI_SUCCESS) rc = rs;
+    }
+    return rc;
+}
+
+// One operation on window memory `taddr` of this rank.  `fetch` receives the
+// target's previous contents (GET / GACC / CAS).  T: derived target type or null.
+int rma_apply(const RmaDesc& d, const Dtype* T, const char* payload, const char* cmp, char* taddr, char* fetch,
+              hipStream_t s)
+{
+    if (T) return rma_apply_typed(d, T, payload, taddr, fetch, s);
+    const size_t bytes = (size_t)d.count * (size_t)d.usize;
     switch (d.kind) {
     case RMA_PUT: return copy_async(taddr, payload, bytes, s);
     case RMA_GET: return copy_async(fetch, taddr, bytes, s);
@@ -1688,11 +1728,11 @@ int rma_apply(const RmaDesc& d, const char* payload, const char* cmp, char* tadd
 
 bool rma_in_bounds(const RmaDesc& d, int64_t winsize)
 {
-    const int64_t esz = type_size(d.dt);
+    if (d.tdisp < 0 || d.count < 0 || d.usize <= 0) return false;
+    if (d.layout >= 0) return d.tdisp + d.span_lo >= 0 && d.span_hi <= winsize - d.tdisp;
     const int64_t n = (d.kind == RMA_CAS) ? 1 : d.count;
-    if (d.tdisp < 0 || n < 0 || esz <= 0) return false;
-    if (n > (INT64_MAX - d.tdisp) / esz) return false;
-    return d.tdisp + n * esz <= winsize;
+    if (n > (INT64_MAX - d.tdisp) / d.usize) return false;
+    return d.tdisp + n * d.usize <= winsize;
 }
 
 hipStream_t rma_self_stream()
@@ -1710,9 +1750,17 @@ hipStream_t rma_self_stream()
 struct RmaPiece {
     int origin;
     int64_t idx;           // index in the origin's queue
-    int64_t lo, hi;        // element range
+    int64_t lo, hi;        // unit range
     size_t in_off, out_off;
     size_t in_b, out_b;
+};
+
+struct TypeCache {         // standalone target layouts rebuilt at this rank
+    std::map<std::pair<int, int64_t>, Dtype*> m;
+    ~TypeCache()
+    {
+        for (auto& kv : m) dtype_delete(kv.second);
+    }
 };
 
 int do_rma_fence(RmaWin* win)
@@ -1722,17 +1770,37 @@ int do_rma_fence(RmaWin* win)
     const int p = c->size, me = c->rank;
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
-    // 1. every origin's queue, on every rank (same order everywhere)
-    int64_t mine = (int64_t)win->q.size();
-    std::vector<int64_t> ns((size_t)p);
-    if ((rc = tp->allgather(&mine, sizeof(mine), ns.data())) != MPI_SUCCESS) return rc;
-    int64_t maxn = 0;
-    for (int64_t v : ns) maxn = std::max(maxn, v);
-    trace("rma fence: %lld local ops, max %lld", (long long)mine, (long long)maxn);
+    // 1. every origin's queue and derived-layout blob, on every rank
+    int64_t mine[2] = {(int64_t)win->q.size(), (int64_t)win->blob.size()};
+    std::vector<int64_t> ns((size_t)p * 2);
+    if ((rc = tp->allgather(mine, sizeof(mine), ns.data())) != MPI_SUCCESS) return rc;
+    int64_t maxn = 0, maxb = 0;
+    for (int r = 0; r < p; ++r) {
+        maxn = std::max(maxn, ns[(size_t)r * 2]);
+        maxb = std::max(maxb, ns[(size_t)r * 2 + 1]);
+    }
+    trace("rma fence: %lld local ops, max %lld", (long long)mine[0], (long long)maxn);
     if (maxn == 0) return tp->barrier();
     std::vector<RmaDesc> padded((size_t)maxn), all((size_t)p * (size_t)maxn);
     std::copy(win->q.begin(), win->q.end(), padded.begin());
     if ((rc = tp->allgather(padded.data(), (size_t)maxn * sizeof(RmaDesc), all.data())) != MPI_SUCCESS) return rc;
+    std::vector<int64_t> blobs;
+    if (maxb > 0) {
+        std::vector<int64_t> pb((size_t)maxb, 0);
+        std::copy(win->blob.begin(), win->blob.end(), pb.begin());
+        blobs.resize((size_t)p * (size_t)maxb);
+        if ((rc = tp->allgather(pb.data(), (size_t)maxb * sizeof(int64_t), blobs.data())) != MPI_SUCCESS) return rc;
+    }
+    TypeCache types;
+    auto target_type = [&](int o, int64_t i, const RmaDesc& d) -> const Dtype* {
+        if (d.layout < 0) return nullptr;
+        auto key = std::make_pair(o, i);
+        auto it = types.m.find(key);
+        if (it != types.m.end()) return it->second;
+        Dtype* t = dtype_from_blob(blobs.data() + (size_t)o * maxb + d.layout, ns[(size_t)o * 2 + 1] - d.layout);
+        types.m[key] = t;
+        return t;
+    };
     Windows w;
     if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
     const size_t C = w.C;
@@ -1742,8 +1810,9 @@ int do_rma_fence(RmaWin* win)
     std::vector<size_t> in_used((size_t)p, 0), out_used((size_t)p, 0);
     int my_err = MPI_SUCCESS;
     for (int o = 0; o < p; ++o) {
-        for (int64_t i = 0; i < ns[o]; ++i) {
+        for (int64_t i = 0; i < ns[(size_t)o * 2]; ++i) {
             const RmaDesc& d = all[(size_t)o * maxn + i];
+            const size_t esz = (size_t)d.usize;
             if (!rma_in_bounds(d, win->sizes[(size_t)d.target])) {
                 // packethandling.cpp:1339-1383: **requestrmaoutofbounds
                 if (o == me) {
@@ -1753,14 +1822,19 @@ int do_rma_fence(RmaWin* win)
                 }
                 continue;
             }
-            const size_t esz = (size_t)type_size(d.dt);
+            if (esz > C / 2) {
+                if (o == me) {
+                    my_err = MPI_ERR_TYPE;
+                    set_error("RMA target datatype of %zu bytes exceeds the staging window", esz);
+                }
+                continue;
+            }
             const int64_t n = (d.kind == RMA_CAS) ? 1 : d.count;
             const bool sends = d.kind == RMA_PUT || d.kind == RMA_CAS || ((d.kind == RMA_ACC || d.kind == RMA_GACC) && d.opidx != O_NOOP);
             const bool fetches = d.kind == RMA_GET || d.kind == RMA_GACC || d.kind == RMA_CAS;
             int64_t per = (int64_t)(C / esz / 2) & ~(int64_t)15;
             if (per <= 0) per = 1;
-            for (int64_t lo = 0; lo < n || (n == 0 && lo == 0); lo += per) {
-                if (n == 0) break;
+            for (int64_t lo = 0; lo < n; lo += per) {
                 const int64_t hi = std::min(n, lo + per);
                 RmaPiece pc;
                 pc.origin = o;
@@ -1790,7 +1864,7 @@ int do_rma_fence(RmaWin* win)
             if (pc.origin != me || !pc.in_b) continue;
             const RmaDesc& d = all[(size_t)me * maxn + pc.idx];
             const RmaLocal& l = win->ql[(size_t)pc.idx];
-            const size_t esz = (size_t)type_size(d.dt);
+            const size_t esz = (size_t)d.usize;
             char* dst = w.in(d.target) + pc.in_off;
             if (d.kind == RMA_CAS) {
                 rc = copy_async(dst, l.origin, esz, s);
@@ -1807,13 +1881,14 @@ int do_rma_fence(RmaWin* win)
         for (const RmaPiece& pc : round) {
             const RmaDesc& d0 = all[(size_t)pc.origin * maxn + pc.idx];
             if (d0.target != me) continue;
-            const size_t esz = (size_t)type_size(d0.dt);
+            const Dtype* T = target_type(pc.origin, pc.idx, d0);
+            if (d0.layout >= 0 && !T) { set_error("rma: malformed datatype layout"); return MPI_ERR_INTERN; }
             RmaDesc d = d0;
             d.count = (d0.kind == RMA_CAS) ? 1 : pc.hi - pc.lo;
-            char* taddr = win->base + d0.tdisp + pc.lo * (int64_t)esz;
+            char* taddr = win->base + d0.tdisp + pc.lo * d0.uext;
             const char* payload = w.in(me) + pc.in_off;
             char* fetch = pc.out_b ? w.out(pc.origin) + pc.out_off : nullptr;
-            rc = rma_apply(d, payload, payload + esz, taddr, fetch, s);
+            rc = rma_apply(d, T, payload, payload + d0.usize, taddr, fetch, s);
             if (rc != MPI_SUCCESS) return rc;
         }
         if ((rc = sync_stream(s, "rma apply")) != MPI_SUCCESS) return rc;
@@ -1822,22 +1897,43 @@ int do_rma_fence(RmaWin* win)
         for (const RmaPiece& pc : round) {
             if (pc.origin != me || !pc.out_b) continue;
             const RmaDesc& d = all[(size_t)me * maxn + pc.idx];
-            const size_t esz = (size_t)type_size(d.dt);
-            rc = copy_async(static_cast<char*>(win->ql[(size_t)pc.idx].result) + pc.lo * esz,
+            rc = copy_async(static_cast<char*>(win->ql[(size_t)pc.idx].result) + pc.lo * d.usize,
                             w.out(me) + pc.out_off, pc.out_b, s);
             if (rc != MPI_SUCCESS) return rc;
         }
         if ((rc = sync_stream(s, "rma deliver")) != MPI_SUCCESS) return rc;
     }
+    for (RmaLocal& l : win->ql) {
+        const int r2 = rma_local_complete(l);
+        if (rc == MPI_SUCCESS) rc = r2;
+    }
     win->q.clear();
     win->ql.clear();
+    win->blob.clear();
     trace("rma fence: %zu rounds done", rounds.size());
-    return my_err;
+    return rc != MPI_SUCCESS ? rc : my_err;
 }
 
 }  // namespace
 
-int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l)
+int rma_local_complete(RmaLocal& l)
+{
+    int rc = MPI_SUCCESS;
+    if (l.tmp_result) {
+        // a derived result type: the fetched bytes arrived packed
+        Dtype* t = dtype_lookup(l.result_dt);
+        rc = t ? dt_unpack_any(t, l.result_count, l.tmp_result, l.result_user) : MPI_ERR_TYPE;
+        (void)hipFree(l.tmp_result);
+        l.tmp_result = nullptr;
+    }
+    if (l.tmp_origin) {
+        (void)hipFree(l.tmp_origin);
+        l.tmp_origin = nullptr;
+    }
+    return rc;
+}
+
+int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l, const Dtype* T)
 {
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
@@ -1846,7 +1942,7 @@ int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l)
         return MPI_ERR_REQUEST;
     }
     hipStream_t s = rma_self_stream();
-    rc = rma_apply(d, static_cast<const char*>(l.origin), static_cast<const char*>(l.compare),
+    rc = rma_apply(d, T, static_cast<const char*>(l.origin), static_cast<const char*>(l.compare),
                    w->base + d.tdisp, static_cast<char*>(l.result), s);
     return rc == MPI_SUCCESS ? sync_stream(s, "rma self") : rc;
 }

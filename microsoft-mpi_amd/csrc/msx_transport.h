@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "msx_comm.h"
+#include "msx_dtype.h"
 
 namespace msx {
 
@@ -102,14 +103,27 @@ struct RmaDesc {                 // exchanged at synchronisation (plain data)
     int32_t kind = -1;
     int32_t target = -1;
     int32_t opidx = 0;           // builtin op index (O_REPLACE / O_NOOP allowed)
-    int32_t dt = 0;              // MPI_Datatype
-    int64_t count = 0;           // elements
+    int32_t dt = 0;              // target MPI_Datatype (its element type when derived)
+    int64_t count = 0;           // units: elements, or target-type instances when derived
     int64_t tdisp = 0;           // byte offset in the target's window
+    // Derived target datatype (layout >= 0): the target rebuilds it from the
+    // origin's serialized runs at int64 offset `layout` of the origin's blob
+    // (the reference ships the dataloop the same way, packethandling.cpp).
+    int32_t layout = -1;
+    int32_t pad_ = 0;
+    int64_t usize = 0;           // packed bytes per unit (payload / fetch stride)
+    int64_t uext = 0;            // target bytes per unit (extent)
+    int64_t span_lo = 0, span_hi = 0;   // target bytes touched, relative to tdisp
 };
 struct RmaLocal {                // origin-side addresses of a queued operation
-    const void* origin = nullptr;
-    void* result = nullptr;
+    const void* origin = nullptr;   // packed payload (the user's buffer, or tmp_origin)
+    void* result = nullptr;         // packed destination of fetched bytes (user's, or tmp_result)
     const void* compare = nullptr;
+    void* tmp_origin = nullptr;     // device copy of a derived origin, packed at issue
+    void* tmp_result = nullptr;     // device staging of a derived result, unpacked at completion
+    void* result_user = nullptr;
+    MPI_Datatype result_dt = 0;
+    int64_t result_count = 0;
 };
 struct RmaWin {
     int handle = 0;
@@ -122,10 +136,13 @@ struct RmaWin {
     MPI_Errhandler errhandler = MPI_ERRHANDLER_NULL;   // unset: MPI_COMM_WORLD's handler
     std::vector<RmaDesc> q;      // queued remote operations, issue order
     std::vector<RmaLocal> ql;
+    std::vector<int64_t> blob;   // serialized derived target layouts of the queued operations
 };
+// Finish an operation's origin side: unpack a derived result, free temporaries.
+int rma_local_complete(RmaLocal& l);
 // Apply one operation on this rank's own window memory now (target == self,
 // as the reference does, win.cpp:1570-1590); blocking.
-int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l);
+int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l, const Dtype* T);
 // MPI_Win_fence: every queued operation of every origin is applied at its
 // target in (origin rank, issue) order; fetched values are delivered.  Collective.
 int engine_rma_fence(RmaWin* w);

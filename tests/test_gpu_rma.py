@@ -178,3 +178,161 @@ def test_rma_fence_epochs_on_one_gpu(p, chunk):
         line = [l for l in o.splitlines() if l.startswith("RESULT")]
         assert line, (o + e)[-3000:]
         assert line[0].split()[3] == "0", line[0]
+
+
+# ---- derived datatypes in one-sided operations --------------------------------
+# Origin types are packed on the origin's GPU, target types travel as their
+# flattened layout and are walked by the gfx950 unpack / accumulate / pack
+# kernels at the target (the reference ships the dataloop and walks it in
+# do_accumulate_op, packethandling.cpp:2969-3004).  Expected values: the
+# oracle's type maps (oracle/msx_dtype_oracle.py) applied with numpy.
+WORKER_DT = r'''
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd")); sys.path.insert(0, REPO)
+import numpy as np, torch
+import msx
+from oracle import msx_dtype_oracle as O
+C = msx.C
+L = msx.init(errors_return=True)
+r_, s_ = ctypes.c_int(), ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r_)); L.MPI_Comm_size(C.MPI_COMM_WORLD, ctypes.byref(s_))
+rank, p = r_.value, s_.value
+fails = []
+def chk(tag, got, exp):
+    if np.asarray(got).tobytes() != np.asarray(exp).tobytes():
+        fails.append(tag)
+def ok(rc, tag):
+    if rc != 0:
+        fails.append(f"{tag} rc={rc} {msx.last_error()}")
+    return rc == 0
+def new(fn, *a):
+    t = ctypes.c_int()
+    assert fn(*a, ctypes.byref(t)) == 0, msx.last_error()
+    assert L.MPI_Type_commit(ctypes.byref(t)) == 0
+    return t.value
+ia = lambda v, ct=ctypes.c_int: (ct * len(v))(*v)
+D, I = C.MPI_DOUBLE, C.MPI_INT
+N = 64
+# a column of an N x N row-major fp64 matrix, resized so consecutive columns follow
+col0 = new(L.MPI_Type_vector, N, 1, N, D)
+col = new(L.MPI_Type_create_resized, col0, 0, 8)
+ocol = O.resized(O.vector(N, 1, N, O.predefined(D)), 0, 8)
+# a 4 x 8 block at (10, 20) of the matrix
+blk = new(L.MPI_Type_create_subarray, 2, ia([N, N]), ia([4, 8]), ia([10, 20]), C.MPI_ORDER_C, D)
+oblk = O.subarray([N, N], [4, 8], [10, 20], True, O.predefined(D))
+# origin side: every other element of a 64-vector
+ev = new(L.MPI_Type_vector, 32, 1, 2, D)
+oev = O.vector(32, 1, 2, O.predefined(D))
+# irregular int blocks for BXOR
+ix = new(L.MPI_Type_indexed, 3, ia([5, 1, 9]), ia([0, 11, 30]), I)
+oix = O.indexed([5, 1, 9], [0, 11, 30], O.predefined(I))
+idx = lambda t, esz, count=1, base=0: np.array([base + i * t.extent // esz + d // esz
+                                              for i in range(count) for d, _ in t.typemap])
+
+init_m = lambda r: (np.arange(N * N) % 1000 + 10000 * r).astype(np.float64)
+wm_t = torch.from_numpy(init_m(rank)).cuda()
+init_x = lambda r: ((np.arange(256) * 2654435761 + r) % (1 << 31)).astype(np.int32)
+wx_t = torch.from_numpy(init_x(rank)).cuda()
+wh = np.arange(512, dtype=np.float64) - 100.0 * rank        # host (pageable) window
+torch.cuda.synchronize()
+wm, wx, whw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+assert L.MPI_Win_create(wm_t.data_ptr(), N * N * 8, 8, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(wm)) == 0
+assert L.MPI_Win_create(wx_t.data_ptr(), 256 * 4, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(wx)) == 0
+assert L.MPI_Win_create(wh.ctypes.data, wh.nbytes, 8, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(whw)) == 0
+for w in (wm, wx, whw):
+    L.MPI_Win_set_errhandler(w, C.MPI_ERRORS_RETURN)
+    ok(L.MPI_Win_fence(0, w), "open fence")
+
+colv = lambda r: (np.arange(N) * (r + 1) + 0.5).astype(np.float64)
+c_dev = torch.from_numpy(colv(rank)).cuda()
+put64 = lambda r: (np.arange(64) * 3.0 + 1000 * r).astype(np.float64)
+p_host = put64(rank)                                    # host origin, derived origin type
+xo = lambda r: ((np.arange(15) + 1) * (0x01010101 * (r + 3))).astype(np.int32)
+x_dev = torch.from_numpy(xo(rank)).cuda()
+g_res = torch.zeros(64, dtype=torch.float64, device="cuda")
+ga = lambda r: (np.arange(N) % 7 * 1.0 + r).astype(np.float64)
+ga_host = ga(rank)
+ga_res = np.zeros(N, np.float64)
+torch.cuda.synchronize()
+nxt, last = (rank + 1) % p, p - 1
+# column `rank` of rank 0's matrix += my column (derived target, predefined origin)
+ok(L.MPI_Accumulate(c_dev.data_ptr(), N, D, 0, rank, 1, col, C.MPI_SUM, wm), "acc col")
+# the next rank's 4x8 block <- every other element of my 64-vector (derived both sides)
+ok(L.MPI_Put(p_host.ctypes.data, 1, ev, nxt, 0, 1, blk, wm), "put blk")
+# BXOR through an irregular int layout at the last rank, displaced by 40 ints
+ok(L.MPI_Accumulate(x_dev.data_ptr(), 15, I, last, 40, 1, ix, C.MPI_BXOR, wx), "acc bxor")
+# host window at rank 0: MAX through a column layout (stride 8 doubles, 64 rows)
+ok(L.MPI_Get_accumulate(ga_host.ctypes.data, N, D, ga_res.ctypes.data, N, D, 0, 0, 1,
+                        new(L.MPI_Type_vector, N, 1, 8, D), C.MPI_MAX, whw), "gacc host")
+for w in (wm, wx, whw):
+    ok(L.MPI_Win_fence(0, w), "fence")
+# Get with a derived origin (result) type from the block written above
+ok(L.MPI_Get(g_res.data_ptr(), 1, ev, nxt, 0, 1, blk, wm), "get blk")
+ok(L.MPI_Win_fence(0, wm), "fence2")
+
+order = lambda t: [t] + [o for o in range(p) if o != t]
+wm_h = wm_t.cpu().numpy()
+if rank == 0:
+    e = init_m(0).copy()
+    for o in range(p):
+        e[idx(ocol, 8, base=o)] += colv(o)
+    prev = (0 - 1) % p
+    e[idx(oblk, 8)] = put64(prev)[idx(oev, 8)]
+    chk("acc col + put blk @0", wm_h, e)
+else:
+    e = init_m(rank).copy()
+    e[idx(oblk, 8)] = put64(rank - 1)[idx(oev, 8)]
+    chk("put blk", wm_h, e)
+exp_g = np.zeros(64)
+exp_g[idx(oev, 8)] = put64(rank)[idx(oev, 8)]
+chk("get derived result", g_res.cpu().numpy(), exp_g)
+if rank == last:
+    e = init_x(last).copy()
+    for o in order(last):
+        e[40 + idx(oix, 4)] ^= xo(o)
+    chk("bxor indexed", wx_t.cpu().numpy(), e)
+cur = (np.arange(512, dtype=np.float64))[::8][:N].copy()
+for o in order(0):
+    if o == rank:
+        chk("gacc fetched", ga_res, cur)
+    cur = np.maximum(cur, ga(o))
+if rank == 0:
+    e = np.arange(512, dtype=np.float64)
+    e[0:8 * N:8] = cur
+    chk("gacc host window", wh, e)
+for w in (wm, wx, whw):
+    ok(L.MPI_Win_free(ctypes.byref(w)), "free")
+print("RESULT", rank, p, len(fails), fails[:6], flush=True)
+L.MPI_Finalize()
+'''
+
+
+@pytest.mark.parametrize("p,chunk", [(1, None), (2, None), (3, 4096)])
+def test_rma_derived_datatypes_on_one_gpu(p, chunk):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = _free_port()
+    procs = []
+    for r in range(p):
+        env = dict(os.environ)
+        env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
+                    "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
+                    "MSX_BOOTSTRAP_TIMEOUT": "180"})
+        if chunk:
+            env["MSX_CHUNK_BYTES"] = str(chunk)     # pieces of a derived op land in different rounds
+        procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER_DT)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    results = []
+    for pr in procs:
+        try:
+            o, e = pr.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            pr.kill()
+            o, e = pr.communicate()
+        results.append((pr.returncode, o, e))
+    for rc, o, e in results:
+        assert rc == 0, (o + e)[-3000:]
+        line = [l for l in o.splitlines() if l.startswith("RESULT")]
+        assert line, (o + e)[-3000:]
+        assert line[0].split()[3] == "0", line[0]
