@@ -51,6 +51,7 @@ def parse():
                     help="skip the N>1 collective configs (c3-c5, bench_collectives.py)")
     ap.add_argument("--coll-scale", type=float, default=1.0, help="size factor for c3-c5")
     ap.add_argument("--no-per-op", action="store_true", help="skip the per-(op, type) roofline table")
+    ap.add_argument("--no-pack", action="store_true", help="skip the datatype pack/unpack table")
     return ap.parse_args()
 
 
@@ -220,9 +221,11 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
     out = {}
     for opn, dtn in PER_OP:
         op, dt = getattr(C, opn), getattr(C, dtn)
-        sz = ctypes.c_int(0)
-        L.MPI_Type_size(dt, ctypes.byref(sz))
+        # element stride (pair types: the padded struct, e.g. 16 B for
+        # MPI_DOUBLE_INT), not MPI_Type_size's data bytes (12 B)
+        sz = ctypes.c_int(L.msx_type_size(dt))
         n = nbytes // sz.value
+        assert sz.value > 0 and n * sz.value <= nbytes
         with torch.cuda.stream(stream):
             a.random_(0, 256)
             b.random_(0, 256)
@@ -285,6 +288,71 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
                 out[f"tree8_sweep/{name}/cap{cap}"] = entry(time_tree())
         L.msx_tune_tree(0, 0)
     del a, b
+    return out
+
+
+def pack_roofline(L, C, torch, dev, stream):
+    """MPI_Pack / MPI_Unpack kernels (msx_pack.hip) through msx_pack_dev /
+    msx_unpack_dev on device buffers: algorithmic HBM bytes = 2 x packed size
+    per call (each packed byte read once and written once), timed with HIP
+    events on the launch stream (median of 3 rounds of 10 calls).  Layouts:
+    a 16-B-block vector (regular map, 16-B granules), MPI_DOUBLE_INT records
+    (12 of every 16 B, 4-B granules) and a 3-D fp32 subarray (irregular run
+    list, binary-search map).  Every layout is checked against torch first."""
+    import ctypes
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    out = {}
+
+    def mk(fn, *a):
+        t = ctypes.c_int()
+        assert fn(*a, ctypes.byref(t)) == 0, msx_err()
+        assert L.MPI_Type_commit(ctypes.byref(t)) == 0
+        return t
+
+    def msx_err():
+        import msx
+        return msx.last_error()
+
+    ia = lambda v: (ctypes.c_int * len(v))(*v)
+    nf = 1 << 26                                           # 256 MiB of fp32 typed data
+    typed = torch.randn(nf, device=dev)
+    layouts = []
+    t = mk(L.MPI_Type_vector, nf // 8, 4, 8, C.MPI_FLOAT)
+    layouts.append(("vector_16B_blocks_stride32B", t, 1, typed.view(-1, 8)[:, :4].contiguous()))
+    n_di = nf // 4                                          # 16 B records
+    layouts.append(("double_int_records_12of16B", ctypes.c_int(C.MPI_DOUBLE_INT), n_di,
+                    typed.view(-1, 4)[:, :3].contiguous()))
+    dims, sub, st = (256, 512, 512), (192, 400, 384), (32, 56, 64)
+    t3 = mk(L.MPI_Type_create_subarray, 3, ia(dims), ia(sub), ia(st), C.MPI_ORDER_C, C.MPI_FLOAT)
+    v3 = typed.view(*dims)[st[0]:st[0] + sub[0], st[1]:st[1] + sub[1], st[2]:st[2] + sub[2]].contiguous()
+    layouts.append(("subarray3d_fp32_rows1536B", t3, 1, v3))
+    for name, t, count, want in layouts:
+        packed = torch.empty(want.numel() * want.element_size(), dtype=torch.uint8, device=dev)
+        nb = packed.numel()
+        rc = L.msx_pack_dev(typed.data_ptr(), count, t.value, packed.data_ptr(), sp)
+        torch.cuda.synchronize()
+        if rc or not torch.equal(packed, want.view(-1).view(torch.uint8)):
+            raise RuntimeError(f"pack parity failed for {name}: rc={rc}")
+        res = {"packed_bytes": nb}
+        for label, fn, a, b in (("pack", L.msx_pack_dev, typed, packed), ("unpack", L.msx_unpack_dev, packed, typed)):
+            ts = []
+            for _ in range(3):
+                fn(a.data_ptr(), count, t.value, b.data_ptr(), sp)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(10):
+                    fn(a.data_ptr(), count, t.value, b.data_ptr(), sp)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / 10)
+            ms = sorted(ts)[1]
+            gbs = 2 * nb / ms / 1e6
+            res[label] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        out[name] = res
+        del packed
+    for t in (layouts[0][1], t3):
+        L.MPI_Type_free(ctypes.byref(t))
+    del typed
     return out
 
 
@@ -435,6 +503,9 @@ def main():
     per_op = None
     if rank == 0 and world == 1 and not args.no_per_op:
         per_op = per_op_roofline(L, C, torch, dev, stream, n * 4, tree_sweep=args.sweep)
+    pack = None
+    if rank == 0 and world == 1 and not args.no_pack:
+        pack = pack_roofline(L, C, torch, dev, stream)
 
     if rank == 0:
         total_bytes = world * args.steps * n * BYTES_PER_ELEM
@@ -478,6 +549,8 @@ def main():
             out["rccl_native_allreduce_f32"] = rccl_native
         if per_op is not None:
             out["per_op_roofline_hbm"] = per_op
+        if pack is not None:
+            out["datatype_pack_roofline_hbm"] = pack
         if sweep:
             out["variant_sweep_GB_s"] = sweep
         if world == 1:

@@ -15,6 +15,10 @@
  *                            64-bit count, stream-ordered, device pointers.
  *   msx_op_check          <- MPIR_Op_check_dtype_table[op%16-1](dt)
  *                            (op.cpp:653-672, api/mpi_api.h:765)
+ *   msx_pack_dev /        <- MPID_Segment_pack / MPID_Segment_unpack over a
+ *   msx_unpack_dev           committed datatype (src/mpi/msmpi/mpid/segment.cpp,
+ *                            called by MPI_Pack/MPI_Unpack, api/mpi_pack.cpp:41-660);
+ *                            64-bit count, stream-ordered, device pointers.
  *   msx_reduce_tree_dev   <- the per-step MPID_Uop_call chain of the
  *                            recursive-halving/doubling schedules
  *                            (src/mpi/msmpi/mpid/reduce.cpp:3899-3989,
@@ -57,6 +61,14 @@ int msx_type_size(MPI_Datatype datatype);
  * stream-ordered (returns after the launch, not after completion). */
 int msx_reduce_local_dev(const void* in, void* inout, int64_t count,
                          MPI_Datatype datatype, MPI_Op op, void* stream);
+
+/* packed[i*size + b] <- typed[i*extent + map(b)] for `count` instances of a
+ * committed datatype (predefined or derived); typed is the buffer address the
+ * type map is relative to.  Device pointers, stream-ordered. */
+int msx_pack_dev(const void* typed, int64_t count, MPI_Datatype datatype, void* packed,
+                 void* stream);
+int msx_unpack_dev(const void* packed, int64_t count, MPI_Datatype datatype, void* typed,
+                   void* stream);
 
 /* out[i] = tree(srcs[0][i], ..., srcs[p-1][i]) with the balanced binary tree
  * ((s0 op s1) op (s2 op s3)) op ((s4 op s5) op (s6 op s7)), the left operand

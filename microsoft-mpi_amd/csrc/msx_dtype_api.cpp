@@ -570,6 +570,37 @@ MSX_EXPORT int MPI_Pack_size(int incount, MPI_Datatype datatype, MPI_Comm comm, 
     return MPI_SUCCESS;
 }
 
+// ===========================================================================
+// device-side extension ABI (include/msx.h)
+// ===========================================================================
+static int dev_typed_check(int64_t count, MPI_Datatype dt, Dtype** t)
+{
+    if (count < 0) { set_error("negative count"); return MPI_ERR_COUNT; }
+    int rc = v_handle(dt, t);
+    if (rc == MPI_SUCCESS && dtype_is_derived(dt) && !(*t)->committed) {
+        set_error("datatype 0x%x is not committed", dt);
+        rc = MPI_ERR_TYPE;
+    }
+    if (rc == MPI_SUCCESS) rc = ensure_device();
+    return rc;
+}
+
+MSX_EXPORT int msx_pack_dev(const void* typed, int64_t count, MPI_Datatype datatype, void* packed, void* stream)
+{
+    Dtype* t;
+    int rc = dev_typed_check(count, datatype, &t);
+    if (rc != MPI_SUCCESS || count == 0) return rc;
+    return dt_pack_dev(t, count, typed, packed, static_cast<hipStream_t>(stream));
+}
+
+MSX_EXPORT int msx_unpack_dev(const void* packed, int64_t count, MPI_Datatype datatype, void* typed, void* stream)
+{
+    Dtype* t;
+    int rc = dev_typed_check(count, datatype, &t);
+    if (rc != MPI_SUCCESS || count == 0) return rc;
+    return dt_unpack_dev(t, count, packed, typed, static_cast<hipStream_t>(stream));
+}
+
 // ---- PMPI_ profiling aliases --------------------------------------------------
 #define MSX_ALIAS(name) extern "C" __attribute__((visibility("default"), alias(#name)))
 MSX_ALIAS(MPI_Type_contiguous) int PMPI_Type_contiguous(int, MPI_Datatype, MPI_Datatype*);

@@ -118,6 +118,31 @@ __global__ __launch_bounds__(kPackBlock) void k_dt_pack(CopyArgs a)
     }
 }
 
+// Run-parallel form for layouts whose runs are long (subarray rows, big
+// indexed blocks): one wavefront per (instance, run) unit, its 64 lanes
+// stream the run's granules with coalesced accesses on both sides.  No
+// per-granule search: the run's offsets are read once per wave.
+template <int G, bool UNPACK>
+__global__ __launch_bounds__(kPackBlock) void k_dt_runs(CopyArgs a)
+{
+    typedef typename GranT<G>::T T;
+    constexpr int kWaves = kPackBlock / 64;
+    const int lane = threadIdx.x & 63;
+    const int64_t nunits = (a.ngran / a.gsize) * a.nruns;        // instances x runs
+    const int64_t nw = (int64_t)gridDim.x * kWaves;
+    for (int64_t u = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); u < nunits; u += nw) {
+        const int64_t i = u / a.nruns, k = u - i * a.nruns;
+        const int64_t po = a.poff[k];
+        const int64_t len = (a.poff[k + 1] - po) / G;
+        T* t = reinterpret_cast<T*>(a.typed + i * a.extent + a.disp[k]);
+        T* p = reinterpret_cast<T*>(a.packed + i * a.size + po);
+        for (int64_t j = lane; j < len; j += 64) {
+            if constexpr (UNPACK) t[j] = __builtin_nontemporal_load(p + j);
+            else __builtin_nontemporal_store(t[j], p + j);
+        }
+    }
+}
+
 // typed element (op)= packed element.  E = element bytes; granules are whole
 // elements.  ALIGNED: every element address is a multiple of alignof(T);
 // otherwise the element moves through byte copies.
@@ -173,11 +198,23 @@ CopyArgs make_args(const DevLayout& L, int64_t count, void* typed, void* packed,
     return a;
 }
 
+// Average run length (in granules) from which a wave per run beats the
+// per-granule binary search.
+constexpr int64_t kRunParallelMin = 8;
+
 template <int G, bool UNPACK>
 hipError_t run_copy(const CopyArgs& a, bool reg, hipStream_t s)
 {
     const bool narrow = a.ngran < (int64_t)0xffffffffll;
-    const dim3 grid(grid_for(a.ngran)), block(kPackBlock);
+    const dim3 block(kPackBlock);
+    if (!reg && a.gsize >= kRunParallelMin * a.nruns) {
+        const int64_t units = (a.ngran / a.gsize) * a.nruns;
+        const int64_t want = (units + kPackBlock / 64 - 1) / (kPackBlock / 64);
+        const dim3 grid((unsigned)(want < 8192 ? want : 8192));
+        hipLaunchKernelGGL((k_dt_runs<G, UNPACK>), grid, block, 0, s, a);
+        return hipGetLastError();
+    }
+    const dim3 grid(grid_for(a.ngran));
     if (reg && narrow) hipLaunchKernelGGL((k_dt_pack<G, true, true, UNPACK>), grid, block, 0, s, a);
     else if (reg) hipLaunchKernelGGL((k_dt_pack<G, true, false, UNPACK>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_dt_pack<G, false, false, UNPACK>), grid, block, 0, s, a);

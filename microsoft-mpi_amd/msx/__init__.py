@@ -149,6 +149,8 @@ def lib():
         "msx_op_check": (i, [i, i]),
         "msx_type_size": (i, [i]),
         "msx_reduce_local_dev": (i, [p, p, i64, i, i, p]),
+        "msx_pack_dev": (i, [p, i64, i, p, p]),
+        "msx_unpack_dev": (i, [p, i64, i, p, p]),
         "msx_reduce_tree_dev": (i, [ctypes.POINTER(p), i, p, i64, i, i, p]),
         "msx_tune_set": (i, [i, i]),
         "msx_tune_tree": (i, [i, i]),

@@ -337,3 +337,17 @@ def test_pack_without_gpu_fails_loudly(msxlib):
     rc = L.MPI_Pack(src.ctypes.data, 1, t, out.ctypes.data, 32, ctypes.byref(pos), C.MPI_COMM_WORLD)
     assert rc == C.MPI_ERR_OTHER and pos.value == 0 and not out.any()
     assert L.MPI_Type_free(ctypes.byref(t)) == 0
+
+
+def test_pair_type_size_is_data_bytes(msxlib):
+    """MPI_Type_size counts data bytes (SetTypeCharacteristics,
+    datatype.cpp:1282-1293): 12 for MPI_DOUBLE_INT, whose extent (element
+    stride, msx_type_size) is 16; 6 / 8 for MPI_SHORT_INT."""
+    L = msxlib
+    for dt, size, ext in ((C.MPI_DOUBLE_INT, 12, 16), (C.MPI_SHORT_INT, 6, 8), (C.MPI_FLOAT_INT, 8, 8),
+                          (C.MPI_2INT, 8, 8), (C.MPI_DOUBLE, 8, 8)):
+        sz, lb, ex = c_int(), c_i64(), c_i64()
+        assert L.MPI_Type_size(dt, ctypes.byref(sz)) == 0 and sz.value == size
+        assert L.MPI_Type_get_extent(dt, ctypes.byref(lb), ctypes.byref(ex)) == 0
+        assert (lb.value, ex.value) == (0, ext)
+        assert L.msx_type_size(dt) == ext
