@@ -143,31 +143,6 @@ def main(out_path, scale):
         res["c4_reduce_scatter_max_f64"] = {
             "bytes_per_rank": S, "seconds": round(t, 5), "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 2),
             "correct": bool(torch.equal(recv, exp))}
-        L.msx_engine_stats(stats, 7, 1)
-        calls = max(stats[6], 1.0)
-        if stats[6] > 0:    # window plane only (the RCCL plane has no host phases)
-            res["c3_allreduce_sum_f32"]["phase_ms_per_call"] = {
-                k: round(stats[i] / calls * 1e3, 3) for i, k in
-                enumerate(("stage_scatter", "collect_wait_barrier_a", "reduce_push", "barrier_b",
-                           "final_collect"))}
-            res["c3_allreduce_sum_f32"]["chunks_per_call"] = stats[5] / calls
-    # allreduce latency / bandwidth curve (fp32 SUM, exact integer data)
-    curve = {}
-    for nbytes in (4 << 10, 256 << 10, 4 << 20, 64 << 20):
-        m = nbytes // 4
-        a = send[:m].clone() if send.numel() >= m else torch.ones(m, device=dev)
-        b = torch.empty_like(a)
-        L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
-        ts = []
-        for _ in range(5):
-            barrier()
-            t0 = time.perf_counter()
-            L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
-            ts.append(time.perf_counter() - t0)
-        t = sorted(ts)[2]
-        curve[str(nbytes)] = {"us": round(t * 1e6, 1), "busbw_GB_s": round(nbytes / t / 1e9 * 2 * (p - 1) / p, 2),
-                              "correct": bool(torch.equal(b, exp[:m]))}
-    res["allreduce_curve_f32"] = curve
     del send, recv, exp
     torch.cuda.empty_cache()
 

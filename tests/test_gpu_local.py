@@ -322,6 +322,7 @@ def test_maximum_count_int_max_fp32(L):
     a = torch.rand(n, device="cuda", generator=g)
     b = torch.rand(n, device="cuda", generator=g) - 0.5
     exp = a + b
+    torch.cuda.synchronize()          # MPI calls take device buffers whose producers have finished
     assert L.MPI_Reduce_local(a.data_ptr(), b.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM) == 0
     torch.cuda.synchronize()
     assert torch.equal(b.view(torch.int32), exp.view(torch.int32))
