@@ -152,6 +152,27 @@ def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 1, 256, true
     return best
 
 
+def pmc_raw(kernel_substr):
+    """Uncorrected per-launch FETCH_SIZE / WRITE_SIZE (KiB) of a kernel from the
+    newest committed PMC collection.  Only 16-B-per-lane streaming reads have a
+    known gfx950 correction (FETCH_SIZE x 2, MI355X_MICROARCH.md §HBM); other
+    widths are reported raw, for ratios between layouts."""
+    import csv
+    dirs = sorted({os.path.dirname(p) for p in
+                   glob.glob(os.path.join(REPO, "profiles", "*", "pmc_*counter_collection.csv"))})
+    out = None
+    for d in dirs:
+        vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+        for path in glob.glob(os.path.join(d, "pmc_*counter_collection.csv")):
+            with open(path, newline="") as f:
+                for row in csv.DictReader(f):
+                    if kernel_substr in row["Kernel_Name"] and row["Counter_Name"] in vals:
+                        vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+        if vals["FETCH_SIZE"] and vals["WRITE_SIZE"]:
+            out = {k: round(sum(v) / len(v), 1) for k, v in vals.items()}
+    return out
+
+
 def cpu_baseline(seconds, elems):
     import numpy as np
     import oracle
@@ -291,6 +312,16 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
     return out
 
 
+# rocprofv3 kernel symbol of each pack-table entry (for the PMC traffic lookup)
+KERNEL_OF = {
+    "vector_16B_blocks_stride32B": {"pack": "k_dt_pack<16, true, true, false>",
+                                    "unpack": "k_dt_pack<16, true, true, true>"},
+    "double_int_records_12of16B": {"pack": "k_dt_pack<4, true, true, false>",
+                                   "unpack": "k_dt_pack<4, true, true, true>"},
+    "subarray3d_fp32_rows1536B": {"pack": "k_dt_runs<16, false>", "unpack": "k_dt_runs<16, true>"},
+}
+
+
 def pack_roofline(L, C, torch, dev, stream):
     """MPI_Pack / MPI_Unpack kernels (msx_pack.hip) through msx_pack_dev /
     msx_unpack_dev on device buffers: algorithmic HBM bytes = 2 x packed size
@@ -333,7 +364,7 @@ def pack_roofline(L, C, torch, dev, stream):
         torch.cuda.synchronize()
         if rc or not torch.equal(packed, want.view(-1).view(torch.uint8)):
             raise RuntimeError(f"pack parity failed for {name}: rc={rc}")
-        res = {"packed_bytes": nb}
+        res = {"packed_bytes": nb, "algorithmic_bytes_per_call": 2 * nb}
         for label, fn, a, b in (("pack", L.msx_pack_dev, typed, packed), ("unpack", L.msx_unpack_dev, packed, typed)):
             ts = []
             for _ in range(3):
@@ -347,7 +378,9 @@ def pack_roofline(L, C, torch, dev, stream):
                 ts.append(e0.elapsed_time(e1) / 10)
             ms = sorted(ts)[1]
             gbs = 2 * nb / ms / 1e6
-            res[label] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+            res[label] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                          "kernel": KERNEL_OF[name][label]}
+            res[label]["pmc_raw_kib"] = pmc_raw(KERNEL_OF[name][label])
         out[name] = res
         del packed
     for t in (layouts[0][1], t3):

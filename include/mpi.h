@@ -310,6 +310,11 @@ MPI_METHOD MPI_Compare_and_swap(const void* origin_addr, const void* compare_add
 #define MPI_ORDER_C         56
 #define MPI_ORDER_FORTRAN   57
 
+#define MPI_DISTRIBUTE_BLOCK        121     /* mpi.h:1513-1516 */
+#define MPI_DISTRIBUTE_CYCLIC       122
+#define MPI_DISTRIBUTE_NONE         123
+#define MPI_DISTRIBUTE_DFLT_DARG    (-49767)
+
 enum {                                  /* mpi.h:1758-1778 */
     MPI_COMBINER_NAMED            = 1,
     MPI_COMBINER_DUP              = 2,
@@ -363,6 +368,10 @@ MPI_METHOD MPI_Type_struct(int count, const int array_of_blocklengths[],
 MPI_METHOD MPI_Type_create_subarray(int ndims, const int array_of_sizes[],
                                     const int array_of_subsizes[], const int array_of_starts[],
                                     int order, MPI_Datatype oldtype, MPI_Datatype* newtype);
+MPI_METHOD MPI_Type_create_darray(int size, int rank, int ndims, const int array_of_gsizes[],
+                                  const int array_of_distribs[], const int array_of_dargs[],
+                                  const int array_of_psizes[], int order, MPI_Datatype oldtype,
+                                  MPI_Datatype* newtype);
 MPI_METHOD MPI_Type_create_resized(MPI_Datatype oldtype, MPI_Aint lb, MPI_Aint extent,
                                    MPI_Datatype* newtype);
 MPI_METHOD MPI_Type_dup(MPI_Datatype oldtype, MPI_Datatype* newtype);

@@ -137,6 +137,21 @@ int v_dtype(const void* buf, long long count, MPI_Datatype dt)
     return MPI_SUCCESS;
 }
 
+// MpiaDatatypeValidate (mpi_api.h:113-164) with derived datatypes: the
+// one-sided calls and MPI_Reduce_local (user ops) accept committed derived types.
+int v_dtype_any(const void* buf, long long count, MPI_Datatype dt)
+{
+    if (count == 0) return MPI_SUCCESS;
+    if (count < 0) { set_error("negative count %lld", count); return MPI_ERR_COUNT; }
+    if (dt == MPI_DATATYPE_NULL) { set_error("null datatype"); return MPI_ERR_TYPE; }
+    if (!dtype_is_derived(dt)) return v_dtype(buf, count, dt);
+    Dtype* t = dtype_lookup(dt);
+    if (!t) { set_error("invalid datatype 0x%x", dt); return MPI_ERR_TYPE; }
+    if (!t->committed) { set_error("datatype 0x%x is not committed", dt); return MPI_ERR_TYPE; }
+    if (buf == nullptr && t->true_lb == 0 && t->size > 0) { set_error("null buffer"); return MPI_ERR_BUFFER; }
+    return MPI_SUCCESS;
+}
+
 // MpiaDatatypeValidateBuffer (mpi_api.h:190-212)
 int v_buffer(MPI_Datatype dt, const void* buf, long long count)
 {
@@ -403,7 +418,7 @@ MSX_EXPORT int MPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
     int rc = v_op(op, datatype, &r);                // :324
     if (rc == MPI_SUCCESS && inbuf == MPI_IN_PLACE) { set_error("inbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
     if (rc == MPI_SUCCESS && inoutbuf == MPI_IN_PLACE) { set_error("inoutbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
-    if (rc == MPI_SUCCESS) rc = v_dtype(inbuf, count, datatype);   // :343
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(inbuf, count, datatype);   // :343
     if (rc == MPI_SUCCESS && inbuf == inoutbuf) { set_error("inbuf aliases inoutbuf"); rc = MPI_ERR_BUFFER; }
     if (rc == MPI_SUCCESS) rc = local_combine(r, datatype, inbuf, inoutbuf, (size_t)count);
     return err_return(nullptr, "MPI_Reduce_local", rc);
@@ -762,26 +777,11 @@ int err_win(RmaWin* w, const char* fn, int code)
     return err_return_h(w->errhandler, fn, code);
 }
 
-// MpiaDatatypeValidate (mpi_api.h:113-164) as the one-sided calls use it:
-// predefined and committed derived datatypes.
-int v_dtype_rma(const void* buf, long long count, MPI_Datatype dt)
-{
-    if (count == 0) return MPI_SUCCESS;
-    if (count < 0) { set_error("negative count %lld", count); return MPI_ERR_COUNT; }
-    if (dt == MPI_DATATYPE_NULL) { set_error("null datatype"); return MPI_ERR_TYPE; }
-    if (!dtype_is_derived(dt)) return v_dtype(buf, count, dt);
-    Dtype* t = dtype_lookup(dt);
-    if (!t) { set_error("invalid datatype 0x%x", dt); return MPI_ERR_TYPE; }
-    if (!t->committed) { set_error("datatype 0x%x is not committed", dt); return MPI_ERR_TYPE; }
-    if (buf == nullptr && t->true_lb == 0 && t->size > 0) { set_error("null buffer"); return MPI_ERR_BUFFER; }
-    return MPI_SUCCESS;
-}
-
 // target datatype checks (MpiaDatatypeValidate with MPI_IN_PLACE as buffer),
 // the displacement and the rank, in the order of mpi_rma.cpp:697-735
 int v_target(RmaWin* w, int target_count, MPI_Datatype target_dt, int target_rank, MPI_Aint target_disp)
 {
-    int rc = v_dtype_rma(MPI_IN_PLACE, target_count, target_dt);
+    int rc = v_dtype_any(MPI_IN_PLACE, target_count, target_dt);
     if (rc != MPI_SUCCESS) return rc;
     if (target_disp < 0) { set_error("negative target displacement"); return MPI_ERR_DISP; }
     if (target_rank != MPI_PROC_NULL && (target_rank < 0 || target_rank >= w->comm->size)) {
@@ -1007,7 +1007,7 @@ MSX_EXPORT int MPI_Put(const void* origin_addr, int origin_count, MPI_Datatype o
     RmaWin* w;
     int rc = v_win(win, &w);
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Put", rc);
-    rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
+    rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
         rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
@@ -1024,7 +1024,7 @@ MSX_EXPORT int MPI_Get(void* origin_addr, int origin_count, MPI_Datatype origin_
     RmaWin* w;
     int rc = v_win(win, &w);
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Get", rc);
-    rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
+    rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
         rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
@@ -1043,7 +1043,7 @@ MSX_EXPORT int MPI_Accumulate(const void* origin_addr, int origin_count, MPI_Dat
     int rc = v_win(win, &w);
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Accumulate", rc);
     OpRef r;
-    rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
+    rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
     if (rc == MPI_SUCCESS) rc = rma_op(op, &r, false);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
@@ -1066,8 +1066,8 @@ MSX_EXPORT int MPI_Get_accumulate(const void* origin_addr, int origin_count, MPI
     OpRef r;
     rc = v_op_handle(op, &r);
     const bool noop = rc == MPI_SUCCESS && r.opidx == O_NOOP;
-    if (rc == MPI_SUCCESS && !noop) rc = v_dtype_rma(origin_addr, origin_count, origin_datatype);
-    if (rc == MPI_SUCCESS) rc = v_dtype_rma(result_addr, result_count, result_datatype);
+    if (rc == MPI_SUCCESS && !noop) rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(result_addr, result_count, result_datatype);
     if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
     if (rc == MPI_SUCCESS) rc = rma_op(op, &r, true);
     if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && result_count > 0) {

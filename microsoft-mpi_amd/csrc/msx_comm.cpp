@@ -5,8 +5,10 @@
 //   MPID_Uop_call / MPIR_Op_c_proxy (include/op.h:171-174, mpid/op.cpp:542-545)
 //   NBC requests progressed in MPI_Test/Wait (mpid/request.cpp:780-886)
 #include "msx_comm.h"
+#include "msx_dtype.h"
 
 #include <atomic>
+#include <deque>
 #include <chrono>
 #include <functional>
 #include <future>
@@ -106,6 +108,41 @@ int copy_any(void* dst, const void* src, size_t bytes)
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy");
 }
 
+// A derived datatype reaches only user functions (the builtin ops' check
+// tables reject it): MPID_Uop_call(op, in, inout, &count, &dt) on the typed
+// buffers (api/mpi_reduce.cpp:361).  Device operands are staged through host
+// memory over the whole byte span the type map touches, so the bytes between
+// the mapped elements of `inout` are written back unchanged.
+int local_combine_typed(const OpRef& op, MPI_Datatype dt, const void* in, void* inout, size_t count)
+{
+    const Dtype* t = dtype_lookup(dt);
+    if (!t) { set_error("invalid datatype 0x%x", dt); return MPI_ERR_TYPE; }
+    if (count > 0x7fffffff) { set_error("count exceeds the MPI_User_function range"); return MPI_ERR_COUNT; }
+    int64_t lo, hi;
+    dt_span(t, (int64_t)count, &lo, &hi);
+    const size_t span = (size_t)(hi - lo);
+    const char* pin = static_cast<const char*>(in);
+    char* pio = static_cast<char*>(inout);
+    const BufInfo bi = classify(pin + lo), bo = classify(pio + lo);
+    std::vector<char> hin, hio;
+    int rc = MPI_SUCCESS;
+    if (span && bi.place == Place::Device) {
+        hin.resize(span);
+        if ((rc = copy_any(hin.data(), pin + lo, span)) != MPI_SUCCESS) return rc;
+        pin = hin.data() - lo;
+    }
+    if (span && bo.place == Place::Device) {
+        hio.resize(span);
+        if ((rc = copy_any(hio.data(), pio + lo, span)) != MPI_SUCCESS) return rc;
+        pio = hio.data() - lo;
+    }
+    int len = (int)count;
+    MPI_Datatype d = dt;
+    op.user_fn(const_cast<char*>(pin), pio, &len, &d);
+    if (span && bo.place == Place::Device) rc = copy_any(static_cast<char*>(inout) + lo, hio.data(), span);
+    return rc;
+}
+
 int local_combine(const OpRef& op, MPI_Datatype dt, const void* in, void* inout, size_t count)
 {
     if (count == 0) return MPI_SUCCESS;
@@ -117,6 +154,7 @@ int local_combine(const OpRef& op, MPI_Datatype dt, const void* in, void* inout,
     // User-defined op: MPI_User_function is host code (mpi.h:2258-2265), called
     // through the C proxy with int-sized chunks.  Device operands are staged
     // to host memory around the call.
+    if (dtype_is_derived(dt)) return local_combine_typed(op, dt, in, inout, count);
     const int esz = type_size(dt);
     if (esz <= 0) { set_error("datatype 0x%x not supported with user ops", dt); return MPI_ERR_TYPE; }
     const size_t bytes = count * (size_t)esz;
@@ -211,7 +249,7 @@ struct Request {
 
 namespace {
 std::mutex g_req_mu;
-std::vector<Request> g_reqs;
+std::deque<Request> g_reqs;     // deque: a Request* stays valid while other threads add slots
 constexpr int kReqBase = (int)0xAC000000;
 
 int req_alloc(MPI_Request* out, Request** r)

@@ -159,9 +159,43 @@ void destroy(Dtype* t)
     delete t;
 }
 
-// Append `nrep` copies of old's runs, copy r at disp0 + r*ext.
-int append_copies(std::vector<DtRun>& out, const Dtype* old, int64_t disp0, int64_t nrep, int64_t ext)
+// Expand a compact run list into `runs`.
+int materialise(Dtype* t)
 {
+    if (t->rn == 0) return MPI_SUCCESS;
+    if (t->rn > kMaxRuns) {
+        set_error("datatype type map exceeds %lld contiguous pieces", (long long)kMaxRuns);
+        return MPI_ERR_NO_MEM;
+    }
+    t->runs.clear();
+    t->runs.reserve((size_t)t->rn);
+    for (int64_t k = 0; k < t->rn; ++k) push_run(t->runs, t->rfirst + k * t->rstride, t->rlen);
+    t->rn = 0;
+    return MPI_SUCCESS;
+}
+
+// The single run of a one-run type (either form).
+bool single_run(const Dtype* t, DtRun* r)
+{
+    if (t->rn == 1) { *r = {t->rfirst, t->rlen}; return true; }
+    if (t->rn == 0 && t->runs.size() == 1) { *r = t->runs[0]; return true; }
+    return false;
+}
+
+void copy_layout(Dtype* t, const Dtype* o)
+{
+    t->runs = o->runs;
+    t->rn = o->rn;
+    t->rfirst = o->rfirst;
+    t->rlen = o->rlen;
+    t->rstride = o->rstride;
+}
+
+// Append `nrep` copies of old's runs, copy r at disp0 + r*ext.
+int append_copies(std::vector<DtRun>& out, Dtype* old, int64_t disp0, int64_t nrep, int64_t ext)
+{
+    int rc = materialise(old);
+    if (rc != MPI_SUCCESS) return rc;
     if (nrep <= 0 || old->runs.empty()) return MPI_SUCCESS;
     // one contiguous run spanning exactly the extent: the copies merge into one
     if (old->runs.size() == 1 && old->runs[0].len == ext && ext > 0) {
@@ -262,6 +296,8 @@ int64_t dtype_size(MPI_Datatype h)
     return t ? t->size : -1;
 }
 
+int64_t dtype_nruns(const Dtype* t) { return t->rn ? t->rn : (int64_t)t->runs.size(); }
+
 void dtype_add_ref(MPI_Datatype h)
 {
     std::lock_guard<std::recursive_mutex> g(g_mu);
@@ -297,9 +333,23 @@ int dtype_vector(int count, int blocklen, int64_t stride, bool stride_bytes, MPI
         t->true_ub = t->ub + (a.true_ub - a.ub);
         t->extent = t->ub - t->lb;
         t->is_contig = (t->size == t->extent && eff == (int64_t)blocklen * a.size && a.contig);
-        for (int j = 0; j < count; ++j) {
-            int rc = append_copies(t->runs, o, (int64_t)j * eff, blocklen, a.extent);
-            if (rc != MPI_SUCCESS) return rc;
+        // a one-run old type whose `blocklen` copies merge into one run gives a
+        // regular run list: keep it compact (merged into one run if contiguous)
+        DtRun r1;
+        const bool one = blocklen > 0 && single_run(o, &r1) && (blocklen == 1 || r1.len == a.extent);
+        const int64_t blen = one ? (blocklen == 1 ? r1.len : (int64_t)blocklen * a.extent) : 0;
+        if (one && blen > 0 && eff == blen) {
+            push_run(t->runs, r1.disp, (int64_t)count * blen);
+        } else if (one && blen > 0 && count > 1) {
+            t->rn = count;
+            t->rfirst = r1.disp;
+            t->rlen = blen;
+            t->rstride = eff;
+        } else {
+            for (int j = 0; j < count; ++j) {
+                int rc = append_copies(t->runs, o, (int64_t)j * eff, blocklen, a.extent);
+                if (rc != MPI_SUCCESS) return rc;
+            }
         }
     }
     if (combiner == 3)          // MPI_COMBINER_CONTIGUOUS
@@ -426,7 +476,7 @@ int dtype_struct(int count, const int* blens, const MPI_Aint* disps, const MPI_D
         for (i = 0; i < count; ++i) {
             if (blens[i] == 0) continue;
             const bool bi = is_builtin_h(types[i]);
-            const Dtype* o = olds[i];
+            Dtype* o = olds[i];
             const bool marker = (types[i] == MPI_LB || types[i] == MPI_UB);
             int64_t l, u, tl, tu, esz;
             MPI_Datatype et;
@@ -534,7 +584,7 @@ int dtype_resized(MPI_Datatype oldh, int64_t lb, int64_t extent, MPI_Datatype* o
     t->el_size = bi ? o->size : o->el_size;
     t->eltype = bi ? oldh : o->eltype;
     t->is_contig = bi ? (extent == o->size) : (extent == o->size ? o->is_contig : false);
-    t->runs = o->runs;
+    copy_layout(t.get(), o);
     set_contents(t.get(), 18, {}, {lb, extent}, {oldh});
     *out = register_type(std::move(t));
     return MPI_SUCCESS;
@@ -552,7 +602,7 @@ int dtype_dup(MPI_Datatype oldh, MPI_Datatype* out)
     t->sticky_lb = o->sticky_lb; t->sticky_ub = o->sticky_ub;
     t->alignsize = o->alignsize; t->eltype = o->eltype; t->el_size = o->el_size;
     t->n_elements = o->n_elements; t->is_contig = o->is_contig;
-    t->runs = o->runs;
+    copy_layout(t.get(), o);
     t->committed = o->committed;
     set_contents(t.get(), 2, {}, {}, {oldh});
     *out = register_type(std::move(t));
@@ -637,6 +687,185 @@ int dtype_subarray(int ndims, const int* sizes, const int* subsizes, const int* 
     return MPI_SUCCESS;
 }
 
+// ---- MPI_Type_create_darray (api/mpi_datatype.cpp:218-600) ------------------
+namespace {
+
+constexpr int kDistBlock = 121, kDistCyclic = 122, kDfltDarg = -49767;
+
+void free_tmp(MPI_Datatype h)
+{
+    MPI_Datatype x = h;
+    if (dtype_is_derived(x)) dtype_free(&x);
+}
+
+// MPIR_Type_block (mpid/datatype.cpp:409-509)
+int darray_block(const int* gsizes, int dim, int ndims, int nprocs, int rank, int darg, int order,
+                 int64_t orig_extent, MPI_Datatype old, MPI_Datatype* out, int64_t* st_offset)
+{
+    const int global_size = gsizes[dim];
+    int blksize;
+    if (darg == kDfltDarg) {
+        blksize = (global_size + nprocs - 1) / nprocs;
+    } else {
+        blksize = darg;
+        if (blksize <= 0) { set_error("darray block size %d", blksize); return MPI_ERR_ARG; }
+        if ((int64_t)blksize * nprocs < global_size) {
+            set_error("darray blocks of %d x %d processes do not cover %d", blksize, nprocs, global_size);
+            return MPI_ERR_ARG;
+        }
+    }
+    const int64_t j = global_size - (int64_t)blksize * rank;
+    const int mysize = (int)std::max<int64_t>(0, std::min<int64_t>(blksize, j));
+    const bool fastest = order == MPI_ORDER_FORTRAN ? dim == 0 : dim == ndims - 1;
+    int rc;
+    if (fastest) {
+        rc = dtype_contiguous(mysize, old, out);
+    } else {
+        int64_t stride = orig_extent;
+        if (order == MPI_ORDER_FORTRAN)
+            for (int i = 0; i < dim; ++i) stride *= gsizes[i];
+        else
+            for (int i = ndims - 1; i > dim; --i) stride *= gsizes[i];
+        rc = dtype_vector(mysize, 1, stride, true, old, out, 6);
+    }
+    if (rc != MPI_SUCCESS) return rc;
+    *st_offset = mysize == 0 ? 0 : (int64_t)blksize * rank;
+    return MPI_SUCCESS;
+}
+
+// MPIR_Type_cyclic (mpid/datatype.cpp:512-637)
+int darray_cyclic(const int* gsizes, int dim, int ndims, int nprocs, int rank, int darg, int order,
+                  int64_t orig_extent, MPI_Datatype old, MPI_Datatype* out, int64_t* st_offset)
+{
+    const int blksize = darg == kDfltDarg ? 1 : darg;
+    if (blksize <= 0) { set_error("darray cyclic block size %d", blksize); return MPI_ERR_ARG; }
+    const int64_t st_index = (int64_t)rank * blksize, end_index = gsizes[dim] - 1;
+    int64_t local_size = 0;
+    if (end_index >= st_index) {
+        const int64_t per = (int64_t)nprocs * blksize;
+        local_size = ((end_index - st_index + 1) / per) * blksize;
+        local_size += std::min<int64_t>((end_index - st_index + 1) % per, blksize);
+    }
+    const int count = (int)(local_size / blksize), rem = (int)(local_size % blksize);
+    int64_t stride = (int64_t)nprocs * blksize * orig_extent;
+    if (order == MPI_ORDER_FORTRAN)
+        for (int i = 0; i < dim; ++i) stride *= gsizes[i];
+    else
+        for (int i = ndims - 1; i > dim; --i) stride *= gsizes[i];
+    MPI_Datatype t;
+    int rc = dtype_vector(count, blksize, stride, true, old, &t, 6);
+    if (rc != MPI_SUCCESS) return rc;
+    if (rem) {
+        // the last, short block is appended as a struct member
+        const int blk[2] = {1, rem};
+        const MPI_Aint d[2] = {0, (MPI_Aint)count * stride};
+        const MPI_Datatype ty[2] = {t, old};
+        MPI_Datatype tmp;
+        rc = dtype_struct(2, blk, d, ty, &tmp, 12);
+        free_tmp(t);
+        if (rc != MPI_SUCCESS) return rc;
+        t = tmp;
+    }
+    const bool first = order == MPI_ORDER_FORTRAN ? dim == 0 : dim == ndims - 1;
+    if (first) {
+        // the first dimension's offset and extent are set with LB / UB markers
+        const int blk[3] = {1, 1, 1};
+        const MPI_Aint d[3] = {0, (MPI_Aint)rank * blksize * orig_extent, orig_extent * gsizes[dim]};
+        const MPI_Datatype ty[3] = {MPI_LB, t, MPI_UB};
+        MPI_Datatype tmp;
+        rc = dtype_struct(3, blk, d, ty, &tmp, 12);
+        free_tmp(t);
+        if (rc != MPI_SUCCESS) return rc;
+        t = tmp;
+        *st_offset = 0;
+    } else {
+        *st_offset = (int64_t)rank * blksize;
+    }
+    if (local_size == 0) *st_offset = 0;
+    *out = t;
+    return MPI_SUCCESS;
+}
+
+}  // namespace
+
+int dtype_darray(int size, int rank, int ndims, const int* gsizes, const int* distribs, const int* dargs,
+                 const int* psizes, int order, MPI_Datatype oldh, MPI_Datatype* out)
+{
+    std::lock_guard<std::recursive_mutex> g(g_mu);
+    Dtype* o = lookup_locked(oldh);
+    if (!o) { set_error("invalid oldtype 0x%x", oldh); return MPI_ERR_TYPE; }
+    const int64_t orig_extent = is_builtin_h(oldh) ? o->size : o->extent;
+    // position in the process grid, row-major (api/mpi_datatype.cpp:346-353)
+    std::vector<int> coords((size_t)std::max(ndims, 1));
+    int procs = size, tmp_rank = rank;
+    for (int i = 0; i < ndims; ++i) {
+        if (psizes[i] == 0 || procs / psizes[i] == 0) {
+            // the reference divides by zero here
+            set_error("darray process grid does not divide size %d", size);
+            return MPI_ERR_ARG;
+        }
+        procs /= psizes[i];
+        coords[(size_t)i] = tmp_rank / procs;
+        tmp_rank %= procs;
+    }
+    std::vector<int64_t> st((size_t)std::max(ndims, 1), 0);
+    MPI_Datatype cur = oldh;
+    auto step = [&](int i) -> int {
+        MPI_Datatype nt;
+        int rc;
+        if (distribs[i] == kDistCyclic)
+            rc = darray_cyclic(gsizes, i, ndims, psizes[i], coords[(size_t)i], dargs[i], order, orig_extent, cur,
+                               &nt, &st[(size_t)i]);
+        else if (distribs[i] == kDistBlock)
+            rc = darray_block(gsizes, i, ndims, psizes[i], coords[(size_t)i], dargs[i], order, orig_extent, cur,
+                              &nt, &st[(size_t)i]);
+        else   // MPI_DISTRIBUTE_NONE: a block distribution over one process
+            rc = darray_block(gsizes, i, ndims, psizes[i], coords[(size_t)i], kDfltDarg, order, orig_extent, cur,
+                              &nt, &st[(size_t)i]);
+        if (cur != oldh) free_tmp(cur);
+        cur = rc == MPI_SUCCESS ? nt : oldh;
+        return rc;
+    };
+    int64_t disp1 = 0, tmp_size = 1;
+    int rc = MPI_SUCCESS;
+    if (order == MPI_ORDER_FORTRAN) {
+        for (int i = 0; rc == MPI_SUCCESS && i < ndims; ++i) rc = step(i);
+        if (ndims > 0) disp1 = st[0];
+        for (int i = 1; i < ndims; ++i) {
+            tmp_size *= gsizes[i - 1];
+            disp1 += tmp_size * st[(size_t)i];
+        }
+    } else {
+        for (int i = ndims - 1; rc == MPI_SUCCESS && i >= 0; --i) rc = step(i);
+        if (ndims > 0) disp1 = st[(size_t)ndims - 1];
+        for (int i = ndims - 2; i >= 0; --i) {
+            tmp_size *= gsizes[i + 1];
+            disp1 += tmp_size * st[(size_t)i];
+        }
+    }
+    if (rc != MPI_SUCCESS) return rc;
+    disp1 *= orig_extent;
+    int64_t disp2 = orig_extent;
+    for (int i = 0; i < ndims; ++i) disp2 *= gsizes[i];
+    const int blk[3] = {1, 1, 1};
+    const MPI_Aint d[3] = {0, disp1, disp2};
+    const MPI_Datatype ty[3] = {MPI_LB, cur, MPI_UB};
+    rc = dtype_struct(3, blk, d, ty, out, 12);
+    if (cur != oldh) free_tmp(cur);
+    if (rc != MPI_SUCCESS) return rc;
+    Dtype* t = lookup_locked(*out);
+    for (MPI_Datatype h : t->types) free_tmp(h);      // drop the struct's references
+    std::vector<int> ints{size, rank, ndims};
+    ints.insert(ints.end(), gsizes, gsizes + ndims);
+    ints.insert(ints.end(), distribs, distribs + ndims);
+    ints.insert(ints.end(), dargs, dargs + ndims);
+    ints.insert(ints.end(), psizes, psizes + ndims);
+    ints.push_back(order);
+    set_contents(t, 14, ints, {}, {oldh});
+    if (dtype_is_derived(oldh)) o->refs++;
+    return MPI_SUCCESS;
+}
+
 int dtype_commit(MPI_Datatype h)
 {
     std::lock_guard<std::recursive_mutex> g(g_mu);
@@ -675,10 +904,22 @@ int build_dev_layout(Dtype* t)
     DevLayout L;
     L.size = t->size;
     L.extent = t->extent;
-    L.nruns = (int64_t)t->runs.size();
+    L.nruns = dtype_nruns(t);
     int64_t al = 16;
     al = std::min(al, lowbit_align(t->size));
     al = std::min(al, lowbit_align(t->extent));
+    if (t->rn) {
+        // compact regular form: no run table at all
+        al = std::min({al, lowbit_align(t->rfirst), lowbit_align(t->rlen), lowbit_align(t->rstride)});
+        L.align = (int)al;
+        L.regular = 1;
+        L.first = t->rfirst;
+        L.blen = t->rlen;
+        L.stride = t->rstride;
+        t->dev = L;
+        t->dev_ready = true;
+        return MPI_SUCCESS;
+    }
     for (const DtRun& r : t->runs) {
         al = std::min(al, lowbit_align(r.disp));
         al = std::min(al, lowbit_align(r.len));
@@ -749,6 +990,10 @@ void dtype_serialize(const Dtype* t, std::vector<int64_t>& out)
     out.push_back(t->size);
     out.push_back(t->extent);
     out.push_back((int64_t)t->eltype);
+    if (t->rn) {            // compact form: flag -1, then first, len, stride, n
+        out.insert(out.end(), {-1, t->rfirst, t->rlen, t->rstride, t->rn});
+        return;
+    }
     out.push_back((int64_t)t->runs.size());
     for (const DtRun& r : t->runs) {
         out.push_back(r.disp);
@@ -758,6 +1003,21 @@ void dtype_serialize(const Dtype* t, std::vector<int64_t>& out)
 
 Dtype* dtype_from_blob(const int64_t* b, int64_t avail)
 {
+    if (avail >= 8 && b[3] == -1) {
+        if (b[7] <= 0 || b[5] <= 0 || b[7] > ((int64_t)1 << 40) || b[7] * b[5] != b[0]) return nullptr;
+        auto* t = new Dtype();
+        t->size = b[0];
+        t->extent = b[1];
+        t->eltype = (MPI_Datatype)b[2];
+        const TypeInfo* ti = type_info(t->eltype);
+        t->el_size = ti ? ti->size : -1;
+        t->committed = true;
+        t->rfirst = b[4];
+        t->rlen = b[5];
+        t->rstride = b[6];
+        t->rn = b[7];
+        return t;
+    }
     if (avail < 4 || b[3] < 0 || b[3] > kMaxRuns || avail < 4 + 2 * b[3]) return nullptr;
     auto* t = new Dtype();
     t->size = b[0];
@@ -786,8 +1046,13 @@ void dtype_delete(Dtype* t)
 
 void dt_span(const Dtype* t, int64_t count, int64_t* lo, int64_t* hi)
 {
-    if (t->runs.empty() || count <= 0) { *lo = *hi = 0; return; }
+    if ((t->runs.empty() && !t->rn) || count <= 0) { *lo = *hi = 0; return; }
     int64_t rl = INT64_MAX, rh = INT64_MIN;
+    if (t->rn) {
+        const int64_t last = t->rfirst + (t->rn - 1) * t->rstride;
+        rl = std::min(t->rfirst, last);
+        rh = std::max(t->rfirst, last) + t->rlen;
+    }
     for (const DtRun& r : t->runs) {
         rl = std::min(rl, r.disp);
         rh = std::max(rh, r.disp + r.len);
@@ -838,6 +1103,10 @@ int dt_acc_dev(int opidx, const Dtype* tc, int64_t count, const void* packed, vo
     const TypeInfo* ti = type_info(tc->eltype);
     if (!ti || op_check_dtype(opidx, tc->eltype) != MPI_SUCCESS) return MPI_SUCCESS;
     // every run holds whole elements (true for any type built from one basic type)
+    if (tc->rn && tc->rlen % ti->size) {
+        set_error("datatype runs split elements of 0x%x", tc->eltype);
+        return MPI_ERR_TYPE;
+    }
     for (const DtRun& r : tc->runs)
         if (r.len % ti->size) {
             set_error("datatype runs split elements of 0x%x", tc->eltype);
@@ -947,13 +1216,13 @@ int dt_copy_any(const void* src, int64_t scount, MPI_Datatype sdt, void* dst, in
     if (!st || !rt) { set_error("invalid datatype"); return MPI_ERR_TYPE; }
     const int64_t sbytes = scount * st->size, rbytes = rcount * rt->size;
     int64_t n = std::min(sbytes, rbytes);
-    const bool s_contig = st->runs.size() <= 1 && (scount <= 1 || st->size == st->extent);
-    const bool r_contig = rt->runs.size() <= 1 && (rcount <= 1 || rt->size == rt->extent);
+    DtRun s1{0, 0}, r1{0, 0};
+    const bool s_contig = single_run(st, &s1) && (scount <= 1 || st->size == st->extent);
+    const bool r_contig = single_run(rt, &r1) && (rcount <= 1 || rt->size == rt->extent);
     int rc = MPI_SUCCESS;
     if (n > 0) {
         if (s_contig && r_contig) {
-            rc = copy_any(static_cast<char*>(dst) + rt->runs[0].disp,
-                          static_cast<const char*>(src) + st->runs[0].disp, (size_t)n);
+            rc = copy_any(static_cast<char*>(dst) + r1.disp, static_cast<const char*>(src) + s1.disp, (size_t)n);
         } else if (sbytes == rbytes) {
             // pack the source into a device buffer, unpack it into the target
             rc = ensure_device();

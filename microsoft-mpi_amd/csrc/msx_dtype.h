@@ -57,6 +57,11 @@ struct Dtype {
     int64_t n_elements = 0;
     bool is_contig = false;
     std::vector<DtRun> runs;      // type map of one instance, in order, adjacent runs merged
+    // Compact regular run list (a vector / hvector of a one-run type), kept
+    // unmaterialised so huge strided types cost O(1) host memory: run k =
+    // [rfirst + k*rstride, +rlen), k < rn; `runs` stays empty while rn > 0 and
+    // is expanded only when another constructor needs the explicit list.
+    int64_t rn = 0, rfirst = 0, rlen = 0, rstride = 0;
     // MPI_Type_get_envelope / get_contents
     int combiner = 1;             // MPI_COMBINER_NAMED
     std::vector<int> ints;
@@ -74,6 +79,8 @@ Dtype* dtype_lookup(MPI_Datatype h);
 bool dtype_is_derived(MPI_Datatype h);
 // Data bytes of one instance (MPI_Type_size), -1 for an invalid handle.
 int64_t dtype_size(MPI_Datatype h);
+// Number of contiguous runs of one instance (compact or explicit form).
+int64_t dtype_nruns(const Dtype* t);
 
 // ---- constructors (argument checks are the caller's; return MPI error class)
 // Each creates an uncommitted type and stores its handle in *out.
@@ -90,6 +97,8 @@ int dtype_resized(MPI_Datatype old, int64_t lb, int64_t extent, MPI_Datatype* ou
 int dtype_dup(MPI_Datatype old, MPI_Datatype* out);
 int dtype_subarray(int ndims, const int* sizes, const int* subsizes, const int* starts, int order,
                    MPI_Datatype old, MPI_Datatype* out);
+int dtype_darray(int size, int rank, int ndims, const int* gsizes, const int* distribs, const int* dargs,
+                 const int* psizes, int order, MPI_Datatype old, MPI_Datatype* out);
 int dtype_commit(MPI_Datatype h);
 int dtype_free(MPI_Datatype* h);   // derived only (caller checked)
 void dtype_add_ref(MPI_Datatype h);

@@ -276,6 +276,41 @@ MSX_EXPORT int MPI_Type_create_subarray(int ndims, const int array_of_sizes[], c
     return fail("MPI_Type_create_subarray", rc);
 }
 
+// MPI_Type_create_darray (mpi_datatype.cpp:218-600): the checks in the
+// reference's order, then MPIR_Type_block / MPIR_Type_cyclic per dimension.
+MSX_EXPORT int MPI_Type_create_darray(int size, int rank, int ndims, const int array_of_gsizes[],
+                                      const int array_of_distribs[], const int array_of_dargs[],
+                                      const int array_of_psizes[], int order, MPI_Datatype oldtype,
+                                      MPI_Datatype* newtype)
+{
+    api_require_init("MPI_Type_create_darray");
+    Dtype* o;
+    int rc = v_handle(oldtype, &o);
+    if (rc == MPI_SUCCESS && rank < 0) rc = arg_err("negative rank");
+    if (rc == MPI_SUCCESS && size < 0) rc = arg_err("negative size");
+    if (rc == MPI_SUCCESS && ndims < 0) rc = arg_err("negative ndims");
+    if (rc == MPI_SUCCESS && !array_of_gsizes) rc = arg_err("null array_of_gsizes");
+    if (rc == MPI_SUCCESS && !array_of_distribs) rc = arg_err("null array_of_distribs");
+    if (rc == MPI_SUCCESS && !array_of_dargs) rc = arg_err("null array_of_dargs");
+    if (rc == MPI_SUCCESS && !array_of_psizes) rc = arg_err("null array_of_psizes");
+    if (rc == MPI_SUCCESS && order != MPI_ORDER_C && order != MPI_ORDER_FORTRAN) rc = arg_err("invalid order");
+    for (int i = 0; rc == MPI_SUCCESS && i < ndims; ++i) {
+        const int dist = array_of_distribs[i], darg = array_of_dargs[i];
+        if (array_of_gsizes[i] < 0) rc = arg_err("negative gsize");
+        else if (array_of_psizes[i] < 0) rc = arg_err("negative psize");
+        else if (dist != MPI_DISTRIBUTE_NONE && dist != MPI_DISTRIBUTE_BLOCK && dist != MPI_DISTRIBUTE_CYCLIC)
+            rc = arg_err("unknown distribution");
+        else if (darg != MPI_DISTRIBUTE_DFLT_DARG && darg <= 0) rc = arg_err("invalid array_of_dargs");
+        else if (dist == MPI_DISTRIBUTE_NONE && array_of_psizes[i] != 1)
+            rc = arg_err("MPI_DISTRIBUTE_NONE needs a process-grid size of 1");
+    }
+    if (rc == MPI_SUCCESS && !newtype) rc = arg_err("null newtype");
+    if (rc == MPI_SUCCESS)
+        rc = dtype_darray(size, rank, ndims, array_of_gsizes, array_of_distribs, array_of_dargs, array_of_psizes,
+                          order, oldtype, newtype);
+    return fail("MPI_Type_create_darray", rc);
+}
+
 // MPI_Type_create_resized (mpi_datatype.cpp)
 MSX_EXPORT int MPI_Type_create_resized(MPI_Datatype oldtype, MPI_Aint lb, MPI_Aint extent, MPI_Datatype* newtype)
 {
@@ -615,6 +650,7 @@ MSX_ALIAS(MPI_Type_create_hindexed_block) int PMPI_Type_create_hindexed_block(in
 MSX_ALIAS(MPI_Type_create_struct) int PMPI_Type_create_struct(int, const int[], const MPI_Aint[], const MPI_Datatype[], MPI_Datatype*);
 MSX_ALIAS(MPI_Type_struct) int PMPI_Type_struct(int, const int[], const MPI_Aint[], const MPI_Datatype[], MPI_Datatype*);
 MSX_ALIAS(MPI_Type_create_subarray) int PMPI_Type_create_subarray(int, const int[], const int[], const int[], int, MPI_Datatype, MPI_Datatype*);
+MSX_ALIAS(MPI_Type_create_darray) int PMPI_Type_create_darray(int, int, int, const int[], const int[], const int[], const int[], int, MPI_Datatype, MPI_Datatype*);
 MSX_ALIAS(MPI_Type_create_resized) int PMPI_Type_create_resized(MPI_Datatype, MPI_Aint, MPI_Aint, MPI_Datatype*);
 MSX_ALIAS(MPI_Type_dup) int PMPI_Type_dup(MPI_Datatype, MPI_Datatype*);
 MSX_ALIAS(MPI_Type_commit) int PMPI_Type_commit(MPI_Datatype*);

@@ -121,6 +121,7 @@ def lib():
         "MPI_Type_struct": (i, [i, p, p, p, p]),
         "MPI_Type_create_subarray": (i, [i, p, p, p, i, i, p]),
         "MPI_Type_create_resized": (i, [i, i64, i64, p]),
+        "MPI_Type_create_darray": (i, [i, i, i, p, p, p, p, i, i, p]),
         "MPI_Type_dup": (i, [i, p]),
         "MPI_Type_commit": (i, [p]),
         "MPI_Type_free": (i, [p]),

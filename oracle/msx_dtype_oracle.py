@@ -20,6 +20,8 @@ Attribute formulas follow the reference:
   MPID_Type_struct           mpid/datatype.cpp:2214-2473 (+ alignsize 2149-2195)
   MPID_Type_create_resized   mpid/datatype.cpp:1417-1493
   MPID_Type_convert_subarray mpid/datatype.cpp:3274-3399
+  MPI_Type_create_darray     api/mpi_datatype.cpp:218-600 with MPIR_Type_block /
+                             MPIR_Type_cyclic, mpid/datatype.cpp:409-637
 Parity pin: no reference test covers datatypes and the
 reference's datatype engine does not build here (it needs the CH3 runtime), so
 the restatement is pinned by the MPI-2.2 standard's worked examples
@@ -232,6 +234,79 @@ def subarray(sizes, subsizes, starts, order_c: bool, old: OType) -> OType:
     for s in sizes:
         full *= s
     return struct([1, 1, 1], [0, disp * ext, full], [marker(MPI_LB), t, marker(MPI_UB)])
+
+
+DIST_BLOCK, DIST_CYCLIC, DIST_NONE, DFLT_DARG = 121, 122, 123, -49767
+
+
+def _dims_after(gsizes, dim, order_c):
+    """Product of the faster-varying global sizes (the stride factor)."""
+    p = 1
+    for i in (range(dim + 1, len(gsizes)) if order_c else range(dim)):
+        p *= gsizes[i]
+    return p
+
+
+def _darray_block(gsizes, dim, nprocs, rank, darg, order_c, ext, old):
+    g = gsizes[dim]
+    blk = (g + nprocs - 1) // nprocs if darg == DFLT_DARG else darg
+    mysize = max(0, min(blk, g - blk * rank))
+    fastest = dim == len(gsizes) - 1 if order_c else dim == 0
+    if fastest:
+        t = contiguous(mysize, old)
+    else:
+        t = hvector(mysize, 1, ext * _dims_after(gsizes, dim, order_c), old)
+    return t, (0 if mysize == 0 else blk * rank)
+
+
+def _darray_cyclic(gsizes, dim, nprocs, rank, darg, order_c, ext, old):
+    blk = 1 if darg == DFLT_DARG else darg
+    st_i, end_i = rank * blk, gsizes[dim] - 1
+    local = 0
+    if end_i >= st_i:
+        per = nprocs * blk
+        local = ((end_i - st_i + 1) // per) * blk + min((end_i - st_i + 1) % per, blk)
+    count, rem = divmod(local, blk)
+    stride = nprocs * blk * ext * _dims_after(gsizes, dim, order_c)
+    t = hvector(count, blk, stride, old)
+    if rem:
+        t = struct([1, rem], [0, count * stride], [t, old])
+    first = dim == len(gsizes) - 1 if order_c else dim == 0
+    if first:
+        t = struct([1, 1, 1], [0, rank * blk * ext, ext * gsizes[dim]], [marker(MPI_LB), t, marker(MPI_UB)])
+        off = 0
+    else:
+        off = rank * blk
+    return t, (0 if local == 0 else off)
+
+
+def darray(size, rank, gsizes, distribs, dargs, psizes, order_c, old: OType) -> OType:
+    n = len(gsizes)
+    ext = old.extent
+    coords, procs, r = [], size, rank
+    for i in range(n):
+        procs //= psizes[i]
+        coords.append(r // procs)
+        r %= procs
+    st = [0] * n
+    cur = old
+    for i in (range(n - 1, -1, -1) if order_c else range(n)):
+        if distribs[i] == DIST_CYCLIC:
+            cur, st[i] = _darray_cyclic(gsizes, i, psizes[i], coords[i], dargs[i], order_c, ext, cur)
+        elif distribs[i] == DIST_BLOCK:
+            cur, st[i] = _darray_block(gsizes, i, psizes[i], coords[i], dargs[i], order_c, ext, cur)
+        else:
+            cur, st[i] = _darray_block(gsizes, i, psizes[i], coords[i], DFLT_DARG, order_c, ext, cur)
+    disp, step = 0, 1
+    dims = list(range(n - 1, -1, -1)) if order_c else list(range(n))
+    for k, i in enumerate(dims):
+        if k:
+            step *= gsizes[dims[k - 1]]
+        disp += step * st[i]
+    full = ext
+    for g in gsizes:
+        full *= g
+    return struct([1, 1, 1], [0, disp * ext, full], [marker(MPI_LB), cur, marker(MPI_UB)])
 
 
 # ---- data movement --------------------------------------------------------------

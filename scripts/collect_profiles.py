@@ -40,6 +40,13 @@ with open(os.path.join(SRC, "prof_trace", "trace_kernel_trace.csv")) as fi, \
         if any(s in row[k] for s in keep) and "k_combine_host" not in row[k]:
             w.writerow(row)
 for n in ("pmc_fetch_counter_collection.csv", "pmc_write_counter_collection.csv"):
-    shutil.copy(os.path.join(SRC, "prof_pmc", n), DST)
+    with open(os.path.join(SRC, "prof_pmc", n)) as fi, open(os.path.join(DST, n), "w", newline="") as fo:
+        r, w = csv.reader(fi), csv.writer(fo)
+        hdr = next(r)
+        w.writerow(hdr)
+        k = hdr.index("Kernel_Name")
+        for row in r:
+            if any(s in row[k] for s in keep) and "k_combine_host" not in row[k]:
+                w.writerow(row)
 shutil.copy(os.path.join(SRC, "steps.log"), DST)
 print("profiles ->", DST)

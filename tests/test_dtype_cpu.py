@@ -50,6 +50,8 @@ def build_oracle(r):
         return build_oracle(r[1])
     if k == "subarray":
         return O.subarray(r[1], r[2], r[3], r[4], build_oracle(r[5]))
+    if k == "darray":
+        return O.darray(r[1], r[2], r[3], r[4], r[5], r[6], r[7], build_oracle(r[8]))
     raise ValueError(k)
 
 
@@ -85,6 +87,11 @@ def build_lib(L, r, keep):
         rc = L.MPI_Type_create_subarray(n, ibuf(r[1]), ibuf(r[2]), ibuf(r[3]),
                                         C.MPI_ORDER_C if r[4] else C.MPI_ORDER_FORTRAN, build_lib(L, r[5], keep),
                                         ctypes.byref(out))
+    elif k == "darray":
+        n = len(r[3])
+        rc = L.MPI_Type_create_darray(r[1], r[2], n, ibuf(r[3]), ibuf(r[4]), ibuf(r[5]), ibuf(r[6]),
+                                      C.MPI_ORDER_C if r[7] else C.MPI_ORDER_FORTRAN, build_lib(L, r[8], keep),
+                                      ctypes.byref(out))
     else:
         raise ValueError(k)
     assert rc == 0, (r, rc, msx.last_error())
@@ -118,7 +125,7 @@ def random_recipe(rng, depth=0):
     if depth >= 2 or rng.random() < 0.3:
         return ("basic", rng.choice(BASICS))
     k = rng.choice(["contig", "vector", "hvector", "indexed", "hindexed", "iblock", "struct", "resized",
-                    "subarray", "dup"])
+                    "subarray", "dup", "darray"])
     sub = random_recipe(rng, depth + 1)
     if k == "contig":
         return ("contig", rng.randint(0, 4), sub)
@@ -147,7 +154,34 @@ def random_recipe(rng, depth=0):
         subs = [rng.randint(0, s) for s in sizes]
         starts = [rng.randint(0, s - ss) for s, ss in zip(sizes, subs)]
         return ("subarray", sizes, subs, starts, rng.random() < 0.5, sub)
+    if k == "darray":
+        return random_darray(rng, sub)
     return ("dup", sub)
+
+
+def random_darray(rng, sub):
+    nd = rng.randint(1, 3)
+    psizes = [rng.randint(1, 3) for _ in range(nd)]
+    size = 1
+    for q in psizes:
+        size *= q
+    gsizes = [rng.randint(1, 9) for _ in range(nd)]
+    distribs, dargs = [], []
+    for i in range(nd):
+        d = rng.choice([C.MPI_DISTRIBUTE_BLOCK, C.MPI_DISTRIBUTE_CYCLIC, C.MPI_DISTRIBUTE_NONE])
+        if d == C.MPI_DISTRIBUTE_NONE:
+            psizes[i] = 1
+        distribs.append(d)
+        if d == C.MPI_DISTRIBUTE_BLOCK and rng.random() < 0.5:
+            dargs.append(-(-gsizes[i] // psizes[i]) + rng.randint(0, 2))     # a block size that covers
+        elif d == C.MPI_DISTRIBUTE_CYCLIC and rng.random() < 0.5:
+            dargs.append(rng.randint(1, 3))
+        else:
+            dargs.append(C.MPI_DISTRIBUTE_DFLT_DARG)
+    size = 1
+    for q in psizes:
+        size *= q
+    return ("darray", size, rng.randrange(size), gsizes, distribs, dargs, psizes, rng.random() < 0.5, sub)
 
 
 # ---------------------------------------------------------------------------------
@@ -185,7 +219,7 @@ def test_oracle_standard_examples():
     assert (sa.lb, sa.extent, sa.true_lb) == (0, 160, 56)
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(80))
 def test_library_attributes_match_oracle(msxlib, seed):
     rng = random.Random(seed)
     r = random_recipe(rng)
@@ -218,6 +252,55 @@ def test_library_standard_examples(msxlib):
         assert lib_attrs(L, h) == want, r
         assert oracle_attrs(build_oracle(r)) == want, r
     free_all(L, keep)
+
+
+def test_darray_known_answers(msxlib):
+    """Hand-derived darray layouts (MPI-2.2 §4.1.4 semantics; the reference's
+    MPIR_Type_block / MPIR_Type_cyclic, mpid/datatype.cpp:409-637)."""
+    L = msxlib
+    I, B, Cy, N, D = C.MPI_INT, C.MPI_DISTRIBUTE_BLOCK, C.MPI_DISTRIBUTE_CYCLIC, C.MPI_DISTRIBUTE_NONE, \
+        C.MPI_DISTRIBUTE_DFLT_DARG
+    cases = [
+        # 1-D block, 10 ints over 3 processes, rank 1: elements 4..7
+        (("darray", 3, 1, [10], [B], [D], [3], True, ("basic", I)), [16, 20, 24, 28], (16, 0, 40, 16, 16)),
+        # 1-D cyclic(2), rank 1: elements 2, 3, 8, 9
+        (("darray", 3, 1, [10], [Cy], [2], [3], True, ("basic", I)), [8, 12, 32, 36], (16, 0, 40, 8, 32)),
+        # 2-D C order, 4 x 6 block x cyclic over a 2 x 3 grid, rank 4: rows 2-3, columns 1 and 4
+        (("darray", 6, 4, [4, 6], [B, Cy], [D, D], [2, 3], True, ("basic", I)), [52, 64, 76, 88],
+         (16, 0, 96, 52, 40)),
+        # the same grid in Fortran order: dimension 0 fastest
+        (("darray", 6, 4, [4, 6], [B, Cy], [D, D], [2, 3], False, ("basic", I)), None, None),
+        # MPI_DISTRIBUTE_NONE keeps the whole dimension
+        (("darray", 2, 1, [3, 4], [N, B], [D, D], [1, 2], True, ("basic", I)), [8, 12, 24, 28, 40, 44],
+         (24, 0, 48, 8, 40)),
+    ]
+    keep = []
+    for r, disps, attrs in cases:
+        t = build_oracle(r)
+        h = build_lib(L, r, keep)
+        if disps is not None:
+            assert [d for d, _ in t.typemap] == disps, r
+            assert oracle_attrs(t) == attrs, r
+        assert lib_attrs(L, h) == oracle_attrs(t), r
+    ni, na, nt, comb = c_int(), c_int(), c_int(), c_int()
+    assert L.MPI_Type_get_envelope(h, ctypes.byref(ni), ctypes.byref(na), ctypes.byref(nt), ctypes.byref(comb)) == 0
+    assert (ni.value, na.value, nt.value, comb.value) == (4 * 2 + 4, 0, 1, C.MPI_COMBINER_DARRAY)
+    free_all(L, keep)
+    # argument checks in the reference's order
+    t = c_int()
+    g, dd, ds, ps = ibuf([4]), ibuf([B]), ibuf([D]), ibuf([2])
+    assert L.MPI_Type_create_darray(2, 0, 1, g, dd, ds, ps, C.MPI_ORDER_C, C.MPI_DATATYPE_NULL,
+                                    ctypes.byref(t)) == C.MPI_ERR_TYPE
+    assert L.MPI_Type_create_darray(2, -1, 1, g, dd, ds, ps, C.MPI_ORDER_C, I, ctypes.byref(t)) == C.MPI_ERR_ARG
+    assert L.MPI_Type_create_darray(2, 0, 1, g, ibuf([99]), ds, ps, C.MPI_ORDER_C, I, ctypes.byref(t)) \
+        == C.MPI_ERR_ARG
+    assert L.MPI_Type_create_darray(2, 0, 1, g, dd, ibuf([0]), ps, C.MPI_ORDER_C, I, ctypes.byref(t)) \
+        == C.MPI_ERR_ARG
+    assert L.MPI_Type_create_darray(2, 0, 1, g, ibuf([N]), ds, ps, C.MPI_ORDER_C, I, ctypes.byref(t)) \
+        == C.MPI_ERR_ARG                                                # NONE needs psize 1
+    assert L.MPI_Type_create_darray(2, 0, 1, g, dd, ibuf([1]), ps, C.MPI_ORDER_C, I, ctypes.byref(t)) \
+        == C.MPI_ERR_ARG                                                # 1 x 2 blocks < 4 elements
+    assert L.MPI_Type_create_darray(2, 0, 1, g, dd, ds, ps, 7, I, ctypes.byref(t)) == C.MPI_ERR_ARG
 
 
 def test_envelope_and_contents(msxlib):
@@ -351,3 +434,77 @@ def test_pair_type_size_is_data_bytes(msxlib):
         assert L.MPI_Type_get_extent(dt, ctypes.byref(lb), ctypes.byref(ex)) == 0
         assert (lb.value, ex.value) == (0, ext)
         assert L.msx_type_size(dt) == ext
+
+
+def test_huge_strided_vector_stays_compact(msxlib):
+    """A vector of 2^30 single-element blocks keeps its run list compact (first,
+    length, stride): built instantly with the reference's attributes.  Using it
+    inside another constructor expands the list, past the 2^25-run limit ->
+    MPI_ERR_NO_MEM, a clean error rather than an allocation of 16 GiB."""
+    import time
+    L = msxlib
+    t = c_int()
+    t0 = time.perf_counter()
+    assert L.MPI_Type_vector(1 << 30, 1, 2, C.MPI_FLOAT, ctypes.byref(t)) == 0
+    assert time.perf_counter() - t0 < 0.5
+    assert lib_attrs(L, t.value) == (4 << 30, 0, ((1 << 30) - 1) * 8 + 4, 0, ((1 << 30) - 1) * 8 + 4)
+    assert L.MPI_Type_commit(ctypes.byref(t)) == 0
+    s = c_int()
+    assert L.MPI_Type_create_struct(2, ibuf([1, 1]), ibuf([0, 1 << 34], c_i64), ibuf([t.value, C.MPI_INT]),
+                                    ctypes.byref(s)) == C.MPI_ERR_NO_MEM
+    # a contiguous run of them merges into one run (no list at all)
+    u = c_int()
+    assert L.MPI_Type_vector(1 << 30, 4, 4, C.MPI_FLOAT, ctypes.byref(u)) == 0
+    assert lib_attrs(L, u.value) == (16 << 30, 0, 16 << 30, 0, 16 << 30)
+    assert L.MPI_Type_free(ctypes.byref(t)) == 0 and L.MPI_Type_free(ctypes.byref(u)) == 0
+
+
+UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                      ctypes.POINTER(ctypes.c_int))
+
+
+def make_typed_sub_op(L, t):
+    """A user function that walks the datatype's type map (from the oracle)
+    and computes inout = in - inout element by element, as a user of a derived
+    datatype would write it; it checks it received the handle it expects."""
+    seen = []
+
+    def fn(invec, inoutvec, n, dt):
+        seen.append((n[0], dt[0]))
+        for i in range(n[0]):
+            for d, sz in t["map"].typemap:
+                off = i * t["map"].extent + d
+                x = ctypes.c_int.from_address(invec + off)
+                y = ctypes.c_int.from_address(inoutvec + off)
+                y.value = x.value - y.value
+    cb = UF(fn)
+    op = c_int()
+    assert L.MPI_Op_create(cb, 0, ctypes.byref(op)) == 0
+    return op, cb, seen
+
+
+def test_reduce_local_user_op_on_derived_type(msxlib):
+    """MPI_Reduce_local with a user op and a committed derived datatype calls
+    the user function once with (in, inout, count, handle) on the typed buffers
+    (MPID_Uop_call, api/mpi_reduce.cpp:361); a builtin op rejects the derived
+    type with MPI_ERR_OP (the check table), an uncommitted one MPI_ERR_TYPE."""
+    L = msxlib
+    r = ("indexed", [2, 1, 3], [0, 4, 7], ("basic", C.MPI_INT))
+    keep = []
+    h = build_lib(L, r, keep)
+    t = {"map": build_oracle(r)}
+    op, cb, seen = make_typed_sub_op(L, t)
+    a = np.arange(40, dtype=np.int32)
+    b = np.full(40, 100, dtype=np.int32)
+    assert L.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, 3, h, op.value) == C.MPI_ERR_TYPE   # uncommitted
+    x = c_int(h)
+    assert L.MPI_Type_commit(ctypes.byref(x)) == 0
+    assert L.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, 3, h, C.MPI_SUM) == C.MPI_ERR_OP
+    assert L.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, 3, h, op.value) == 0
+    assert seen == [(3, h)]
+    exp = np.full(40, 100, dtype=np.int32)
+    idx = [i * t["map"].extent // 4 + d // 4 for i in range(3) for d, _ in t["map"].typemap]
+    exp[idx] = a[idx] - 100
+    assert b.tolist() == exp.tolist()
+    assert L.MPI_Op_free(ctypes.byref(op)) == 0
+    free_all(L, keep)

@@ -122,6 +122,7 @@ def test_pack_unpack_device_buffers(L, case):
     typed = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
     want = O.pack(t, count, typed.cpu().numpy(), base)
     out = torch.zeros(want.size, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
     pos = c_int(0)
     rc = L.MPI_Pack(typed.data_ptr() + base, count, h, out.data_ptr(), out.numel(), ctypes.byref(pos),
                     C.MPI_COMM_WORLD)
@@ -175,6 +176,7 @@ def test_large_subarray_equals_torch_slice(L):
     h = _commit(L, ("subarray", [n0, n1, n2], [s0, s1, s2], list(st), True, ("basic", C.MPI_FLOAT)), keep)
     want = x[st[0]:st[0] + s0, st[1]:st[1] + s1, st[2]:st[2] + s2].contiguous()
     out = torch.empty_like(want)
+    torch.cuda.synchronize()          # blocking MPI calls take buffers whose producers have finished
     pos = c_int(0)
     nb = want.numel() * 4
     assert L.MPI_Pack(x.data_ptr(), 1, h, out.data_ptr(), nb, ctypes.byref(pos), C.MPI_COMM_WORLD) == 0
@@ -182,6 +184,7 @@ def test_large_subarray_equals_torch_slice(L):
     assert pos.value == nb
     assert torch.equal(out.view(torch.int32), want.view(torch.int32))
     y = torch.zeros_like(x)
+    torch.cuda.synchronize()
     pos = c_int(0)
     assert L.MPI_Unpack(out.data_ptr(), nb, ctypes.byref(pos), y.data_ptr(), 1, h, C.MPI_COMM_WORLD) == 0
     torch.cuda.synchronize()
@@ -203,6 +206,7 @@ def test_large_vector_round_trip_general_layout(L):
     ext = t.extent
     x = torch.randint(-2**31, 2**31 - 1, (count * ext // 4,), dtype=torch.int32, device="cuda")
     packed = torch.empty(count * t.size // 4, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
     pos = c_int(0)
     assert L.MPI_Pack(x.data_ptr(), count, h, packed.data_ptr(), packed.numel() * 4, ctypes.byref(pos),
                       C.MPI_COMM_WORLD) == 0
@@ -210,6 +214,7 @@ def test_large_vector_round_trip_general_layout(L):
     rows = (torch.arange(count, device="cuda") * (ext // 4)).unsqueeze(1) + idx.unsqueeze(0)
     assert torch.equal(packed, x[rows.reshape(-1)])
     y = torch.zeros_like(x)
+    torch.cuda.synchronize()
     pos = c_int(0)
     assert L.MPI_Unpack(packed.data_ptr(), packed.numel() * 4, ctypes.byref(pos), y.data_ptr(), count, h,
                         C.MPI_COMM_WORLD) == 0
@@ -243,6 +248,7 @@ def test_long_run_layouts(L, r, mis):
         want = O.pack(t, count, typed, base)
         td = torch.from_numpy(typed).cuda()
         out = torch.zeros(want.size, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
         pos = c_int(0)
         assert L.MPI_Pack(td.data_ptr() + base, count, h, out.data_ptr(), want.size, ctypes.byref(pos),
                           C.MPI_COMM_WORLD) == 0, msx.last_error()
@@ -255,4 +261,53 @@ def test_long_run_layouts(L, r, mis):
         assert L.MPI_Unpack(src.ctypes.data, src.size, ctypes.byref(pos), dst.ctypes.data + base, count, h,
                             C.MPI_COMM_WORLD) == 0, msx.last_error()
         assert np.array_equal(dst, exp), (r, count, mis)
+    free_all(L, keep)
+
+
+def test_compact_vector_beyond_explicit_run_limit(L):
+    """2^27 strided blocks (4x the explicit run-list limit) pack straight from
+    the compact (first, length, stride) form: MPI_Pack of every other fp32 of a
+    1 GiB buffer equals torch's x[::2], and unpack restores exactly those."""
+    n = 1 << 28
+    x = torch.randn(n, device="cuda")
+    t = c_int()
+    assert L.MPI_Type_vector(n // 2, 1, 2, C.MPI_FLOAT, ctypes.byref(t)) == 0
+    assert L.MPI_Type_commit(ctypes.byref(t)) == 0
+    out = torch.empty(n // 2, device="cuda")
+    torch.cuda.synchronize()
+    pos = c_int(0)
+    assert L.MPI_Pack(x.data_ptr(), 1, t.value, out.data_ptr(), 2 * n, ctypes.byref(pos), C.MPI_COMM_WORLD) == 0, \
+        msx.last_error()
+    torch.cuda.synchronize()
+    bad = (out != x[::2]).nonzero().flatten()
+    assert bad.numel() == 0, (bad.numel(), bad[:8].tolist(), bad[-4:].tolist())
+    y = torch.zeros_like(x)
+    torch.cuda.synchronize()
+    pos = c_int(0)
+    assert L.MPI_Unpack(out.data_ptr(), 2 * n, ctypes.byref(pos), y.data_ptr(), 1, t.value, C.MPI_COMM_WORLD) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y[::2], x[::2]) and not y[1::2].any()
+    assert L.MPI_Type_free(ctypes.byref(t)) == 0
+
+
+def test_reduce_local_user_op_derived_type_device_buffers(L):
+    """User op + derived type on DEVICE buffers: the library stages the type's
+    byte span through host memory around the user function; the bytes between
+    mapped elements of inout come back unchanged."""
+    from test_dtype_cpu import make_typed_sub_op
+    r = ("hvector", 5, 2, 24, ("basic", C.MPI_INT))
+    keep = []
+    h = _commit(L, r, keep)
+    t = {"map": build_oracle(r)}
+    op, cb, seen = make_typed_sub_op(L, t)
+    a = torch.arange(200, dtype=torch.int32, device="cuda")
+    b = torch.full((200,), 7, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert L.MPI_Reduce_local(a.data_ptr() + 8, b.data_ptr() + 8, 4, h, op.value) == 0, msx.last_error()
+    exp = np.full(200, 7, dtype=np.int32)
+    idx = [2 + i * t["map"].extent // 4 + d // 4 for i in range(4) for d, _ in t["map"].typemap]
+    exp[idx] = np.arange(200, dtype=np.int32)[idx] - 7
+    assert b.cpu().numpy().tolist() == exp.tolist()
+    assert seen == [(4, h)]
+    assert L.MPI_Op_free(ctypes.byref(op)) == 0
     free_all(L, keep)

@@ -42,6 +42,7 @@ def _dev(a, offset=0):
     t = torch.zeros(raw.size + offset + 64, dtype=torch.uint8, device="cuda")
     if raw.size:
         t[offset:offset + raw.size] = torch.from_numpy(raw.copy()).cuda()
+    torch.cuda.synchronize()      # the library's streams do not order after torch's
     return t, t.data_ptr() + offset
 
 

@@ -40,6 +40,7 @@ def todev(a):
     t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
     if a.nbytes:
         t.copy_(torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()))
+    torch.cuda.synchronize()      # the library's streams do not order after torch's
     return t
 
 def fromdev(t, like, n=None):
