@@ -41,17 +41,6 @@ __device__ __forceinline__ void issued_together(u32x4& x, u32x4& y)
 // T  = element type used for scalar elements;
 // VT = lane type used inside a 16-byte vector (== T except bitwise ops, which
 //      run on 32-bit words regardless of the MPI element type).
-// XCD-contiguous tile order (the default): workgroup b is dispatched to XCD
-// b % 8, so with XCD set XCD x processes one contiguous 1/8 of the tiles (its
-// own L2 and a sequential DRAM page stream) instead of every 8th tile.
-// Measured on the 256 MiB fp32 SUM: 7.14 TB/s vs 7.01 TB/s in dispatch order
-// (interleaved sweep, profiles/r01/bench_sweep.log).
-__device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned nb)
-{
-    const unsigned q = nb >> 3, r = nb & 7, x = b & 7, j = b >> 3;
-    return x * q + (x < r ? x : r) + j;
-}
-
 template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, bool XCD = true>
 __device__ __forceinline__ void combine_body(const T* __restrict__ in, T* __restrict__ io, size_t head,
                                              size_t nvec, size_t tail)

@@ -110,7 +110,8 @@ __global__ __launch_bounds__(kPackBlock) void k_dt_pack(CopyArgs a)
 {
     typedef typename GranT<G>::T T;
     const int64_t stride = (int64_t)gridDim.x * kPackBlock;
-    for (int64_t g = (int64_t)blockIdx.x * kPackBlock + threadIdx.x; g < a.ngran; g += stride) {
+    const int64_t bid = xcd_tile(blockIdx.x, gridDim.x);
+    for (int64_t g = bid * kPackBlock + threadIdx.x; g < a.ngran; g += stride) {
         T* t = reinterpret_cast<T*>(a.typed + typed_off<G, REG, NARROW>(a, g));
         T* p = reinterpret_cast<T*>(a.packed) + g;
         if constexpr (UNPACK) *t = __builtin_nontemporal_load(p);
@@ -130,6 +131,7 @@ __global__ __launch_bounds__(kPackBlock) void k_dt_runs(CopyArgs a)
     const int lane = threadIdx.x & 63;
     const int64_t nunits = (a.ngran / a.gsize) * a.nruns;        // instances x runs
     const int64_t nw = (int64_t)gridDim.x * kWaves;
+    // (dispatch order here: XCD-contiguous order measured 10 % slower for this kernel)
     for (int64_t u = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); u < nunits; u += nw) {
         const int64_t i = u / a.nruns, k = u - i * a.nruns;
         const int64_t po = a.poff[k];
