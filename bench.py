@@ -230,6 +230,57 @@ PER_OP = [
 ]
 
 
+def cpu_baseline_collectives(p=8, seconds_each=2.0):
+    """The reference's collective schedules restated on the CPU
+    (oracle/msx_oracle_sched.c, from mpid/reduce.cpp: Rabenseifner allreduce,
+    recursive-halving reduce_scatter), p ranks simulated in lock step on ONE
+    core with memcpy as the transport: the combine + copy work of a p-rank
+    MS-MPI job, serialised.  Bounded samples (SURVEY.md §8(d) CPU baseline for
+    c3-c5): 16 MiB per rank for c3 / c5, a 64 MiB sendbuf per rank for c4.
+    busBW uses the same formulas as the GPU numbers (S/t·2(p-1)/p, S/t·(p-1)/p)."""
+    import numpy as np
+    import oracle
+    import msx
+    C = msx.C
+    rng = np.random.default_rng(0x5EED)
+
+    def timed(fn):
+        fn()
+        calls, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            calls += 1
+            el = time.perf_counter() - t0
+            if el >= seconds_each:
+                return el / calls, calls
+
+    out = {"ranks_simulated": p, "cores": 1, "kind": "port"}
+    n = 1 << 22
+    send = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(p)]
+    recv = [np.empty(n, np.float32) for _ in range(p)]
+    t, k = timed(lambda: oracle.allreduce(C.MPI_SUM, C.MPI_FLOAT, send, recv))
+    S = n * 4
+    out["c3_allreduce_sum_f32"] = {"bytes_per_rank": S, "seconds": round(t, 5), "calls": k,
+                                   "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 3)}
+    del send, recv
+    per = (1 << 23) // p
+    send = [rng.integers(0, 1000003, per * p).astype(np.float64) for _ in range(p)]
+    recv = [np.empty(per, np.float64) for _ in range(p)]
+    t, k = timed(lambda: oracle.reduce_scatter(C.MPI_MAX, C.MPI_DOUBLE, [per] * p, send, recv))
+    S = per * p * 8
+    out["c4_reduce_scatter_max_f64"] = {"bytes_per_rank": S, "seconds": round(t, 5), "calls": k,
+                                        "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 3)}
+    del send, recv
+    n = 1 << 21
+    send = [rng.integers(0, 2**63 - 1, n, dtype=np.int64).astype(np.uint64) for _ in range(p)]
+    recv = [np.empty(n, np.uint64) for _ in range(p)]
+    t, k = timed(lambda: oracle.allreduce(C.MPI_BAND, C.MPI_UINT64_T, send, recv))
+    S = n * 8
+    out["c5_allreduce_band_u64"] = {"bytes_per_rank": S, "seconds": round(t, 5), "calls": k,
+                                    "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 3)}
+    return out
+
+
 def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
     """GB/s of HBM traffic (2 reads + 1 write per element) per (op, type), from
     HIP events on the launch stream around 10 launches (median of 3 rounds).
@@ -590,6 +641,8 @@ def main():
             del src, acc
             torch.cuda.empty_cache()
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
+            if not args.no_collectives:
+                out["cpu_baseline_collectives"] = cpu_baseline_collectives(8, min(2.0, args.cpu_seconds))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
