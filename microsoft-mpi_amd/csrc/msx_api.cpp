@@ -155,6 +155,14 @@ int v_dtype_any(const void* buf, long long count, MPI_Datatype dt)
 // MpiaDatatypeValidateBuffer (mpi_api.h:190-212)
 int v_buffer(MPI_Datatype dt, const void* buf, long long count)
 {
+    if (dtype_is_derived(dt)) {
+        const Dtype* t = dtype_lookup(dt);
+        if (buf == nullptr && count > 0 && t && t->true_lb == 0 && t->size > 0) {
+            set_error("null buffer");
+            return MPI_ERR_BUFFER;
+        }
+        return MPI_SUCCESS;
+    }
     if (buf == nullptr && count > 0 && type_size(dt) > 0) {
         set_error("null buffer");
         return MPI_ERR_BUFFER;
@@ -434,7 +442,7 @@ MSX_EXPORT int MPI_Allreduce(const void* sendbuf, void* recvbuf, int count, MPI_
     Comm* c;
     OpRef r;
     int rc = v_comm(comm, &c);
-    if (rc == MPI_SUCCESS) rc = v_dtype(recvbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(recvbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
     if (rc == MPI_SUCCESS && count > 0) {
         if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
@@ -456,7 +464,7 @@ MSX_EXPORT int MPI_Reduce(const void* sendbuf, void* recvbuf, int count, MPI_Dat
     OpRef r;
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS && (root < 0 || root >= c->size)) { set_error("invalid root %d", root); rc = MPI_ERR_ROOT; }
-    if (rc == MPI_SUCCESS) rc = v_dtype(sendbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(sendbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
     if (rc == MPI_SUCCESS) {
         if (c->rank == root) {
@@ -484,7 +492,7 @@ int validate_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const i
         if (recvcounts[i] < 0) { set_error("negative recvcount %d", recvcounts[i]); return MPI_ERR_COUNT; }
         sentinel |= recvcounts[i];   // the reference's OR trick (mpi_reduce.cpp:833-847)
     }
-    int rc = v_dtype(sendbuf, sentinel, datatype);
+    int rc = v_dtype_any(sendbuf, sentinel, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, r);
     if (rc == MPI_SUCCESS && recvcounts[c->rank] > 0) {
         if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
@@ -542,7 +550,7 @@ int scan_common(const char* fn, const void* sendbuf, void* recvbuf, int count, M
         if (request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
         else *request = MPI_REQUEST_NULL;
     }
-    if (rc == MPI_SUCCESS) rc = v_dtype(recvbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(recvbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
     if (rc == MPI_SUCCESS && count > 0) {
         if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
@@ -602,7 +610,7 @@ MSX_EXPORT int MPI_Iallreduce(const void* sendbuf, void* recvbuf, int count, MPI
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS && request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
     if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
-    if (rc == MPI_SUCCESS) rc = v_dtype(recvbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(recvbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
     if (rc == MPI_SUCCESS && count > 0) {
         if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
@@ -626,7 +634,7 @@ MSX_EXPORT int MPI_Ireduce(const void* sendbuf, void* recvbuf, int count, MPI_Da
     if (rc == MPI_SUCCESS && request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
     if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
     if (rc == MPI_SUCCESS && (root < 0 || root >= c->size)) { set_error("invalid root"); rc = MPI_ERR_ROOT; }
-    if (rc == MPI_SUCCESS) rc = v_dtype(sendbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(sendbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
     if (rc == MPI_SUCCESS) {
         if (c->rank == root) {

@@ -189,6 +189,14 @@ int local_combine(const OpRef& op, MPI_Datatype dt, const void* in, void* inout,
 // ---------------------------------------------------------------------------
 // collectives: single-rank forms here, multi-rank forms in the transport engine
 // ---------------------------------------------------------------------------
+// MPIR_Localcopy (mpid/pt2pt.cpp:770-948): a predefined type is one memcpy,
+// a derived one goes through the pack / unpack kernels (non-contiguous copy).
+int local_copy(const void* src, void* dst, size_t count, MPI_Datatype dt)
+{
+    if (dtype_is_derived(dt)) return dt_copy_any(src, (int64_t)count, dt, dst, (int64_t)count, dt);
+    return copy_any(dst, src, count * (size_t)type_size(dt));
+}
+
 int coll_barrier(Comm* c)
 {
     if (c->size == 1 || !c->tp) return MPI_SUCCESS;
@@ -200,7 +208,7 @@ int coll_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MP
 {
     if (c->size == 1) {
         if (sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
-        return copy_any(recvbuf, sendbuf, count * (size_t)type_size(dt));
+        return local_copy(sendbuf, recvbuf, count, dt);
     }
     return engine_allreduce(c, sendbuf, recvbuf, count, dt, op);
 }
@@ -210,7 +218,7 @@ int coll_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_D
 {
     if (c->size == 1) {
         if (sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
-        return copy_any(recvbuf, sendbuf, count * (size_t)type_size(dt));
+        return local_copy(sendbuf, recvbuf, count, dt);
     }
     return engine_reduce(c, sendbuf, recvbuf, count, dt, op, root);
 }
@@ -220,7 +228,7 @@ int coll_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* 
 {
     if (c->size == 1) {
         if (sendbuf == MPI_IN_PLACE || recvcounts[0] == 0) return MPI_SUCCESS;
-        return copy_any(recvbuf, sendbuf, (size_t)recvcounts[0] * (size_t)type_size(dt));
+        return local_copy(sendbuf, recvbuf, (size_t)recvcounts[0], dt);
     }
     return engine_reduce_scatter(c, sendbuf, recvbuf, recvcounts, dt, op);
 }
@@ -231,7 +239,7 @@ int coll_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Dat
     if (c->size == 1) {
         // Exscan leaves rank 0's recvbuf undefined (unchanged here).
         if (exclusive || sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
-        return copy_any(recvbuf, sendbuf, count * (size_t)type_size(dt));
+        return local_copy(sendbuf, recvbuf, count, dt);
     }
     return engine_scan(c, sendbuf, recvbuf, count, dt, op, exclusive);
 }

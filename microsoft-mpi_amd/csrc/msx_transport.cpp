@@ -681,29 +681,94 @@ int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>
 }
 
 // ---- host path for user-defined ops --------------------------------------
-// User functions are host code; gather every contribution to host memory and
-// evaluate the reference's recursive-doubling order (reduce.cpp:3890-3925,
+// User functions are host code; every contribution is gathered to host memory
+// as an IMAGE: the bytes `count` elements of `dt` span.  For a predefined type
+// that is the packed array; for a derived datatype (which only user ops
+// accept, the builtin check tables reject it) it is the typed byte span, so
+// the user function sees the layout it was written for.  Pointers handed
+// around below are TYPED BASES (image start - lo), like the user's buffers.
+struct Img {
+    int64_t lo = 0;            // image byte 0 = typed byte lo
+    size_t bytes = 0;
+    const Dtype* t = nullptr;  // derived type, or null (predefined)
+    size_t esz = 0;            // predefined element size
+};
+
+Img img_of(MPI_Datatype dt, size_t count)
+{
+    Img m;
+    if (dtype_is_derived(dt)) {
+        m.t = dtype_lookup(dt);
+        int64_t lo, hi;
+        dt_span(m.t, (int64_t)count, &lo, &hi);
+        m.lo = lo;
+        m.bytes = (size_t)(hi - lo);
+    } else {
+        m.esz = (size_t)type_size(dt);
+        m.bytes = count * m.esz;
+    }
+    return m;
+}
+
+// image <- buf (any memory)
+int img_load(const Img& m, const void* buf, char* img)
+{
+    return copy_any(img, static_cast<const char*>(buf) + m.lo, m.bytes);
+}
+
+// buf <- image: a derived type writes only the bytes its type map covers
+// (MPIR_Localcopy through the type, gaps of `buf` untouched): the mapped bytes
+// are gathered on the host and the GPU unpack kernel scatters them.
+int img_store(const Img& m, size_t count, const char* typed_base, void* buf)
+{
+    if (!m.t) return copy_any(buf, typed_base, m.bytes);
+    if (count == 0 || m.t->size == 0) return MPI_SUCCESS;
+    std::vector<char> packed((size_t)m.t->size * count);
+    Dtype* t = const_cast<Dtype*>(m.t);
+    size_t p = 0;
+    auto run = [&](int64_t i, int64_t disp, int64_t len) {
+        memcpy(packed.data() + p, typed_base + i * t->extent + disp, (size_t)len);
+        p += (size_t)len;
+    };
+    for (size_t i = 0; i < count; ++i) {
+        if (t->rn)
+            for (int64_t k = 0; k < t->rn; ++k) run((int64_t)i, t->rfirst + k * t->rstride, t->rlen);
+        else
+            for (const DtRun& r : t->runs) run((int64_t)i, r.disp, r.len);
+    }
+    return dt_unpack_any(t, (int64_t)count, packed.data(), buf);
+}
+
+// inout = in (op) inout over `count` elements, typed bases
+void img_call(const OpRef& op, MPI_Datatype dt, const Img& m, size_t count, const char* in, char* io)
+{
+    MPI_Datatype d = dt;
+    if (m.t) {
+        int len = (int)count;      // API counts are int
+        op.user_fn(const_cast<char*>(in), io, &len, &d);
+        return;
+    }
+    for (size_t off = 0; off < count;) {
+        size_t n = std::min(count - off, (size_t)0x7fffffff);
+        int len = (int)n;
+        op.user_fn(const_cast<char*>(in) + off * m.esz, io + off * m.esz, &len, &d);
+        off += n;
+    }
+}
+
+// Evaluate the reference's recursive-doubling order (reduce.cpp:3890-3925,
 // non-commutative branch included) with the user's function.
 int host_user_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count,
                         MPI_Datatype dt, const OpRef& op)
 {
-    const int p = c->size, esz = type_size(dt);
-    const size_t bytes = count * (size_t)esz;
+    const int p = c->size;
+    const Img m = img_of(dt, count);
+    const size_t bytes = m.bytes;
     std::vector<char> mine(bytes), all((size_t)p * bytes);
-    int rc = copy_any(mine.data(), sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, bytes);
+    int rc = img_load(m, sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, mine.data());
     if (rc == MPI_SUCCESS) rc = c->tp->allgather(mine.data(), bytes, all.data());
     if (rc != MPI_SUCCESS) return rc;
-    auto call = [&](const char* in, char* io) {
-        size_t off = 0;
-        while (off < count) {
-            size_t n = count - off;
-            if (n > 0x7fffffff) n = 0x7fffffff;
-            int len = (int)n;
-            MPI_Datatype d = dt;
-            op.user_fn(const_cast<char*>(in) + off * esz, io + off * esz, &len, &d);
-            off += n;
-        }
-    };
+    auto call = [&](const char* in, char* io) { img_call(op, dt, m, count, in - m.lo, io - m.lo); };
     // Simulate every rank's recursive doubling; keep our own rank's result.
     const int pof2 = pof2_floor(p), rem = p - pof2;
     std::vector<std::vector<char>> v((size_t)p);
@@ -725,40 +790,34 @@ int host_user_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t coun
     }
     const int me = c->rank;
     const int src = (me < 2 * rem && (me & 1) == 0) ? me + 1 : me;
-    return copy_any(recvbuf, v[src].data(), bytes);
+    return img_store(m, count, v[src].data() - m.lo, recvbuf);
 }
 
 // Evaluate RankTree `t` on host with a user function (same association and
-// inout/in roles as k_tree: the left operand is `inout`).  x[r] = rank r's
-// contribution (count elements).
+// inout/in roles as k_tree: the left operand is `inout`).  x[r] = typed base of
+// rank r's contribution (count elements, image `m`); the result image is
+// written at typed base `out`.
 void eval_tree_host(const RankTree& t, const std::vector<const char*>& x, char* out, size_t count,
-                    MPI_Datatype dt, const OpRef& op)
+                    MPI_Datatype dt, const OpRef& op, const Img& m)
 {
-    const size_t esz = (size_t)type_size(dt), bytes = count * esz;
-    auto call = [&](const char* in, char* io) {
-        for (size_t off = 0; off < count;) {
-            size_t n = std::min(count - off, (size_t)0x7fffffff);
-            int len = (int)n;
-            MPI_Datatype d = dt;
-            op.user_fn(const_cast<char*>(in) + off * esz, io + off * esz, &len, &d);
-            off += n;
-        }
-    };
+    const size_t bytes = m.bytes;
+    auto call = [&](const char* in, char* io) { img_call(op, dt, m, count, in, io); };
+    auto img = [&](const char* base) { return base + m.lo; };
     if (t.chain) {
-        memcpy(out, x[(size_t)t.src[0]], bytes);
+        memcpy(out + m.lo, img(x[(size_t)t.src[0]]), bytes);
         for (int k = 1; k < t.P; ++k) call(x[(size_t)t.src[k]], out);
         return;
     }
     const int nl = t.nleaves ? t.nleaves : t.P;
     std::vector<std::vector<char>> v((size_t)nl);
     for (int k = 0; k < nl; ++k) {
-        v[(size_t)k].assign(x[(size_t)t.src[2 * k]], x[(size_t)t.src[2 * k]] + bytes);
-        if ((t.pairmask >> k) & 1u) call(x[(size_t)t.src[2 * k + 1]], v[(size_t)k].data());
+        v[(size_t)k].assign(img(x[(size_t)t.src[2 * k]]), img(x[(size_t)t.src[2 * k]]) + bytes);
+        if ((t.pairmask >> k) & 1u) call(x[(size_t)t.src[2 * k + 1]], v[(size_t)k].data() - m.lo);
     }
     for (int w = 1; w < t.P; w *= 2)
         for (int k = 0; k + w < t.P; k += 2 * w)
-            if (k + w < nl) call(v[(size_t)(k + w)].data(), v[(size_t)k].data());
-    memcpy(out, v[0].data(), bytes);
+            if (k + w < nl) call(v[(size_t)(k + w)].data() - m.lo, v[(size_t)k].data() - m.lo);
+    memcpy(out + m.lo, v[0].data(), bytes);
 }
 
 // Engine-private device scratch (grows, never shrinks; engine worker only).
@@ -1103,7 +1162,7 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
 {
     Transport* tp = c->tp;
     const int p = c->size, me = c->rank;
-    const size_t esz = (size_t)type_size(dt);
+    const size_t esz = dtype_is_derived(dt) ? 0 : (size_t)type_size(dt);   // derived: user ops only
     std::vector<size_t> disp((size_t)p + 1, 0);
     size_t maxcnt = 0;
     for (int r = 0; r < p; ++r) {
@@ -1308,7 +1367,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
 {
     Transport* tp = c->tp;
     const int p = c->size, me = c->rank;
-    const size_t esz = (size_t)type_size(dt);
+    const size_t esz = dtype_is_derived(dt) ? 0 : (size_t)type_size(dt);   // derived: user ops only
     std::vector<size_t> disp((size_t)p + 1, 0);
     size_t maxcnt = 0;
     for (int r = 0; r < p; ++r) {
@@ -1321,33 +1380,39 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
     const char* src = static_cast<const char*>(in_place ? recvbuf : sendbuf);
 
     if (op.opidx == O_NULL) {
-        std::vector<char> full(total * esz);
-        int rc = copy_any(full.data(), src, total * esz);
+        // images of the whole input (total elements) and of my block (mycnt);
+        // block r starts disp[r] elements (x extent for a derived type) into it
+        const Img mf = img_of(dt, total), mb = img_of(dt, (size_t)recvcounts[me]);
+        const int64_t unit = mf.t ? mf.t->extent : (int64_t)esz;
+        std::vector<char> full(mf.bytes);
+        int rc = img_load(mf, src, full.data());
         if (rc != MPI_SUCCESS) return rc;
+        const size_t mycnt = (size_t)recvcounts[me];
         if (op.commutative) {
             // commutative user op: the builtin schedules (recursive halving or
             // pairwise, same 32-bit gate) evaluated on host with the user's
             // function, reduce.cpp:917-1334
-            std::vector<char> all((size_t)p * total * esz);
-            if ((rc = c->tp->allgather(full.data(), total * esz, all.data())) != MPI_SUCCESS) return rc;
-            const int algo = reduce_scatter_algo(p, total, (int)esz, true);
+            std::vector<char> all((size_t)p * mf.bytes);
+            if ((rc = c->tp->allgather(full.data(), mf.bytes, all.data())) != MPI_SUCCESS) return rc;
+            const int gate_esz = mf.t ? (int)mf.t->size : (int)esz;
+            const int algo = reduce_scatter_algo(p, total, gate_esz, true);
             const int n = newrank_of(me, p);
             const RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
                                                        : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
-            const size_t mycnt = (size_t)recvcounts[me];
             std::vector<const char*> x((size_t)p);
-            for (int r = 0; r < p; ++r) x[(size_t)r] = all.data() + ((size_t)r * total + disp[me]) * esz;
-            std::vector<char> res(mycnt * esz);
-            eval_tree_host(t, x, res.data(), mycnt, dt, op);
-            return mycnt ? copy_any(recvbuf, res.data(), mycnt * esz) : MPI_SUCCESS;
+            for (int r = 0; r < p; ++r)
+                x[(size_t)r] = all.data() + (size_t)r * mf.bytes - mf.lo + (int64_t)disp[me] * unit;
+            std::vector<char> res(mb.bytes);
+            eval_tree_host(t, x, res.data() - mb.lo, mycnt, dt, op, mb);
+            return mycnt ? img_store(mb, mycnt, res.data() - mb.lo, recvbuf) : MPI_SUCCESS;
         }
         // non-commutative: recursive doubling (MPIR_Reduce_scatter_non_commutative,
         // reduce.cpp:1340-1630) -- for a power-of-two p each block is exactly the
         // recursive-doubling allreduce value; other p share its lower-first order
-        std::vector<char> res(total * esz);
-        rc = host_user_allreduce(c, full.data(), res.data(), total, dt, op);
-        if (rc == MPI_SUCCESS && recvcounts[me])
-            rc = copy_any(recvbuf, res.data() + disp[me] * esz, (size_t)recvcounts[me] * esz);
+        std::vector<char> res(mf.bytes);
+        rc = host_user_allreduce(c, full.data() - mf.lo, res.data() - mf.lo, total, dt, op);
+        if (rc == MPI_SUCCESS && mycnt)
+            rc = img_store(mb, mycnt, res.data() - mf.lo + (int64_t)disp[me] * unit, recvbuf);
         return rc;
     }
     int rc = ensure_device();
@@ -1448,21 +1513,14 @@ namespace {
 int host_user_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                      const OpRef& op, int root)
 {
-    const int p = c->size, me = c->rank, esz = type_size(dt);
-    const size_t bytes = count * (size_t)esz;
+    const int p = c->size, me = c->rank;
+    const Img m = img_of(dt, count);
+    const size_t bytes = m.bytes;
     std::vector<char> mine(bytes), all((size_t)p * bytes);
-    int rc = copy_any(mine.data(), sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, bytes);
+    int rc = img_load(m, sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, mine.data());
     if (rc == MPI_SUCCESS) rc = c->tp->allgather(mine.data(), bytes, all.data());
     if (rc != MPI_SUCCESS || me != root) return rc;
-    auto call = [&](const char* in, char* io) {
-        for (size_t off = 0; off < count;) {
-            size_t n = std::min(count - off, (size_t)0x7fffffff);
-            int len = (int)n;
-            MPI_Datatype d = dt;
-            op.user_fn(const_cast<char*>(in) + off * esz, io + off * esz, &len, &d);
-            off += n;
-        }
-    };
+    auto call = [&](const char* in, char* io) { img_call(op, dt, m, count, in - m.lo, io - m.lo); };
     const int lroot = op.commutative ? root : 0;
     auto buf = [&](int rel) { return all.data() + (size_t)((rel + lroot) % p) * bytes; };
     std::vector<char> tmp(bytes);
@@ -1479,7 +1537,7 @@ int host_user_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, 
             }
         }
     }
-    return copy_any(recvbuf, buf(0), bytes);
+    return img_store(m, count, buf(0) - m.lo, recvbuf);
 }
 
 }  // namespace
@@ -1510,21 +1568,14 @@ namespace {
 int host_user_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                    const OpRef& op, bool exclusive)
 {
-    const int p = c->size, me = c->rank, esz = type_size(dt);
-    const size_t bytes = count * (size_t)esz;
+    const int p = c->size, me = c->rank;
+    const Img m = img_of(dt, count);
+    const size_t bytes = m.bytes;
     std::vector<char> mine(bytes), all((size_t)p * bytes);
-    int rc = copy_any(mine.data(), sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, bytes);
+    int rc = img_load(m, sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, mine.data());
     if (rc == MPI_SUCCESS) rc = c->tp->allgather(mine.data(), bytes, all.data());
     if (rc != MPI_SUCCESS) return rc;
-    auto call = [&](const char* in, char* io) {
-        for (size_t off = 0; off < count;) {
-            size_t n = std::min(count - off, (size_t)0x7fffffff);
-            int len = (int)n;
-            MPI_Datatype d = dt;
-            op.user_fn(const_cast<char*>(in) + off * esz, io + off * esz, &len, &d);
-            off += n;
-        }
-    };
+    auto call = [&](const char* in, char* io) { img_call(op, dt, m, count, in - m.lo, io - m.lo); };
     std::vector<std::vector<char>> part((size_t)p), res((size_t)p);
     std::vector<bool> have((size_t)p, !exclusive);
     for (int r = 0; r < p; ++r) {
@@ -1551,7 +1602,7 @@ int host_user_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MP
         }
     }
     if (exclusive && !have[me]) return MPI_SUCCESS;     // rank 0: recvbuf undefined
-    return copy_any(recvbuf, res[me].data(), bytes);
+    return img_store(m, count, res[me].data() - m.lo, recvbuf);
 }
 
 int combine2(int opidx, Kind k, const char* inout_src, const char* in, char* out, size_t n, hipStream_t s)

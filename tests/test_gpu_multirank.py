@@ -36,6 +36,11 @@ fails = []
 def raw(a):
     return np.frombuffer(bytearray(a.tobytes()), dtype=a.dtype)
 
+def dzeros(*a, **k):
+    t = torch.zeros(*a, **k)
+    torch.cuda.synchronize()      # the library's streams do not order after torch's
+    return t
+
 def todev(a):
     t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
     if a.nbytes:
@@ -67,7 +72,7 @@ for i, (opn, dtn, count) in enumerate(ALLREDUCE):
     assert oracle.allreduce(op, dt, xs, exp) == 0
     for mode in ("dev", "inplace", "host"):
         if mode == "dev":
-            sb, rb = todev(xs[rank]), torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+            sb, rb = todev(xs[rank]), dzeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
             rc = L.MPI_Allreduce(sb.data_ptr(), rb.data_ptr(), count, dt, op, C.MPI_COMM_WORLD)
             got = fromdev(rb, xs[rank])
         elif mode == "inplace":
@@ -97,7 +102,7 @@ for i, (opn, dtn, per) in enumerate(RS):
     for mode in ("dev", "inplace"):
         if mode == "dev":
             sb = todev(xs[rank])
-            rb = torch.zeros(max(counts[rank] * xs[0].dtype.itemsize, 1), dtype=torch.uint8, device="cuda")
+            rb = dzeros(max(counts[rank] * xs[0].dtype.itemsize, 1), dtype=torch.uint8, device="cuda")
             rc = L.MPI_Reduce_scatter(sb.data_ptr(), rb.data_ptr(), cnt, dt, op, C.MPI_COMM_WORLD)
         else:
             rb = todev(xs[rank])
@@ -117,7 +122,7 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 5000), ("MPI_SUM
         exp = raw(np.zeros_like(xs[0]))
         assert oracle.reduce(op, dt, root, xs, exp) == 0
         sb = todev(xs[rank])
-        rb = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+        rb = dzeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
         rc = L.MPI_Reduce(sb.data_ptr(), rb.data_ptr(), count, dt, op, root, C.MPI_COMM_WORLD)
         if rc != 0:
             fails.append(f"reduce {opn} {count} root={root} rc={rc} {msx.last_error()}")
@@ -133,7 +138,7 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
         exp = [raw(np.zeros_like(xs[0])) for _ in range(p)]
         assert oracle.scan(op, dt, xs, exp, exclusive=excl) == 0
         sb = todev(xs[rank])
-        rb = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+        rb = dzeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
         fn = L.MPI_Exscan if excl else L.MPI_Scan
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         rc = fn(sb.data_ptr(), rb.data_ptr(), count, dt, op, C.MPI_COMM_WORLD)
@@ -142,7 +147,7 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
         elif not (excl and rank == 0):
             check(f"scan {opn} {dtn} excl={excl}", fromdev(rb, xs[rank]), exp[rank])
         # MPI_Iscan / MPI_Iexscan: same task order, completed in MPI_Wait
-        rb2 = torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+        rb2 = dzeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
         req = ctypes.c_int()
         fi = L.MPI_Iexscan if excl else L.MPI_Iscan
         rc = fi(ctypes.c_void_p(sb.data_ptr()), ctypes.c_void_p(rb2.data_ptr()), count, dt, op, C.MPI_COMM_WORLD,
@@ -168,9 +173,9 @@ counts_v = [1000 + 7 * k for k in range(p)]
 xs_v = inputs("MPI_BXOR", "MPI_INT", sum(counts_v), 6002)
 es_v = [raw(np.zeros(c, xs_v[0].dtype)) for c in counts_v]
 assert oracle.reduce_scatter(C.MPI_BXOR, C.MPI_INT, counts_v, xs_v, es_v) == 0
-d_r, o_r = todev(xr[rank]), torch.zeros(xr[rank].nbytes, dtype=torch.uint8, device="cuda")
-d_b, o_b = todev(xs_b[rank]), torch.zeros(per * 8, dtype=torch.uint8, device="cuda")
-d_v, o_v = todev(xs_v[rank]), torch.zeros(counts_v[rank] * 4, dtype=torch.uint8, device="cuda")
+d_r, o_r = todev(xr[rank]), dzeros(xr[rank].nbytes, dtype=torch.uint8, device="cuda")
+d_b, o_b = todev(xs_b[rank]), dzeros(per * 8, dtype=torch.uint8, device="cuda")
+d_v, o_v = todev(xs_v[rank]), dzeros(counts_v[rank] * 4, dtype=torch.uint8, device="cuda")
 reqs = (ctypes.c_int * 3)()
 cv = (ctypes.c_int * p)(*counts_v)
 rcs = [L.MPI_Ireduce(d_r.data_ptr(), o_r.data_ptr(), cnt, C.MPI_FLOAT, C.MPI_SUM, p - 1, C.MPI_COMM_WORLD,
@@ -197,7 +202,7 @@ else:
 xs = inputs("MPI_BAND", "MPI_UINT64_T", 1 << 18, 4000)
 exp = [raw(x.copy()) for x in xs]
 oracle.allreduce(C.MPI_BAND, C.MPI_UINT64_T, xs, exp)
-sb, rb = todev(xs[rank]), torch.zeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
+sb, rb = todev(xs[rank]), dzeros(xs[rank].nbytes, dtype=torch.uint8, device="cuda")
 req = ctypes.c_int()
 rc = L.MPI_Iallreduce(sb.data_ptr(), rb.data_ptr(), 1 << 18, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD,
                       ctypes.byref(req))
