@@ -875,11 +875,18 @@ struct Windows {
     char* out(int r) const { return base[(size_t)r] + C; }
 };
 
-int get_windows(Transport* tp, Windows* w)
+int get_windows(Transport* tp, Windows* w, bool rd_single = false)
 {
     w->C = chunk_bytes();
     w->Q = (w->C / (size_t)tp->size) & ~(size_t)255;
-    return tp->window(2 * w->C, w->base);
+    int rc = tp->window(2 * w->C, w->base);
+    if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
+        // the last recursive-doubling call left without its closing barrier:
+        // peers may still be reading their IN areas
+        rc = tp->barrier();
+        tp->window_open = false;
+    }
+    return rc;
 }
 
 int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
@@ -1246,8 +1253,16 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     const bool is_reduce = root >= 0;
     const int algo = is_reduce ? reduce_algo(p, count, (int)esz, true)
                                : allreduce_algo(p, count, (int)esz, true);
+    // A recursive-doubling (or binomial) call that fits half a sub-slot runs
+    // barrier-free at its end: it uses the IN half `rd_parity`, alternating per
+    // call.  Pushing into a peer's half P again (two calls later) happens only
+    // after this rank passed the previous call's barrier A, which that peer
+    // reached only after finishing its tree on half P.
+    const size_t Qh = ((chunk_bytes() / (size_t)p) & ~(size_t)255) / 2;
+    const bool rd_single = (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) &&
+                           count * esz <= (Qh & ~(size_t)(16 * esz - 1));
     Windows w;
-    if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
+    if ((rc = get_windows(tp, &w, rd_single)) != MPI_SUCCESS) return rc;
     const BufInfo bs = classify(src), bd = classify(dst);
     // elements per sub-slot, whole 16-element granules
     size_t qmax = w.Q / esz;
@@ -1270,6 +1285,52 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // recursive doubling -> all ranks evaluate their own lineage's tree;
         // binomial reduce -> only the root evaluates
         const RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
+        if (rd_single) {
+            const size_t half = (size_t)tp->rd_parity * Qh;
+            for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
+            const char* mine = nullptr;
+            rc = device_view(bs, src, 0, count * esz, stage, s, &mine);
+            Segs sg;                      // my own contribution is read in place
+            for (int r = 0; r < p; ++r)
+                if (r != me && (root < 0 || r == root)) sg.add(mine, w.sub(r, me) + half, count * esz);
+            subs[(size_t)me] = const_cast<char*>(mine);
+            if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
+            if (rc == MPI_SUCCESS) rc = tp->barrier();                              // A
+            if (rc == MPI_SUCCESS && want) {
+                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
+                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s);
+                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
+                if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce tree");
+            }
+            tp->rd_parity ^= 1;
+            tp->window_open = true;       // no barrier B (see above)
+            trace("allreduce: done (barrier-free) rc=%d", rc);
+            return rc;
+        }
+        if (rd_single) {
+            const size_t half = (size_t)tp->rd_parity * Qh;
+            for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
+            const char* mine = nullptr;
+            rc = device_view(bs, src, 0, count * esz, stage, s, &mine);
+            Segs sg;                      // my own contribution is read in place
+            for (int r = 0; r < p; ++r)
+                if (r != me && (root < 0 || r == root)) sg.add(mine, w.sub(r, me) + half, count * esz);
+            subs[(size_t)me] = const_cast<char*>(mine);
+            if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
+            if (rc == MPI_SUCCESS) rc = tp->barrier();                              // A
+            if (rc == MPI_SUCCESS && want) {
+                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
+                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s);
+                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
+                if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce tree");
+            }
+            tp->rd_parity ^= 1;
+            tp->window_open = true;       // no barrier B (see above)
+            trace("allreduce: done (barrier-free) rc=%d", rc);
+            return rc;
+        }
         for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += qmax) {
             const size_t len = std::min(qmax, count - o);
             const char* mine = nullptr;

@@ -26,6 +26,12 @@ public:
     virtual ~Transport() = default;
     int rank = 0;
     int size = 1;
+    // Single-chunk recursive-doubling calls skip their closing barrier and
+    // alternate between two halves of the IN sub-slots (rd_parity); a later
+    // window user of another kind barriers first while window_open is set.
+    // Every rank runs the same collective sequence, so these agree everywhere.
+    bool window_open = false;
+    int rd_parity = 0;
     // lock-step host collectives over the bootstrap hub (all ranks, same n)
     virtual int allgather(const void* mine, size_t n, void* all) = 0;
     virtual int barrier() = 0;
