@@ -86,10 +86,11 @@ void not_initialized_exit(const char* fn)
     exit(1);
 }
 
+// Entry of every MPI call: MpiaIsInitializedOrExit, then an API range that
+// spans the rest of the call (ApiRange, msx_runtime.h).
 #define MSX_REQUIRE_INIT(fn)                                                  \
-    do {                                                                      \
-        if (!is_initialized() || is_finalized()) not_initialized_exit(fn);    \
-    } while (0)
+    if (!is_initialized() || is_finalized()) not_initialized_exit(fn);        \
+    ApiRange msx_api_range_(fn)
 
 // MPIR_Err_return_comm (mpid/error.cpp:85-134): default handler is the one on
 // MPI_COMM_WORLD; ERRORS_ARE_FATAL aborts the job.
@@ -225,6 +226,8 @@ void api_require_init(const char* fn)
 {
     if (!is_initialized() || is_finalized()) not_initialized_exit(fn);
 }
+// (datatype entry points are not traced: no device work of their own except
+// MPI_Pack / MPI_Unpack, which open their own range)
 int api_err_return(const char* fn, int code) { return err_return(nullptr, fn, code); }
 int api_comm_valid(MPI_Comm comm)
 {

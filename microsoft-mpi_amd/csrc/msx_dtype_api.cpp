@@ -543,6 +543,7 @@ MSX_EXPORT int MPI_Pack(const void* inbuf, int incount, MPI_Datatype datatype, v
                         int* position, MPI_Comm comm)
 {
     api_require_init("MPI_Pack");
+    ApiRange range("MPI_Pack");
     int rc = api_comm_valid(comm);
     Dtype* t = nullptr;
     if (rc == MPI_SUCCESS) rc = v_typed(inbuf, incount, datatype, &t);     // inbuf may be MPI_BOTTOM
@@ -566,6 +567,7 @@ MSX_EXPORT int MPI_Unpack(const void* inbuf, int insize, int* position, void* ou
                           MPI_Datatype datatype, MPI_Comm comm)
 {
     api_require_init("MPI_Unpack");
+    ApiRange range("MPI_Unpack");
     int rc = api_comm_valid(comm);                                       // mpi_pack.cpp:570-591
     Dtype* t = nullptr;
     if (rc == MPI_SUCCESS) rc = v_typed(outbuf, outcount, datatype, &t);

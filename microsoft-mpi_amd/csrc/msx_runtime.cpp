@@ -10,6 +10,7 @@
 #include "msx_runtime.h"
 
 #include <atomic>
+#include <dlfcn.h>
 #include <mutex>
 #include <stdarg.h>
 #include <stdio.h>
@@ -267,6 +268,40 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
         if (e == hipSuccess) e = e2;
     }
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "host-staged combine");
+}
+
+namespace {
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+    bool ok = false;
+};
+const Roctx& roctx()
+{
+    static const Roctx r = [] {
+        Roctx x;
+        const char* e = getenv("MSX_TRACE_RANGES");
+        if (!e || atoi(e) == 0) return x;
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return x;
+        x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+        x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+        x.ok = x.push && x.pop;
+        return x;
+    }();
+    return r;
+}
+}  // namespace
+
+ApiRange::ApiRange(const char* fn) : on_(roctx().ok)
+{
+    if (on_) roctx().push(fn);
+}
+
+ApiRange::~ApiRange()
+{
+    if (on_) roctx().pop();
 }
 
 }  // namespace msx

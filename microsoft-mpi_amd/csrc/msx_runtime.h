@@ -54,4 +54,18 @@ int reduce_local_device(int opidx, Kind k, const void* in, void* inout, size_t c
 // hipError_t -> MPI error class with the HIP error text recorded.
 int hip_fail(hipError_t e, const char* what);
 
+// API entry/exit ranges for `rocprofv3 --marker-trace`: the counterpart of the
+// reference's ETW TraceEnter_/TraceLeave_ wrappers around every MPI call
+// (api/mpi_reduce.cpp:58,249,271,...).  Off unless MSX_TRACE_RANGES=1; roctx
+// is opened with dlopen, so the library has no link-time dependency on it.
+class ApiRange {
+public:
+    explicit ApiRange(const char* fn);
+    ~ApiRange();
+    ApiRange(const ApiRange&) = delete;
+    ApiRange& operator=(const ApiRange&) = delete;
+private:
+    bool on_;
+};
+
 }  // namespace msx
