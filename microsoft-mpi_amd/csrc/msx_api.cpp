@@ -566,7 +566,7 @@ int scan_common(const char* fn, const void* sendbuf, void* recvbuf, int count, M
         const size_t n = (size_t)count;
         rc = request_start_generic(c, [=] {
             return n ? coll_scan(c, sendbuf, recvbuf, n, datatype, r, exclusive) : MPI_SUCCESS;
-        }, request);
+        }, request, datatype);
     } else if (rc == MPI_SUCCESS && count > 0) {
         rc = coll_scan(c, sendbuf, recvbuf, (size_t)count, datatype, r, exclusive);
     }
@@ -653,7 +653,7 @@ MSX_EXPORT int MPI_Ireduce(const void* sendbuf, void* recvbuf, int count, MPI_Da
         const size_t n = (size_t)count;
         rc = request_start_generic(c, [=] {
             return n ? coll_reduce(c, sendbuf, recvbuf, n, datatype, r, root) : MPI_SUCCESS;
-        }, request);
+        }, request, datatype);
     }
     return err_return(c, "MPI_Ireduce", rc);
 }
@@ -673,7 +673,7 @@ MSX_EXPORT int MPI_Ireduce_scatter(const void* sendbuf, void* recvbuf, const int
         std::vector<int> counts(recvcounts, recvcounts + c->size);
         rc = request_start_generic(c, [=] {
             return coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
-        }, request);
+        }, request, datatype);
     }
     return err_return(c, "MPI_Ireduce_scatter", rc);
 }
@@ -697,7 +697,7 @@ MSX_EXPORT int MPI_Ireduce_scatter_block(const void* sendbuf, void* recvbuf, int
     if (rc == MPI_SUCCESS) {
         rc = request_start_generic(c, [=] {
             return coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
-        }, request);
+        }, request, datatype);
     }
     return err_return(c, "MPI_Ireduce_scatter_block", rc);
 }
@@ -896,6 +896,7 @@ int rma_issue(RmaWin* w, RmaKind kind, int target, MPI_Aint disp, int opidx, con
         l.result_user = result;
         l.result_dt = rdt;
         l.result_count = rcount;
+        if (l.tmp_result) dtype_add_ref(rdt);      // released by rma_local_complete
     }
     if (rc != MPI_SUCCESS) {
         rma_local_complete(l);

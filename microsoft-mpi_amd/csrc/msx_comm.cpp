@@ -292,8 +292,17 @@ void fill_status(MPI_Status* st, int rc)
 
 }  // namespace
 
-int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req)
+int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req, MPI_Datatype hold)
 {
+    if (dtype_is_derived(hold)) {
+        dtype_add_ref(hold);
+        body = [body, hold]() {
+            const int rc = body();
+            MPI_Datatype h = hold;
+            dtype_free(&h);
+            return rc;
+        };
+    }
     Request* r;
     if (c->size > 1) {
         // The engine worker runs it behind every earlier collective; the
@@ -316,7 +325,7 @@ int request_start_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t 
 {
     return request_start_generic(
         c, [=] { return count ? coll_allreduce(c, sendbuf, recvbuf, count, dt, op) : MPI_SUCCESS; },
-        req);
+        req, dt);
 }
 
 int request_test(MPI_Request* req, int* flag, MPI_Status* st)

@@ -61,8 +61,11 @@ struct Request;
 int request_start_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count,
                             MPI_Datatype dt, const OpRef& op, MPI_Request* req);
 // Start `body` as a request: on the engine worker when c->size > 1 (true
-// overlap with the caller), inline otherwise.
-int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req);
+// overlap with the caller), inline otherwise.  A derived datatype named by
+// `hold` keeps a reference until the request completes (MPI_Type_free of a
+// type in use by a pending operation defers its destruction).
+int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req,
+                          MPI_Datatype hold = MPI_DATATYPE_NULL);
 int request_wait(MPI_Request* req, MPI_Status* st);
 int request_test(MPI_Request* req, int* flag, MPI_Status* st);
 

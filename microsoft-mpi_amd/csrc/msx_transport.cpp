@@ -2037,6 +2037,8 @@ int rma_local_complete(RmaLocal& l)
         rc = t ? dt_unpack_any(t, l.result_count, l.tmp_result, l.result_user) : MPI_ERR_TYPE;
         (void)hipFree(l.tmp_result);
         l.tmp_result = nullptr;
+        MPI_Datatype h = l.result_dt;
+        if (dtype_is_derived(h)) dtype_free(&h);     // the reference taken at issue
     }
     if (l.tmp_origin) {
         (void)hipFree(l.tmp_origin);

@@ -311,3 +311,28 @@ def test_reduce_local_user_op_derived_type_device_buffers(L):
     assert seen == [(4, h)]
     assert L.MPI_Op_free(ctypes.byref(op)) == 0
     free_all(L, keep)
+
+
+def test_type_freed_while_nonblocking_op_pending(L):
+    """MPI_Type_free of a derived type used by a pending MPI_Iallreduce (user
+    op, one-rank communicator: the non-contiguous local copy) only marks it:
+    the request keeps a reference until it completes."""
+    from test_dtype_cpu import make_typed_sub_op
+    r = ("vector", 4, 2, 3, ("basic", C.MPI_INT))
+    keep = []
+    h = _commit(L, r, keep)
+    t = {"map": build_oracle(r)}
+    op, cb, seen = make_typed_sub_op(L, t)
+    a = torch.arange(64, dtype=torch.int32, device="cuda")
+    b = torch.full((64,), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    req = c_int()
+    assert L.MPI_Iallreduce(a.data_ptr(), b.data_ptr(), 2, h, op.value, C.MPI_COMM_WORLD, ctypes.byref(req)) == 0
+    x = c_int(h)
+    assert L.MPI_Type_free(ctypes.byref(x)) == 0            # user frees it while pending
+    assert L.MPI_Wait(ctypes.byref(req), None) == 0, msx.last_error()
+    idx = [i * t["map"].extent // 4 + d // 4 for i in range(2) for d, _ in t["map"].typemap]
+    exp = np.full(64, -1, np.int32)
+    exp[idx] = np.arange(64, dtype=np.int32)[idx]
+    assert b.cpu().numpy().tolist() == exp.tolist()
+    assert L.MPI_Op_free(ctypes.byref(op)) == 0
