@@ -234,7 +234,8 @@ def _free_port():
 
 
 @pytest.mark.parametrize("p,chunk,transport", [(2, None, None), (3, 65536, None), (4, 1 << 20, None),
-                                               (5, None, None), (3, 65536, "rccl")])
+                                               (5, None, None), (3, 65536, "rccl"),
+                                               (8, None, None), (7, 1 << 20, None)])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
