@@ -6,6 +6,8 @@ take the headline local-reduce line down with it).
   c3  MPI_Allreduce      MPI_SUM  MPI_FLOAT     1 GiB per rank
   c4  MPI_Reduce_scatter MPI_MAX  MPI_DOUBLE    4 GiB sendbuf per rank, recvcount = total/p
   c5  MPI_Iallreduce     MPI_BAND MPI_UINT64_T  512 MiB, overlapped with a host compute loop
+  + the §8f neighbours: MPI_Reduce (root 0, 1 GiB), MPI_Scan (64 MiB), one-sided
+    MPI_Accumulate + MPI_Win_fence (256 MiB into the next rank's window)
 
 Each rank is an MPI process of libmsmpi_mi355x.so (MSX_SIZE/MSX_RANK/MSX_DEVICE
 set by the parent).  Inputs are integer-valued patterns whose reductions are
@@ -208,6 +210,92 @@ def main(out_path, scale):
             "busbw_GB_s": round(S / t_comm / 1e9 * 2 * (p - 1) / p, 2),
             "overlap_efficiency": round((t_comm + t_host - t_total) / min(t_comm, t_host), 3),
             "correct": bool(torch.equal(recv, exp))}
+    del send, recv, exp
+    torch.cuda.empty_cache()
+
+    # ---- §8f neighbours at the same measurement bar -------------------------
+    def timed(fn, reps=3):
+        ts = []
+        for _ in range(reps + 1):
+            barrier()
+            t0 = time.perf_counter()
+            rc = fn()
+            ts.append(time.perf_counter() - t0)
+            if rc:
+                return None, rc
+        return sorted(ts[1:])[len(ts[1:]) // 2], 0
+
+    # MPI_Reduce SUM fp32 at root 0 (Rabenseifner reduce-scatter + gather),
+    # 1 GiB per rank like c3
+    n = int((256 << 20) * scale)
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    send = (((i * 5 + rank * 3) % 13) - 6).to(torch.float32)
+    exp = torch.zeros(n, device=dev, dtype=torch.float32)
+    for r in range(p):
+        exp += (((i * 5 + r * 3) % 13) - 6).to(torch.float32)
+    del i
+    recv = torch.zeros_like(send)
+    torch.cuda.synchronize()
+    t, rc = timed(lambda: L.MPI_Reduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, 0,
+                                       C.MPI_COMM_WORLD))
+    if rc:
+        res["reduce_error"] = f"rc={rc} {msx.last_error()}"
+    else:
+        S = n * 4
+        res["reduce_sum_f32_root0"] = {"bytes_per_rank": S, "seconds": round(t, 5),
+                                       "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 2),
+                                       "correct": bool(torch.equal(recv, exp)) if rank == 0 else None}
+    # MPI_Scan SUM fp32, 64 MiB per rank (recursive-doubling task order)
+    m = int((16 << 20) * max(scale, 1.0 / 16))
+    send2 = send[:m].clone()
+    pre = torch.zeros(m, device=dev, dtype=torch.float32)
+    i = torch.arange(m, device=dev, dtype=torch.int64)
+    for r in range(rank + 1):
+        pre += (((i * 5 + r * 3) % 13) - 6).to(torch.float32)
+    del i
+    out = torch.zeros_like(send2)
+    torch.cuda.synchronize()
+    t, rc = timed(lambda: L.MPI_Scan(send2.data_ptr(), out.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM,
+                                     C.MPI_COMM_WORLD))
+    if rc:
+        res["scan_error"] = f"rc={rc} {msx.last_error()}"
+    else:
+        res["scan_sum_f32"] = {"bytes_per_rank": m * 4, "seconds": round(t, 5),
+                               "GB_s_per_rank": round(m * 4 / t / 1e9, 2), "correct": bool(torch.equal(out, pre))}
+    del send, recv, exp, send2, pre, out
+    torch.cuda.empty_cache()
+
+    # one-sided MPI_Accumulate SUM fp32: every rank adds 256 MiB into the next
+    # rank's device window; a fence closes the epoch (target-side application)
+    n = int((64 << 20) * max(scale, 1.0 / 16))
+    base = torch.full((n,), 1.0, device=dev)
+    contrib = torch.full((n,), float(rank + 1), device=dev)
+    torch.cuda.synchronize()
+    win = ctypes.c_int()
+    rc = L.MPI_Win_create(base.data_ptr(), n * 4, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(win))
+    if not rc:
+        rc = L.MPI_Win_fence(0, win)
+    reps = 3
+    if not rc:
+        tgt = (rank + 1) % p
+        ts = []
+        for _ in range(reps + 1):
+            barrier()
+            t0 = time.perf_counter()
+            rc = L.MPI_Accumulate(contrib.data_ptr(), n, C.MPI_FLOAT, tgt, 0, n, C.MPI_FLOAT, C.MPI_SUM, win) or \
+                L.MPI_Win_fence(0, win)
+            ts.append(time.perf_counter() - t0)
+            if rc:
+                break
+    if rc:
+        res["rma_error"] = f"rc={rc} {msx.last_error()}"
+    else:
+        t = sorted(ts[1:])[len(ts[1:]) // 2]
+        src_rank = (rank - 1) % p
+        res["rma_accumulate_sum_f32_fence"] = {
+            "bytes_per_rank": n * 4, "seconds": round(t, 5), "GB_s_per_rank": round(n * 4 / t / 1e9, 2),
+            "correct": bool(torch.all(base == 1.0 + (reps + 1) * (src_rank + 1)).item())}
+        L.MPI_Win_free(ctypes.byref(win))
     barrier()
     L.msx_engine_transport.restype = ctypes.c_char_p
     res["transport_used"] = L.msx_engine_transport().decode()
