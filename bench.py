@@ -440,6 +440,41 @@ def pack_roofline(L, C, torch, dev, stream):
     return out
 
 
+def rma_self_roofline(L, C, torch, dev, n):
+    """One-sided MPI_Accumulate (MPI_SUM, fp32) into this rank's own device
+    window: the reference applies a self-targeted accumulate at the call
+    (win.cpp:1570-1590, MPIDI_Win_local_accumulate), here through the combine
+    kernels.  Wall clock per blocking call (launch + sync included), 12 B per
+    element of HBM traffic like the local combine."""
+    import ctypes
+    win_buf = torch.zeros(n, device=dev)
+    origin = torch.rand(n, device=dev)
+    torch.cuda.synchronize()
+    win = ctypes.c_int()
+    if L.MPI_Win_create(win_buf.data_ptr(), n * 4, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(win)):
+        return {"error": "MPI_Win_create failed"}
+    acc = lambda: L.MPI_Accumulate(origin.data_ptr(), n, C.MPI_FLOAT, 0, 0, n, C.MPI_FLOAT, C.MPI_SUM, win)
+    for _ in range(3):
+        acc()
+    reps, t0 = 20, time.perf_counter()
+    for _ in range(reps):
+        rc = acc()
+        if rc:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    correct = None
+    if not rc:
+        # 23 accumulations of the same origin into zeros: exact check on a sample
+        ref = torch.zeros(4096, device=dev)
+        for _ in range(23):
+            ref += origin[:4096]
+        correct = bool(torch.equal(win_buf[:4096], ref))
+    L.MPI_Win_free(ctypes.byref(win))
+    gbs = 12 * n / dt / 1e9
+    return {"bytes_per_call": 12 * n, "ms_per_call": round(dt * 1e3, 3), "GB_s": round(gbs, 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "correct": correct}
+
+
 def main():
     args = parse()
     import torch
@@ -590,6 +625,9 @@ def main():
     pack = None
     if rank == 0 and world == 1 and not args.no_pack:
         pack = pack_roofline(L, C, torch, dev, stream)
+    rma = None
+    if rank == 0 and world == 1 and not args.no_per_op:
+        rma = rma_self_roofline(L, C, torch, dev, n)
 
     if rank == 0:
         total_bytes = world * args.steps * n * BYTES_PER_ELEM
@@ -635,6 +673,8 @@ def main():
             out["per_op_roofline_hbm"] = per_op
         if pack is not None:
             out["datatype_pack_roofline_hbm"] = pack
+        if rma is not None:
+            out["rma_self_accumulate_f32"] = rma
         if sweep:
             out["variant_sweep_GB_s"] = sweep
         if world == 1:

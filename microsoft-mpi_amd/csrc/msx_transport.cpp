@@ -1762,8 +1762,12 @@ int rma_combine(const RmaDesc& d, const char* payload, char* taddr, hipStream_t 
     if (d.opidx == O_REPLACE) return copy_async(taddr, payload, bytes, s);
     if (op_check_dtype(d.opidx, d.dt) != MPI_SUCCESS) return MPI_SUCCESS;
     const Kind k = type_info(d.dt)->kind;
-    if (classify(taddr).place == Place::Device && classify(payload).place == Place::Device)
-        return combine2(d.opidx, k, taddr, payload, taddr, (size_t)d.count, s);
+    if (classify(taddr).place == Place::Device && classify(payload).place == Place::Device) {
+        // the streaming combine in place on the target (payloads written by
+        // peers sit in uncached window memory, so plain loads see them)
+        const hipError_t e = launch_combine(d.opidx, k, payload, taddr, (size_t)d.count, s, LaunchCfg());
+        return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "rma combine");
+    }
     int rc = sync_stream(s, "rma");
     return rc == MPI_SUCCESS ? reduce_local_any(d.opidx, k, payload, taddr, (size_t)d.count) : rc;
 }
