@@ -159,21 +159,6 @@ void destroy(Dtype* t)
     delete t;
 }
 
-// Expand a compact run list into `runs`.
-int materialise(Dtype* t)
-{
-    if (t->rn == 0) return MPI_SUCCESS;
-    if (t->rn > kMaxRuns) {
-        set_error("datatype type map exceeds %lld contiguous pieces", (long long)kMaxRuns);
-        return MPI_ERR_NO_MEM;
-    }
-    t->runs.clear();
-    t->runs.reserve((size_t)t->rn);
-    for (int64_t k = 0; k < t->rn; ++k) push_run(t->runs, t->rfirst + k * t->rstride, t->rlen);
-    t->rn = 0;
-    return MPI_SUCCESS;
-}
-
 // The single run of a one-run type (either form).
 bool single_run(const Dtype* t, DtRun* r)
 {
@@ -191,23 +176,34 @@ void copy_layout(Dtype* t, const Dtype* o)
     t->rstride = o->rstride;
 }
 
-// Append `nrep` copies of old's runs, copy r at disp0 + r*ext.
-int append_copies(std::vector<DtRun>& out, Dtype* old, int64_t disp0, int64_t nrep, int64_t ext)
+// Append `nrep` copies of old's runs, copy r at disp0 + r*ext.  A compact old
+// type is expanded into a local list: committed types are never modified (a
+// pack may be reading them on another thread).
+int append_copies(std::vector<DtRun>& out, const Dtype* old, int64_t disp0, int64_t nrep, int64_t ext)
 {
-    int rc = materialise(old);
-    if (rc != MPI_SUCCESS) return rc;
-    if (nrep <= 0 || old->runs.empty()) return MPI_SUCCESS;
+    std::vector<DtRun> expanded;
+    const std::vector<DtRun>* runs = &old->runs;
+    if (old->rn) {
+        if (old->rn > kMaxRuns) {
+            set_error("datatype type map exceeds %lld contiguous pieces", (long long)kMaxRuns);
+            return MPI_ERR_NO_MEM;
+        }
+        expanded.reserve((size_t)old->rn);
+        for (int64_t k = 0; k < old->rn; ++k) push_run(expanded, old->rfirst + k * old->rstride, old->rlen);
+        runs = &expanded;
+    }
+    if (nrep <= 0 || runs->empty()) return MPI_SUCCESS;
     // one contiguous run spanning exactly the extent: the copies merge into one
-    if (old->runs.size() == 1 && old->runs[0].len == ext && ext > 0) {
-        push_run(out, disp0 + old->runs[0].disp, nrep * ext);
+    if (runs->size() == 1 && (*runs)[0].len == ext && ext > 0) {
+        push_run(out, disp0 + (*runs)[0].disp, nrep * ext);
         return MPI_SUCCESS;
     }
-    if ((int64_t)out.size() + nrep * (int64_t)old->runs.size() > kMaxRuns) {
+    if ((int64_t)out.size() + nrep * (int64_t)runs->size() > kMaxRuns) {
         set_error("datatype type map exceeds %lld contiguous pieces", (long long)kMaxRuns);
         return MPI_ERR_NO_MEM;
     }
     for (int64_t r = 0; r < nrep; ++r)
-        for (const DtRun& x : old->runs) push_run(out, disp0 + r * ext + x.disp, x.len);
+        for (const DtRun& x : *runs) push_run(out, disp0 + r * ext + x.disp, x.len);
     return MPI_SUCCESS;
 }
 
@@ -476,7 +472,7 @@ int dtype_struct(int count, const int* blens, const MPI_Aint* disps, const MPI_D
         for (i = 0; i < count; ++i) {
             if (blens[i] == 0) continue;
             const bool bi = is_builtin_h(types[i]);
-            Dtype* o = olds[i];
+            const Dtype* o = olds[i];
             const bool marker = (types[i] == MPI_LB || types[i] == MPI_UB);
             int64_t l, u, tl, tu, esz;
             MPI_Datatype et;
