@@ -1691,8 +1691,10 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
     Windows w;
     if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
-    // partials staged in two alternating halves of IN(me): a peer may still be
-    // reading step i's partial while step i+1's is staged
+    // Each step's partial is PUSHED into the consumer's IN window (an xGMI
+    // remote write) and combined there from local HBM; two alternating halves
+    // of IN: a peer writes step i+2's half only after the barrier of step i+1,
+    // which this rank reaches after finishing its reads of step i.
     size_t ce = w.C / 2 / esz;
     ce -= ce % 16;
     if (ce == 0) { set_error("scan: window too small"); return MPI_ERR_INTERN; }
@@ -1708,14 +1710,17 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
         const int dst = me ^ mask;
         const bool last = (mask << 1) >= p;
         const bool use = dst < p && !(last && me < dst);     // this rank consumes dst's partial
+        const bool feeds = dst < p && !(last && dst < me);   // dst consumes this rank's partial
         for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce, slot ^= 1) {
             const size_t len = std::min(ce, count - o);
-            char* stage = w.in(me) + (size_t)slot * (w.C / 2);
-            rc = copy_async(stage, partial + o * esz, len * esz, s);       // partial at step start
-            if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan stage");
+            if (feeds) {
+                char* stage = w.in(dst) + (size_t)slot * (w.C / 2);
+                rc = copy_async(stage, partial + o * esz, len * esz, s);   // partial at step start
+                if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan push");
+            }
             if (rc == MPI_SUCCESS) rc = tp->barrier();
             if (rc != MPI_SUCCESS || !use) continue;
-            const char* tmp = w.in(dst) + (size_t)slot * (w.C / 2);
+            const char* tmp = w.in(me) + (size_t)slot * (w.C / 2);
             char* pp = partial + o * esz;
             char* rr = res + o * esz;
             if (me > dst) {
