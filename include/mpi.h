@@ -401,6 +401,21 @@ MPI_METHOD MPI_Unpack(const void* inbuf, int insize, int* position, void* outbuf
                       MPI_Datatype datatype, MPI_Comm comm);
 MPI_METHOD MPI_Pack_size(int incount, MPI_Datatype datatype, MPI_Comm comm, int* size);
 
+/* ---- Fortran handle conversion (mpi.h:6816-6848): handles are already ints - */
+#define MPI_Comm_c2f(comm)         (MPI_Fint)(comm)
+#define MPI_Comm_f2c(comm)         (MPI_Comm)(comm)
+#define MPI_Type_c2f(datatype)     (MPI_Fint)(datatype)
+#define MPI_Type_f2c(datatype)     (MPI_Datatype)(datatype)
+#define MPI_Op_c2f(op)             (MPI_Fint)(op)
+#define MPI_Op_f2c(op)             (MPI_Op)(op)
+#define MPI_Request_c2f(request)   (MPI_Fint)(request)
+#define MPI_Request_f2c(request)   (MPI_Request)(request)
+#define MPI_Win_c2f(win)           (MPI_Fint)(win)
+#define MPI_Win_f2c(win)           (MPI_Win)(win)
+/* The Fortran bindings (mpif.h, include/mpif.h) are exported by the library
+   as mpi_<name>_ with the MPI_<NAME>, mpi_<name>, mpi_<name>__ and PMPI_ aliases
+   (microsoft-mpi_amd/csrc/msx_fortran.cpp). */
+
 /* ---- profiling interface aliases (msmpi.def:101-102,422-423,478-483,...) -- */
 MPI_METHOD PMPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
                              MPI_Datatype datatype, MPI_Op op);

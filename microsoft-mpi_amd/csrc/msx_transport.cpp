@@ -1308,29 +1308,6 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             trace("allreduce: done (barrier-free) rc=%d", rc);
             return rc;
         }
-        if (rd_single) {
-            const size_t half = (size_t)tp->rd_parity * Qh;
-            for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
-            const char* mine = nullptr;
-            rc = device_view(bs, src, 0, count * esz, stage, s, &mine);
-            Segs sg;                      // my own contribution is read in place
-            for (int r = 0; r < p; ++r)
-                if (r != me && (root < 0 || r == root)) sg.add(mine, w.sub(r, me) + half, count * esz);
-            subs[(size_t)me] = const_cast<char*>(mine);
-            if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
-            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
-            if (rc == MPI_SUCCESS) rc = tp->barrier();                              // A
-            if (rc == MPI_SUCCESS && want) {
-                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
-                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s);
-                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
-                if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce tree");
-            }
-            tp->rd_parity ^= 1;
-            tp->window_open = true;       // no barrier B (see above)
-            trace("allreduce: done (barrier-free) rc=%d", rc);
-            return rc;
-        }
         for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += qmax) {
             const size_t len = std::min(qmax, count - o);
             const char* mine = nullptr;
