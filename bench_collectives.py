@@ -66,6 +66,20 @@ def main(out_path, scale):
     del i
     torch.cuda.synchronize()
     log("c3 data ready")
+    # measured link roofline: every rank writes into all peers' windows at once
+    # (the scatter step's pattern); busBW is also reported against it
+    xgmi_meas = None
+    if p > 1 and res["transport_requested"] == "ipc":
+        sec, used = ctypes.c_double(), ctypes.c_int64()
+        rc = L.msx_peer_write_bandwidth(max(1 << 20, int((64 << 20) * scale)), 5, ctypes.byref(sec),
+                                        ctypes.byref(used))
+        if rc == 0 and sec.value > 0:
+            xgmi_meas = (p - 1) * used.value / sec.value / 1e9
+            res["peer_write_probe"] = {"bytes_per_peer": used.value, "seconds": round(sec.value, 6),
+                                       "outbound_GB_s_per_gpu": round(xgmi_meas, 1)}
+        else:
+            res["peer_write_probe"] = {"error": f"rc={rc} {msx.last_error()}"}
+        log(f"peer write probe {res['peer_write_probe']}")
     times = []
     stats = (ctypes.c_double * 7)()
     L.msx_engine_stats(stats, 7, 1)                 # reset the phase timers
@@ -85,6 +99,8 @@ def main(out_path, scale):
             "bytes_per_rank": S, "seconds": round(t, 5), "algbw_GB_s": round(S / t / 1e9, 2),
             "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 2),
             "busbw_frac_xgmi": round(S / t / 1e9 * 2 * (p - 1) / p / XGMI, 3),
+            "busbw_frac_measured_links": (round(S / t / 1e9 * 2 * (p - 1) / p / xgmi_meas, 3)
+                                          if xgmi_meas else None),
             "correct": bool(torch.equal(recv, exp))}
         L.msx_engine_stats(stats, 7, 1)
         calls = max(stats[6], 1.0)
@@ -148,6 +164,8 @@ def main(out_path, scale):
         S = tot * 8
         res["c4_reduce_scatter_max_f64"] = {
             "bytes_per_rank": S, "seconds": round(t, 5), "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 2),
+            "busbw_frac_xgmi": round(S / t / 1e9 * (p - 1) / p / XGMI, 3),
+            "busbw_frac_measured_links": (round(S / t / 1e9 * (p - 1) / p / xgmi_meas, 3) if xgmi_meas else None),
             "correct": bool(torch.equal(recv, exp))}
     del send, recv, exp
     torch.cuda.empty_cache()
@@ -208,6 +226,8 @@ def main(out_path, scale):
             "bytes_per_rank": S, "t_comm_s": round(t_comm, 5), "t_host_s": round(t_host, 5),
             "t_overlapped_s": round(t_total, 5),
             "busbw_GB_s": round(S / t_comm / 1e9 * 2 * (p - 1) / p, 2),
+            "busbw_frac_measured_links": (round(S / t_comm / 1e9 * 2 * (p - 1) / p / xgmi_meas, 3)
+                                          if xgmi_meas else None),
             "overlap_efficiency": round((t_comm + t_host - t_total) / min(t_comm, t_host), 3),
             "correct": bool(torch.equal(recv, exp))}
     del send, recv, exp

@@ -49,6 +49,12 @@ const char* msx_engine_transport(void);
  * out[0] stage+scatter, [1] collect wait + barrier A, [2] reduce + push,
  * [3] barrier B, [4] final collect, [5] chunks, [6] calls; returns 7 */
 int msx_engine_stats(double* out, int n, int reset);
+/* link roofline probe over MPI_COMM_WORLD (collective): every rank writes
+ * bytes_per_peer (capped at the window sub-slot) into each peer's window at
+ * once, reps timed repetitions; *seconds = median time of one all-peer write
+ * of *bytes_used per peer.  Per-GPU outbound bandwidth =
+ * (size-1) * *bytes_used / *seconds. */
+int msx_peer_write_bandwidth(int64_t bytes_per_peer, int reps, double* seconds, int64_t* bytes_used);
 /* text of the last error raised on the calling thread ("" if none) */
 const char* msx_last_error(void);
 

@@ -1145,6 +1145,13 @@ MSX_EXPORT int msx_engine_stats(double* out, int n, int reset)
     if (!out || n < 0) return -1;
     return engine_stats(out, n, reset);
 }
+MSX_EXPORT int msx_peer_write_bandwidth(int64_t bytes_per_peer, int reps, double* seconds, int64_t* bytes_used)
+{
+    MSX_REQUIRE_INIT("msx_peer_write_bandwidth");
+    if (!seconds || !bytes_used || bytes_per_peer <= 0 || reps <= 0) return MPI_ERR_ARG;
+    Comm* c = world();
+    return engine_peer_write_probe(c, (size_t)bytes_per_peer, reps, seconds, bytes_used);
+}
 MSX_EXPORT int msx_device_count(void) { return device_count_noinit(); }
 MSX_EXPORT const char* msx_last_error(void) { return last_error(); }
 

@@ -47,6 +47,8 @@ int transport_create(int rank, int size, Transport** out);
 // window-allreduce phase timers (seconds): stage+scatter, collect wait+barrier A,
 // reduce+push, barrier B, last collect, chunks, calls; returns 7
 int engine_stats(double* out, int n, int reset);
+// all-peer remote-write bandwidth probe (collective over c)
+int engine_peer_write_probe(Comm* c, size_t bytes, int reps, double* seconds, int64_t* used);
 // data plane the engine uses for `tp`: "rccl", "ipc" or "self" (size 1)
 const char* engine_transport_name(Transport* tp);
 void transport_destroy(Transport* t);
