@@ -657,6 +657,28 @@ int sync_stream(hipStream_t s, const char* what)
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
 }
 
+// Per-workgroup system-scope acquire/release in the engine's kernels (k_tree,
+// k_copy_segs).  Every byte that crosses GPUs lands in a window, and windows
+// are UNCACHED allocations: the kernel driver maps such a buffer MTYPE_UC on
+// the owner and on every peer that imports it, so neither the writer's nor
+// the reader's L2 ever holds a line of it, and the end-of-kernel store
+// completion (awaited by hipStreamSynchronize before the host barrier) is all
+// the ordering a reader behind that barrier needs.  The fences only matter for
+// cached windows (MSX_WINDOW_CACHED=1), and there they are kept.  They are not
+// free: each one writes back / invalidates the whole XCD L2 once per
+// workgroup, which halved the collectives' throughput (p = 2 rehearsal:
+// reduce_scatter 4.17 -> 2.17 ms, allreduce 64 MiB 511 -> 178 us).
+// MSX_KERNEL_SYS_FENCE=0/1 overrides the choice.
+bool sys_fences()
+{
+    static const bool on = [] {
+        if (const char* e = getenv("MSX_KERNEL_SYS_FENCE")) return atoi(e) != 0;
+        const char* c = getenv("MSX_WINDOW_CACHED");
+        return c && atoi(c) != 0;
+    }();
+    return on;
+}
+
 // Evaluate RankTree `t` over [start, start+len) elements of the per-rank
 // source pointers `srcs` into `out`.
 int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>& srcs, size_t esz,
@@ -672,7 +694,7 @@ int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>
     spec.nleaves = t.nleaves;
     spec.pairmask = t.pairmask;
     spec.chain = t.chain;
-    spec.sys = true;
+    spec.sys = sys_fences();
     const int nslots = t.chain ? t.P : 2 * (t.nleaves ? t.nleaves : t.P);
     for (int i = 0; i < nslots; ++i)
         spec.src[i] = t.src[i] >= 0 ? srcs[(size_t)t.src[i]] + start * esz : nullptr;
@@ -931,7 +953,7 @@ struct Segs {
     int run(hipStream_t s, const char* what)
     {
         if (src.empty()) return MPI_SUCCESS;
-        hipError_t e = launch_copy_segs(src.data(), dst.data(), n.data(), (int)src.size(), true, s);
+        hipError_t e = launch_copy_segs(src.data(), dst.data(), n.data(), (int)src.size(), sys_fences(), s);
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
     }
 };
@@ -1649,7 +1671,7 @@ int combine2(int opidx, Kind k, const char* inout_src, const char* in, char* out
     t.P = 2;
     t.src[0] = inout_src;
     t.src[2] = in;
-    t.sys = true;
+    t.sys = sys_fences();
     hipError_t e = launch_tree_spec(opidx, k, t, out, n, s);
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "scan combine");
 }
