@@ -121,13 +121,17 @@ def main(out_path, scale):
         b = torch.empty_like(a)
         torch.cuda.synchronize()
         L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+        # back-to-back calls after one barrier, averaged (the OSU latency
+        # method: no barrier wake-up skew inside the timed calls)
+        iters = 50 if nbytes <= (4 << 20) else 10
         ts = []
-        for _ in range(5):
+        for _ in range(3):
             barrier()
             t0 = time.perf_counter()
-            L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
-            ts.append(time.perf_counter() - t0)
-        t = sorted(ts)[2]
+            for _ in range(iters):
+                L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+            ts.append((time.perf_counter() - t0) / iters)
+        t = sorted(ts)[1]
         curve[str(nbytes)] = {"us": round(t * 1e6, 1), "busbw_GB_s": round(nbytes / t / 1e9 * 2 * (p - 1) / p, 2),
                               "correct": bool(torch.equal(b, want))}
     res["allreduce_curve_f32"] = curve

@@ -45,9 +45,22 @@ struct TreeSpec {
     bool sys = false;   // sources/output shared with peers: system acquire/release
     void* extra[31] = {};   // the result is also stored here (e.g. peers' windows)
     int nextra = 0;
+    // GPU-side arrival wait (barrier-free small allreduce): before reading,
+    // every workgroup waits until wait_flags[r] >= wait_seq for all r < wait_n,
+    // r != wait_skip (flags posted by peers with launch_post_flags); after
+    // ~20 s without them it stores 1 to *wait_err (host-visible) and exits.
+    const unsigned long long* wait_flags = nullptr;
+    unsigned long long wait_seq = 0;
+    int wait_n = 0;
+    int wait_skip = -1;
+    int* wait_err = nullptr;
 };
 hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t count,
                             hipStream_t s);
+
+// Store `seq` to *dst[i] for i < n (system scope): the arrival flags of the
+// barrier-free small allreduce, posted after the data kernel on the same stream.
+hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned long long seq, hipStream_t s);
 
 // Copy nseg independent byte ranges in one launch (one grid row per segment),
 // used to pull allgather blocks from every peer concurrently.

@@ -175,7 +175,40 @@ struct TreeArgs {
     unsigned pairmask;
     int chain;
     int sys;   // sources/outputs shared with other GPUs: system-coherent access
+    const unsigned long long* wait_flags;   // see TreeSpec
+    unsigned long long wait_seq;
+    int wait_n;
+    int wait_skip;
+    int* wait_err;
 };
+
+// Arrival wait of the barrier-free small allreduce: thread 0 of every
+// workgroup polls the peers' flags (uncached window memory, system-scope
+// loads) until each reaches the call's sequence number.  Bounded: after
+// ~20 s (s_memrealtime runs at 100 MHz) it reports through *wait_err and the
+// workgroup exits, so a missing peer can never leave a wave running.
+__device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
+{
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        int good = 1;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (int r = 0; r < a.wait_n && good; ++r) {
+            if (r == a.wait_skip) continue;
+            while (__hip_atomic_load(a.wait_flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.wait_seq) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+                    __hip_atomic_store(a.wait_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    good = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
 
 // Start-of-kernel system acquire: invalidate this CU's L1 and the XCD's L2
 // lines for memory other GPUs may have written since (peer HBM over xGMI).
@@ -276,6 +309,7 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
     constexpr size_t EPV = 16 / sizeof(T);
     const size_t stride = (size_t)gridDim.x * BLOCK;
     const size_t bid = xcd_tile(blockIdx.x, gridDim.x);      // XCD-contiguous (see combine_body)
+    if (a.wait_flags && !arrival_wait(a)) return;
     if (a.sys) acquire_system();
     if (vec_ok) {
         for (size_t i = bid * BLOCK + threadIdx.x; i < nvec; i += stride) {
@@ -310,6 +344,18 @@ struct CopySegs {
     int n;
     int sys;
 };
+
+struct PostFlags {
+    unsigned long long* dst[64];
+    unsigned long long seq;
+    int n;
+};
+
+__global__ __launch_bounds__(64) void k_post_flags(PostFlags f)
+{
+    if (threadIdx.x < (unsigned)f.n)
+        __hip_atomic_store(f.dst[threadIdx.x], f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
 {
@@ -651,7 +697,13 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     a.pairmask = t.pairmask;
     a.chain = t.chain ? 1 : 0;
     a.sys = t.sys ? 1 : 0;
-    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0) {
+    a.wait_flags = t.wait_flags;
+    a.wait_seq = t.wait_seq;
+    a.wait_n = t.wait_n;
+    a.wait_skip = t.wait_skip;
+    a.wait_err = t.wait_err;
+    if (t.wait_flags && (!t.wait_err || t.wait_n < 0)) return hipErrorInvalidValue;
+    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.wait_flags) {
         if (t.src[0] == out) return hipSuccess;
         return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
     }
@@ -678,6 +730,18 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     case O_MINLOC: return tree_loc<O_MINLOC>(k, a, ns, out, n, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned long long seq, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    if (n > 64) return hipErrorInvalidValue;
+    PostFlags f{};
+    for (int i = 0; i < n; ++i) f.dst[i] = dst[i];
+    f.seq = seq;
+    f.n = n;
+    hipLaunchKernelGGL(k_post_flags, dim3(1), dim3(64), 0, s, f);
+    return hipGetLastError();
 }
 
 hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,

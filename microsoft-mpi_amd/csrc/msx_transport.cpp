@@ -379,6 +379,11 @@ public:
             hipError_t e = cached ? hipMalloc(&win_, want) : hipExtMallocWithFlags(&win_, want, hipDeviceMallocUncached);
             trace("window: %zu bytes %s rc=%d", want, cached ? "cached" : "uncached", (int)e);
             if (e != hipSuccess) return hip_fail(e, "window allocation");
+            // zeroed before any peer can map it (map_peers below is collective):
+            // the arrival flags behind the data areas must start at 0
+            e = hipMemset(win_, 0, want);
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+            if (e != hipSuccess) return hip_fail(e, "window clear");
             win_bytes_ = want;
             win_peers_.clear();
         }
@@ -622,6 +627,30 @@ public:
         return f;
     }
 
+    // A blocking call: run it on the calling thread when the worker is idle
+    // (no queued or running task -- the collective order is then the issue
+    // order anyway), which saves two thread hand-offs (~10-20 us) per call;
+    // otherwise queue it behind the pending non-blocking operations.
+    int run(std::function<int()> fn)
+    {
+        if (std::this_thread::get_id() == tid_) return fn();
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            if (!q_.empty() || busy_ || inline_) {
+                g.unlock();
+                return submit(std::move(fn)).get();
+            }
+            inline_ = true;
+        }
+        const int rc = fn();
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            inline_ = false;
+        }
+        cv_.notify_all();
+        return rc;
+    }
+
 private:
     void loop()
     {
@@ -629,12 +658,15 @@ private:
             std::shared_ptr<std::packaged_task<int()>> t;
             {
                 std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+                cv_.wait(g, [this] { return stop_ || (!q_.empty() && !inline_); });
                 if (q_.empty()) return;
                 t = q_.front();
                 q_.pop_front();
+                busy_ = true;
             }
             (*t)();
+            std::lock_guard<std::mutex> g(mu_);
+            busy_ = false;
         }
     }
     std::mutex mu_;
@@ -643,6 +675,8 @@ private:
     std::thread th_;
     std::thread::id tid_;
     bool stop_ = false;
+    bool busy_ = false;     // the worker is running a task
+    bool inline_ = false;   // a blocking call runs on its caller's thread
 };
 
 Worker& worker()
@@ -681,12 +715,26 @@ bool sys_fences()
 
 // Evaluate RankTree `t` over [start, start+len) elements of the per-rank
 // source pointers `srcs` into `out`.
+struct TreeWait {
+    const unsigned long long* flags = nullptr;   // my window's arrival flags
+    unsigned long long seq = 0;
+    int n = 0, skip = -1;
+    int* err = nullptr;                          // device view of a pinned host word
+};
+
 int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>& srcs, size_t esz,
                   size_t start, size_t len, char* out, hipStream_t s,
-                  const std::vector<char*>& extra_outs = {})
+                  const std::vector<char*>& extra_outs = {}, const TreeWait* wait = nullptr)
 {
     if (len == 0) return MPI_SUCCESS;
     TreeSpec spec;
+    if (wait) {
+        spec.wait_flags = wait->flags;
+        spec.wait_seq = wait->seq;
+        spec.wait_n = wait->n;
+        spec.wait_skip = wait->skip;
+        spec.wait_err = wait->err;
+    }
     if (extra_outs.size() > 31) { set_error("tree combine: too many destinations"); return MPI_ERR_INTERN; }
     spec.nextra = (int)extra_outs.size();
     for (size_t e = 0; e < extra_outs.size(); ++e) spec.extra[e] = extra_outs[e];
@@ -889,19 +937,53 @@ size_t chunk_bytes()
     return c;
 }
 
+// Arrival flags of the barrier-free allreduce live behind the two areas:
+// flag k of window r (8 bytes) = the last call sequence rank k posted to r.
+constexpr size_t kFlagBytes = 64 << 10;
+
 struct Windows {
     std::vector<char*> base;
     size_t C = 0, Q = 0;
     char* in(int r) const { return base[(size_t)r]; }
     char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * Q; }
     char* out(int r) const { return base[(size_t)r] + C; }
+    unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + 2 * C); }
 };
+
+// The barrier-free small allreduce synchronises on GPU arrival flags
+// (MSX_RD_FLAGS=0: host barrier instead).
+bool rd_flags()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_RD_FLAGS");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+// Pinned host word the arrival wait reports a timeout through (engine worker
+// only); returns its device view.
+int* wait_err_word(int** host)
+{
+    static int* h = nullptr;
+    static int* d = nullptr;
+    if (!h) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(int), hipHostMallocCoherent | hipHostMallocMapped) !=
+            hipSuccess) {
+            h = nullptr;
+            return nullptr;
+        }
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0) != hipSuccess) d = h;
+    }
+    *host = h;
+    return d;
+}
 
 int get_windows(Transport* tp, Windows* w, bool rd_single = false)
 {
     w->C = chunk_bytes();
     w->Q = (w->C / (size_t)tp->size) & ~(size_t)255;
-    int rc = tp->window(2 * w->C, w->base);
+    int rc = tp->window(2 * w->C + kFlagBytes, w->base);
     if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
         // the last recursive-doubling call left without its closing barrier:
         // peers may still be reading their IN areas
@@ -1307,6 +1389,59 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // recursive doubling -> all ranks evaluate their own lineage's tree;
         // binomial reduce -> only the root evaluates
         const RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
+        if (rd_single && root < 0 && p <= 64 && rd_flags()) {
+            // Allreduce: no host barrier at all.  Each rank pushes its vector
+            // into every peer's IN half, then posts the call's sequence number
+            // into the peers' flag slots (a second kernel on the same stream:
+            // the data stores completed first); the tree kernel waits on the
+            // GPU until all peers' flags reached the sequence.  The half is
+            // reused two calls later only after every peer's tree read it:
+            // a peer posts call k+1 after its call k returned, and this rank
+            // pushes call k+2 after its own call k+1 tree saw those flags.
+            const size_t half = (size_t)tp->rd_parity * Qh;
+            for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
+            const char* mine = nullptr;
+            rc = device_view(bs, src, 0, count * esz, stage, s, &mine);
+            Segs sg;
+            std::vector<unsigned long long*> fl;
+            for (int r = 0; r < p; ++r)
+                if (r != me) {
+                    sg.add(mine, w.sub(r, me) + half, count * esz);
+                    fl.push_back(w.flags(r) + me);
+                }
+            subs[(size_t)me] = const_cast<char*>(mine);
+            const unsigned long long seq = ++tp->rd_seq;
+            int* err_host = nullptr;
+            int* err_dev = wait_err_word(&err_host);
+            if (!err_dev) { set_error("allreduce: arrival word allocation failed"); return MPI_ERR_NO_MEM; }
+            *err_host = 0;
+            if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
+            if (rc == MPI_SUCCESS) {
+                hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);
+                if (e != hipSuccess) rc = hip_fail(e, "allreduce arrival flags");
+            }
+            if (rc == MPI_SUCCESS) {
+                TreeWait tw;
+                tw.flags = w.flags(me);
+                tw.seq = seq;
+                tw.n = p;
+                tw.skip = me;
+                tw.err = err_dev;
+                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
+                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s, {}, &tw);
+                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
+            }
+            const int rs = sync_stream(s, "allreduce tree");
+            if (rc == MPI_SUCCESS) rc = rs;
+            if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
+                set_error("allreduce: a peer's contribution did not arrive within 20 s");
+                rc = MPI_ERR_OTHER;
+            }
+            tp->rd_parity ^= 1;
+            tp->window_open = true;
+            trace("allreduce: done (GPU arrival flags, seq %llu) rc=%d", seq, rc);
+            return rc;
+        }
         if (rd_single) {
             const size_t half = (size_t)tp->rd_parity * Qh;
             for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
@@ -1550,16 +1685,14 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
 int engine_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                      const OpRef& op)
 {
-    return worker().submit([=] { return do_allreduce(c, sendbuf, recvbuf, count, dt, op); }).get();
+    return worker().run([=] { return do_allreduce(c, sendbuf, recvbuf, count, dt, op); });
 }
 
 int engine_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
                           MPI_Datatype dt, const OpRef& op)
 {
     std::vector<int> counts(recvcounts, recvcounts + c->size);
-    return worker()
-        .submit([=] { return do_reduce_scatter(c, sendbuf, recvbuf, counts.data(), dt, op); })
-        .get();
+    return worker().run([=] { return do_reduce_scatter(c, sendbuf, recvbuf, counts.data(), dt, op); });
 }
 
 namespace {
@@ -1607,12 +1740,10 @@ int engine_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI
 {
     // Builtin ops: the reference's binomial / Rabenseifner trees (do_allreduce
     // in reduce mode); user ops: host_user_reduce.
-    return worker()
-        .submit([=]() -> int {
-            if (op.opidx == O_NULL) return host_user_reduce(c, sendbuf, recvbuf, count, dt, op, root);
-            return do_allreduce(c, sendbuf, recvbuf, count, dt, op, root);
-        })
-        .get();
+    return worker().run([=]() -> int {
+        if (op.opidx == O_NULL) return host_user_reduce(c, sendbuf, recvbuf, count, dt, op, root);
+        return do_allreduce(c, sendbuf, recvbuf, count, dt, op, root);
+    });
 }
 
 namespace {
@@ -1746,7 +1877,7 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
 int engine_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                 const OpRef& op, bool exclusive)
 {
-    return worker().submit([=] { return do_scan(c, sendbuf, recvbuf, count, dt, op, exclusive); }).get();
+    return worker().run([=] { return do_scan(c, sendbuf, recvbuf, count, dt, op, exclusive); });
 }
 
 // ===========================================================================
@@ -2095,7 +2226,7 @@ int engine_rma_create(RmaWin* w)
 int engine_rma_fence(RmaWin* w)
 {
     if (w->comm->size == 1 || !w->comm->tp) return MPI_SUCCESS;   // all operations were local
-    return worker().submit([w] { return do_rma_fence(w); }).get();
+    return worker().run([w] { return do_rma_fence(w); });
 }
 
 int engine_stats(double* out, int n, int reset)

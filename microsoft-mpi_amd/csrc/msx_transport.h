@@ -32,6 +32,9 @@ public:
     // Every rank runs the same collective sequence, so these agree everywhere.
     bool window_open = false;
     int rd_parity = 0;
+    // barrier-free allreduce: sequence number of the last flag-synchronised
+    // call (the same on every rank: collectives are called in one order)
+    unsigned long long rd_seq = 0;
     // lock-step host collectives over the bootstrap hub (all ranks, same n)
     virtual int allgather(const void* mine, size_t n, void* all) = 0;
     virtual int barrier() = 0;
