@@ -218,6 +218,47 @@ else:
     check("iallreduce band u64", fromdev(rb, xs[rank]), exp[rank])
 assert req.value == C.MPI_REQUEST_NULL
 
+# Back-to-back stress of the barrier-free small allreduce (GPU arrival flags,
+# alternating IN halves) interleaved with the other window users: rooted
+# reduce (host barrier), a chunked large allreduce (full barrier first),
+# non-blocking calls through the engine worker, in-place calls.
+def ivec(it, r, n):
+    return ((np.arange(n, dtype=np.int64) * 7 + it * 31 + r * 1009) % 100003).astype(np.int32)
+
+for it in range(240):
+    n = (1, 5, 64, 1000, 4096, 65536)[it % 6]
+    tot = sum(ivec(it, r, n).astype(np.int64) for r in range(p)).astype(np.int32)
+    if it % 50 == 49:                      # large: Rabenseifner path, barriers
+        n = 1 << 18
+        tot = sum(ivec(it, r, n).astype(np.int64) for r in range(p)).astype(np.int32)
+    sb = todev(ivec(it, rank, n))
+    if it % 7 == 3:                        # rooted reduce: host-barrier variant
+        root = it % p
+        rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
+        rc = L.MPI_Reduce(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, root, C.MPI_COMM_WORLD)
+        if rc:
+            fails.append(f"stress reduce {it} rc={rc}")
+        elif rank == root:
+            check(f"stress reduce {it}", fromdev(rb, tot), tot)
+        continue
+    if it % 11 == 5:                       # non-blocking, through the worker
+        rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
+        req = ctypes.c_int()
+        rc = L.MPI_Iallreduce(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD,
+                              ctypes.byref(req))
+        rc = rc or L.MPI_Wait(ctypes.byref(req), None)
+    elif it % 5 == 2:                      # in place
+        rb = sb
+        rc = L.MPI_Allreduce(ctypes.c_void_p(C.MPI_IN_PLACE), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM,
+                             C.MPI_COMM_WORLD)
+    else:
+        rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
+        rc = L.MPI_Allreduce(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD)
+    if rc:
+        fails.append(f"stress allreduce {it} rc={rc} {msx.last_error()}")
+        break
+    check(f"stress allreduce {it} n={n}", fromdev(rb, tot), tot)
+
 L.msx_engine_transport.restype = ctypes.c_char_p
 print("TRANSPORT", L.msx_engine_transport().decode(), flush=True)
 print("RESULT", rank, p, len(fails), fails[:5], flush=True)
