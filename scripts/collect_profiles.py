@@ -19,7 +19,10 @@ def json_line(log):
     return json.loads(lines[-1]) if lines else None
 
 
-for log, name in (("bench.log", "bench_n1.json"), ("rocprof_trace.log", "bench_n1_under_rocprof.json")):
+for log, name in (("bench.log", "bench_n1.json"), ("rocprof_trace.log", "bench_n1_under_rocprof.json"),
+                  ("bench_n2.log", "bench_n2_shared_gpu.json")):
+    if not os.path.exists(os.path.join(SRC, log)):
+        continue
     d = json_line(log)
     if d:
         with open(os.path.join(DST, name), "w") as f:
@@ -49,4 +52,6 @@ for n in ("pmc_fetch_counter_collection.csv", "pmc_write_counter_collection.csv"
             if any(s in row[k] for s in keep) and "k_combine_host" not in row[k]:
                 w.writerow(row)
 shutil.copy(os.path.join(SRC, "steps.log"), DST)
+if os.path.exists(os.path.join(SRC, "collectives_n2.log")):
+    shutil.copy(os.path.join(SRC, "collectives_n2.log"), os.path.join(DST, "collectives_n2_shared_gpu.log"))
 print("profiles ->", DST)

@@ -23,6 +23,10 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --sweep
+    # N = 2 with both ranks on this box's one GPU: exercises the N > 1 bench
+    # path and the collectives harness (shared HBM, not xGMI)
+    MSX_BENCH_LOG=$OUT/collectives_n2.log step bench_n2 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 20 --warmup 5
     step rocprof_trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_trace" -o trace --output-format csv -- python bench.py
     step rocprof_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof_pmc" -o pmc_fetch --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0.5 --no-host-path
     step rocprof_pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof_pmc" -o pmc_write --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0.5 --no-host-path
