@@ -276,11 +276,24 @@ typedef int MPI_Info;
 #define MPI_MODE_NOPUT      4096
 #define MPI_MODE_NOPRECEDE  8192
 #define MPI_MODE_NOSUCCEED 16384
+/* passive-target lock types (mpi.h:5324-5325) */
+#define MPI_LOCK_EXCLUSIVE  234
+#define MPI_LOCK_SHARED     235
 
 MPI_METHOD MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info info,
                           MPI_Comm comm, MPI_Win* win);
 MPI_METHOD MPI_Win_free(MPI_Win* win);
 MPI_METHOD MPI_Win_fence(int assert, MPI_Win win);
+/* passive-target synchronisation (api/mpi_win.cpp:1153-1990) */
+MPI_METHOD MPI_Win_lock(int lock_type, int rank, int assert, MPI_Win win);
+MPI_METHOD MPI_Win_unlock(int rank, MPI_Win win);
+MPI_METHOD MPI_Win_lock_all(int assert, MPI_Win win);
+MPI_METHOD MPI_Win_unlock_all(MPI_Win win);
+MPI_METHOD MPI_Win_flush(int rank, MPI_Win win);
+MPI_METHOD MPI_Win_flush_all(MPI_Win win);
+MPI_METHOD MPI_Win_flush_local(int rank, MPI_Win win);
+MPI_METHOD MPI_Win_flush_local_all(MPI_Win win);
+MPI_METHOD MPI_Win_sync(MPI_Win win);
 MPI_METHOD MPI_Win_set_errhandler(MPI_Win win, MPI_Errhandler errhandler);
 MPI_METHOD MPI_Win_get_errhandler(MPI_Win win, MPI_Errhandler* errhandler);
 MPI_METHOD MPI_Put(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,

@@ -903,7 +903,9 @@ int rma_issue(RmaWin* w, RmaKind kind, int target, MPI_Aint disp, int opidx, con
         return rc;
     }
     if (self) {
+        engine_rma_self_guard(w, true);      // not concurrently with the window's service thread
         rc = rma_apply_self(w, d, l, T);
+        engine_rma_self_guard(w, false);
         const int r2 = rma_local_complete(l);
         return rc != MPI_SUCCESS ? rc : r2;
     }
@@ -943,6 +945,8 @@ MSX_EXPORT int MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info
     w->base = static_cast<char*>(base);
     w->size = size;
     w->disp_unit = disp_unit;
+    w->lock_mode.assign((size_t)c->size, 0);
+    w->lock_held.assign((size_t)c->size, 0);
     rc = engine_rma_create(w);
     if (rc != MPI_SUCCESS) {
         delete w;
@@ -966,8 +970,11 @@ MSX_EXPORT int MPI_Win_free(MPI_Win* win)
     int rc = v_win(*win, &w);
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_free", rc);
     if (!w->q.empty()) { set_error("MPI_Win_free with operations pending (no closing fence)"); return err_win(w, "MPI_Win_free", MPI_ERR_RMA_SYNC); }
+    for (int m : w->lock_mode)
+        if (m) { set_error("MPI_Win_free inside a passive-target epoch"); return err_win(w, "MPI_Win_free", MPI_ERR_RMA_SYNC); }
     rc = coll_barrier(w->comm);       // every rank is done with the window
     if (rc != MPI_SUCCESS) return err_win(w, "MPI_Win_free", rc);
+    engine_rma_free(w);               // no request can be in flight after the barrier
     {
         std::lock_guard<std::mutex> g(g_win_mu);
         g_wins[(size_t)(*win & 0x03ffffff)] = nullptr;
@@ -985,6 +992,175 @@ MSX_EXPORT int MPI_Win_fence(int assert_, MPI_Win win)
     if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_fence", rc);
     (void)assert_;                    // hints only
     return err_win(w, "MPI_Win_fence", engine_rma_fence(w));
+}
+
+// ---- passive target (api/mpi_win.cpp:1153-1990, mpid/win.cpp:4090-4500) ----------
+namespace {
+// MpiaCommValidateSendRank: a rank of the window's group or MPI_PROC_NULL
+int v_lock_rank(RmaWin* w, int rank)
+{
+    if (rank == MPI_PROC_NULL || (rank >= 0 && rank < w->comm->size)) return MPI_SUCCESS;
+    set_error("invalid rank %d", rank);
+    return MPI_ERR_RANK;
+}
+
+// MPID_Win_lock: a lock on this rank itself is acquired now (blocking); on
+// another rank it is requested lazily, granted at the first flush / unlock
+int win_lock(RmaWin* w, int lock_type, int rank, int assert_)
+{
+    (void)assert_;                    // MPI_MODE_NOCHECK: a hint
+    if (rank == MPI_PROC_NULL) return MPI_SUCCESS;
+    if (w->lock_mode[(size_t)rank]) {
+        set_error("rank %d is already locked in this window (**rmasyncq)", rank);
+        return MPI_ERR_OTHER;
+    }
+    if (rank == w->comm->rank) {
+        const int rc = engine_rma_lock(w, rank, lock_type);
+        if (rc != MPI_SUCCESS) return rc;
+        w->lock_held[(size_t)rank] = 1;
+    }
+    w->lock_mode[(size_t)rank] = lock_type;
+    return MPI_SUCCESS;
+}
+
+int win_unlock(RmaWin* w, int rank)
+{
+    if (rank == MPI_PROC_NULL) return MPI_SUCCESS;
+    if (!w->lock_mode[(size_t)rank]) {
+        set_error("MPI_Win_unlock without MPI_Win_lock on rank %d (**rmasync)", rank);
+        return MPI_ERR_OTHER;
+    }
+    const int rc = engine_rma_flush(w, rank);
+    engine_rma_unlock_target(w, rank);
+    w->lock_mode[(size_t)rank] = 0;
+    w->lock_held[(size_t)rank] = 0;
+    return rc;
+}
+}  // namespace
+
+MSX_EXPORT int MPI_Win_lock(int lock_type, int rank, int assert_, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_lock");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_lock", rc);
+    if (lock_type != MPI_LOCK_SHARED && lock_type != MPI_LOCK_EXCLUSIVE) {
+        set_error("invalid lock type %d (**locktype)", lock_type);
+        rc = MPI_ERR_OTHER;
+    }
+    if (rc == MPI_SUCCESS) rc = v_lock_rank(w, rank);
+    if (rc == MPI_SUCCESS) rc = win_lock(w, lock_type, rank, assert_);
+    return err_win(w, "MPI_Win_lock", rc);
+}
+
+MSX_EXPORT int MPI_Win_unlock(int rank, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_unlock");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_unlock", rc);
+    rc = v_lock_rank(w, rank);
+    if (rc == MPI_SUCCESS) rc = win_unlock(w, rank);
+    return err_win(w, "MPI_Win_unlock", rc);
+}
+
+// MPID_Win_lock_all: a shared lock on every rank (mpid/win.cpp:4133-4150)
+MSX_EXPORT int MPI_Win_lock_all(int assert_, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_lock_all");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_lock_all", rc);
+    for (int r = 0; rc == MPI_SUCCESS && r < w->comm->size; ++r) rc = win_lock(w, MPI_LOCK_SHARED, r, assert_);
+    if (rc == MPI_SUCCESS) w->lock_all = true;
+    return err_win(w, "MPI_Win_lock_all", rc);
+}
+
+MSX_EXPORT int MPI_Win_unlock_all(MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_unlock_all");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_unlock_all", rc);
+    if (!w->lock_all) {
+        set_error("MPI_Win_unlock_all without MPI_Win_lock_all (**rmasync)");
+        return err_win(w, "MPI_Win_unlock_all", MPI_ERR_OTHER);
+    }
+    for (int r = 0; r < w->comm->size; ++r) {
+        const int r2 = w->lock_mode[(size_t)r] ? win_unlock(w, r) : MPI_SUCCESS;
+        if (rc == MPI_SUCCESS) rc = r2;
+    }
+    w->lock_all = false;
+    return err_win(w, "MPI_Win_unlock_all", rc);
+}
+
+// Flush: every operation this rank issued to `rank` is complete at origin and
+// target (a fetch has landed; an update is visible to the target's next
+// access).  flush_local needs only origin completion, which is the same here.
+MSX_EXPORT int MPI_Win_flush(int rank, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_flush");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_flush", rc);
+    rc = v_lock_rank(w, rank);
+    if (rc == MPI_SUCCESS && rank != MPI_PROC_NULL) rc = engine_rma_flush(w, rank);
+    return err_win(w, "MPI_Win_flush", rc);
+}
+
+MSX_EXPORT int MPI_Win_flush_local(int rank, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_flush_local");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_flush_local", rc);
+    rc = v_lock_rank(w, rank);
+    if (rc == MPI_SUCCESS && rank != MPI_PROC_NULL) rc = engine_rma_flush(w, rank);
+    return err_win(w, "MPI_Win_flush_local", rc);
+}
+
+namespace {
+int flush_all(RmaWin* w)
+{
+    int rc = MPI_SUCCESS;
+    for (int r = 0; r < w->comm->size; ++r) {
+        const int r2 = engine_rma_flush(w, r);
+        if (rc == MPI_SUCCESS) rc = r2;
+    }
+    return rc;
+}
+}  // namespace
+
+MSX_EXPORT int MPI_Win_flush_all(MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_flush_all");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_flush_all", rc);
+    return err_win(w, "MPI_Win_flush_all", flush_all(w));
+}
+
+MSX_EXPORT int MPI_Win_flush_local_all(MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_flush_local_all");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_flush_local_all", rc);
+    return err_win(w, "MPI_Win_flush_local_all", flush_all(w));
+}
+
+// MPI_Win_sync: public and private copies of the window agree.  Remote
+// updates are applied by this rank's own service thread on this GPU and are
+// complete (stream-synchronised) before their origin's flush returns, so
+// a memory fence for the host-side view is all that is left.
+MSX_EXPORT int MPI_Win_sync(MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_sync");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_sync", rc);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    return MPI_SUCCESS;
 }
 
 MSX_EXPORT int MPI_Win_set_errhandler(MPI_Win win, MPI_Errhandler eh)

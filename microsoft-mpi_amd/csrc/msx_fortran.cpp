@@ -520,6 +520,34 @@ FAPI void mpi_win_fence_(const MPI_Fint* assert_, const MPI_Fint* win, MPI_Fint*
     *ierr = MPI_Win_fence(*assert_, *win);
 }
 FNAMES(win_fence, WIN_FENCE)
+FAPI void mpi_win_lock_(const MPI_Fint* lock_type, const MPI_Fint* rank, const MPI_Fint* assert_, const MPI_Fint* win,
+                        MPI_Fint* ierr)
+{
+    *ierr = MPI_Win_lock(*lock_type, *rank, *assert_, *win);
+}
+FNAMES(win_lock, WIN_LOCK)
+FAPI void mpi_win_unlock_(const MPI_Fint* rank, const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_unlock(*rank, *win); }
+FNAMES(win_unlock, WIN_UNLOCK)
+FAPI void mpi_win_lock_all_(const MPI_Fint* assert_, const MPI_Fint* win, MPI_Fint* ierr)
+{
+    *ierr = MPI_Win_lock_all(*assert_, *win);
+}
+FNAMES(win_lock_all, WIN_LOCK_ALL)
+FAPI void mpi_win_unlock_all_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_unlock_all(*win); }
+FNAMES(win_unlock_all, WIN_UNLOCK_ALL)
+FAPI void mpi_win_flush_(const MPI_Fint* rank, const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_flush(*rank, *win); }
+FNAMES(win_flush, WIN_FLUSH)
+FAPI void mpi_win_flush_all_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_flush_all(*win); }
+FNAMES(win_flush_all, WIN_FLUSH_ALL)
+FAPI void mpi_win_flush_local_(const MPI_Fint* rank, const MPI_Fint* win, MPI_Fint* ierr)
+{
+    *ierr = MPI_Win_flush_local(*rank, *win);
+}
+FNAMES(win_flush_local, WIN_FLUSH_LOCAL)
+FAPI void mpi_win_flush_local_all_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_flush_local_all(*win); }
+FNAMES(win_flush_local_all, WIN_FLUSH_LOCAL_ALL)
+FAPI void mpi_win_sync_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_sync(*win); }
+FNAMES(win_sync, WIN_SYNC)
 FAPI void mpi_win_set_errhandler_(const MPI_Fint* win, const MPI_Fint* eh, MPI_Fint* ierr)
 {
     *ierr = MPI_Win_set_errhandler(*win, *eh);

@@ -212,19 +212,22 @@ public:
         size_ = size;
         timeout_ = timeout_s;
         char name[64] = {0};
-        if (rank == 0) snprintf(name, sizeof(name), "/msx_bar_%d_%ld", (int)getpid(), (long)(now_s() * 1e6));
-        std::vector<char> all((size_t)size * sizeof(name));
-        if (hub.allgather(name, sizeof(name), all.data()) != MPI_SUCCESS) return false;
-        memcpy(name, all.data(), sizeof(name));
-        int ok = 1;
-        int fd = shm_open(name, rank == 0 ? (O_CREAT | O_RDWR) : O_RDWR, 0600);
+        int fd = -1;
         if (rank == 0) {
-            if (fd < 0 || ftruncate(fd, 4096) != 0) ok = 0;
+            // created and sized before anyone learns the name
+            snprintf(name, sizeof(name), "/msx_bar_%d_%ld", (int)getpid(), (long)(now_s() * 1e6));
+            fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+            if (fd < 0 || ftruncate(fd, 4096) != 0) name[0] = 0;
         }
-        // rank 0 has sized the segment before anyone maps it
+        std::vector<char> all((size_t)size * sizeof(name));
+        if (hub.allgather(name, sizeof(name), all.data()) != MPI_SUCCESS) {
+            if (fd >= 0) close(fd);
+            return false;
+        }
+        memcpy(name, all.data(), sizeof(name));
+        int ok = name[0] != 0;
+        if (ok && rank != 0) fd = shm_open(name, O_RDWR, 0600);
         std::vector<int> oks((size_t)size);
-        if (hub.allgather(&ok, sizeof(int), oks.data()) != MPI_SUCCESS) ok = 0;
-        for (int v : oks) ok &= v;
         void* m = MAP_FAILED;
         if (ok && fd >= 0) m = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         if (fd >= 0) close(fd);
@@ -638,7 +641,15 @@ public:
             std::unique_lock<std::mutex> g(mu_);
             if (!q_.empty() || busy_ || inline_) {
                 g.unlock();
-                return submit(std::move(fn)).get();
+                // the error text is thread-local: carry it back to the caller
+                auto text = std::make_shared<std::string>();
+                const int rc = submit([fn = std::move(fn), text]() -> int {
+                                   const int r = fn();
+                                   if (r != MPI_SUCCESS) *text = last_error();
+                                   return r;
+                               }).get();
+                if (rc != MPI_SUCCESS) set_error("%s", text->c_str());
+                return rc;
             }
             inline_ = true;
         }
@@ -931,7 +942,7 @@ size_t chunk_bytes()
         size_t v = (size_t)512 << 20;
         if (const char* e = getenv("MSX_CHUNK_BYTES")) v = (size_t)atoll(e);
         if (v < ((size_t)1 << 16)) v = (size_t)1 << 16;
-        if (v > ((size_t)1000 << 20)) v = (size_t)1000 << 20;   // window 2*C < 2 GiB
+        if (v > ((size_t)960 << 20)) v = (size_t)960 << 20;   // whole window < 2 GiB (IPC limit)
         return v & ~(size_t)4095;
     }();
     return c;
@@ -940,6 +951,9 @@ size_t chunk_bytes()
 // Arrival flags of the barrier-free allreduce live behind the two areas:
 // flag k of window r (8 bytes) = the last call sequence rank k posted to r.
 constexpr size_t kFlagBytes = 64 << 10;
+// Passive-target RMA area behind the flags: p payload slots (written by each
+// origin) then p fetch slots (written by each target), kRmaBytes / (2p) each.
+constexpr size_t kRmaBytes = (size_t)64 << 20;
 
 struct Windows {
     std::vector<char*> base;
@@ -948,6 +962,13 @@ struct Windows {
     char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * Q; }
     char* out(int r) const { return base[(size_t)r] + C; }
     unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + 2 * C); }
+    size_t rma_slot() const { return (kRmaBytes / (2 * base.size())) & ~(size_t)255; }
+    // rank r's window: payload slot written by origin o / fetch slot written by target t
+    char* rma_in(int r, int o) const { return base[(size_t)r] + 2 * C + kFlagBytes + (size_t)o * rma_slot(); }
+    char* rma_fetch(int r, int t) const
+    {
+        return base[(size_t)r] + 2 * C + kFlagBytes + (base.size() + (size_t)t) * rma_slot();
+    }
 };
 
 // The barrier-free small allreduce synchronises on GPU arrival flags
@@ -983,7 +1004,7 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
 {
     w->C = chunk_bytes();
     w->Q = (w->C / (size_t)tp->size) & ~(size_t)255;
-    int rc = tp->window(2 * w->C + kFlagBytes, w->base);
+    int rc = tp->window(2 * w->C + kFlagBytes + kRmaBytes, w->base);
     if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
         // the last recursive-doubling call left without its closing barrier:
         // peers may still be reading their IN areas
@@ -2200,6 +2221,10 @@ int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l, const Dtype* 
     return rc == MPI_SUCCESS ? sync_stream(s, "rma self") : rc;
 }
 
+namespace {
+int passive_init(RmaWin* w);   // below, with the passive-target machinery
+}
+
 int engine_rma_create(RmaWin* w)
 {
     Comm* c = w->comm;
@@ -2211,7 +2236,7 @@ int engine_rma_create(RmaWin* w)
         w->disp_units[0] = w->disp_unit;
         return MPI_SUCCESS;
     }
-    return worker().submit([w, c, p] {
+    return worker().run([w, c, p] {
         int64_t mine[2] = {w->size, (int64_t)w->disp_unit};
         std::vector<int64_t> all((size_t)p * 2);
         int rc = c->tp->allgather(mine, sizeof(mine), all.data());
@@ -2219,8 +2244,349 @@ int engine_rma_create(RmaWin* w)
             w->sizes[(size_t)r] = all[(size_t)r * 2];
             w->disp_units[(size_t)r] = (int)all[(size_t)r * 2 + 1];
         }
+        // passive target: mailbox + this rank's service thread (collective)
+        if (rc == MPI_SUCCESS) rc = passive_init(w);
         return rc;
-    }).get();
+    });
+}
+
+// ---- passive target (MPI_Win_lock / unlock / flush) -----------------------------
+struct PassiveReq {               // one request of a mailbox slot (plain data)
+    RmaDesc d;                    // this piece: count, tdisp of its first unit
+    int64_t blob_n = 0;           // int64 words of target layout at the payload slot's start
+    int64_t payload_off = 0;      // payload bytes in the slot (after the layout)
+    int32_t has_fetch = 0;
+    int32_t pad_ = 0;
+};
+struct PassiveSlot {              // mailbox slot (target t, origin o)
+    std::atomic<uint32_t> req;    // origin: +1 after writing r
+    std::atomic<uint32_t> done;   // target: = req once applied
+    std::atomic<int32_t> rc;
+    int32_t pad_;
+    PassiveReq r;
+};
+
+struct PassiveState {
+    RmaWin* w = nullptr;
+    int p = 1, me = 0;
+    Windows win;                          // the communicator's engine windows
+    void* shm = nullptr;
+    size_t shm_bytes = 0;
+    std::atomic<uint32_t>* door = nullptr;    // per target: doorbell of its service thread
+    std::atomic<int32_t>* lock = nullptr;     // per target: 0 free, > 0 readers, -1 writer
+    PassiveSlot* slots = nullptr;             // [target * p + origin]
+    std::thread th;
+    std::atomic<bool> stop{false};
+    std::mutex apply_mu;                      // service thread vs. self-target applies
+    hipStream_t os = nullptr;                 // origin-side copies
+};
+
+namespace {
+
+void futex_wake_all(void* addr)
+{
+    syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr), FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+}
+
+void futex_wait_ms(void* addr, uint32_t val, long ms)
+{
+    struct timespec ts = {ms / 1000, (ms % 1000) * 1000000};
+    syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr), FUTEX_WAIT, val, &ts, nullptr, 0);
+}
+
+// A shared-memory segment of `bytes` mapped by every rank (collective).
+int shm_collective(Transport* tp, size_t bytes, void** out)
+{
+    *out = nullptr;
+    static std::atomic<int> serial{0};
+    char name[64] = {0};
+    if (tp->rank == 0)
+        snprintf(name, sizeof(name), "/msx_win_%d_%d_%ld", (int)getpid(), serial.fetch_add(1),
+                 (long)(now_s() * 1e6) % 1000000000L);
+    // rank 0 creates and sizes the segment BEFORE anyone learns its name
+    int fd = -1;
+    if (tp->rank == 0) {
+        fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) name[0] = 0;
+    }
+    std::vector<char> all((size_t)tp->size * sizeof(name));
+    int rc = tp->allgather(name, sizeof(name), all.data());
+    if (rc != MPI_SUCCESS) {
+        if (fd >= 0) close(fd);
+        return rc;
+    }
+    memcpy(name, all.data(), sizeof(name));
+    int ok = name[0] != 0;
+    if (ok && tp->rank != 0) fd = shm_open(name, O_RDWR, 0600);
+    std::vector<int> oks((size_t)tp->size);
+    void* m = MAP_FAILED;
+    if (ok && fd >= 0) m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (fd >= 0) close(fd);
+    int mine = m != MAP_FAILED ? 1 : 0;
+    rc = tp->allgather(&mine, sizeof(int), oks.data());
+    if (tp->rank == 0) shm_unlink(name);
+    bool all_ok = rc == MPI_SUCCESS && mine;
+    for (int v : oks) all_ok = all_ok && v;
+    if (!all_ok) {
+        if (m != MAP_FAILED) munmap(m, bytes);
+        set_error("passive target: shared-memory mailbox unavailable");
+        return rc != MPI_SUCCESS ? rc : MPI_ERR_NO_MEM;
+    }
+    *out = m;                     // zero-filled by ftruncate
+    return MPI_SUCCESS;
+}
+
+// Target side: apply one request of origin o to this rank's window memory.
+int passive_apply(PassiveState* ps, int o, const PassiveReq& r)
+{
+    std::lock_guard<std::mutex> g(ps->apply_mu);
+    const RmaDesc& d = r.d;
+    const char* slot = ps->win.rma_in(ps->me, o);
+    Dtype* T = nullptr;
+    if (r.blob_n > 0) {
+        std::vector<int64_t> blob((size_t)r.blob_n);
+        int rc = copy_any(blob.data(), slot, (size_t)r.blob_n * sizeof(int64_t));
+        if (rc != MPI_SUCCESS) return rc;
+        T = dtype_from_blob(blob.data(), r.blob_n);
+        if (!T) { set_error("passive target: malformed datatype layout"); return MPI_ERR_INTERN; }
+    }
+    static thread_local hipStream_t s = [] {
+        hipStream_t t = nullptr;
+        (void)hipStreamCreateWithFlags(&t, hipStreamNonBlocking);
+        return t;
+    }();
+    const char* payload = slot + r.payload_off;
+    char* fetch = r.has_fetch ? ps->win.rma_fetch(o, ps->me) : nullptr;
+    int rc = rma_apply(d, T, payload, payload + d.usize, ps->w->base + d.tdisp, fetch, s);
+    const int rs = sync_stream(s, "passive apply");
+    if (T) dtype_delete(T);
+    return rc != MPI_SUCCESS ? rc : rs;
+}
+
+// The service thread of one window: applies every origin's requests in
+// arrival order, whatever this rank's own thread is doing.
+void passive_serve(PassiveState* ps)
+{
+    (void)ensure_device();
+    std::atomic<uint32_t>& door = ps->door[ps->me];
+    for (;;) {
+        const uint32_t d0 = door.load(std::memory_order_acquire);
+        bool any = false;
+        for (int o = 0; o < ps->p; ++o) {
+            PassiveSlot& sl = ps->slots[(size_t)ps->me * ps->p + o];
+            const uint32_t q = sl.req.load(std::memory_order_acquire);
+            if (q == sl.done.load(std::memory_order_relaxed)) continue;
+            any = true;
+            const int rc = passive_apply(ps, o, sl.r);
+            sl.rc.store(rc, std::memory_order_relaxed);
+            sl.done.store(q, std::memory_order_release);
+            futex_wake_all(&sl.done);
+        }
+        if (any) continue;
+        if (ps->stop.load(std::memory_order_acquire)) return;
+        futex_wait_ms(&door, d0, 100);
+    }
+}
+
+int passive_lock(PassiveState* ps, int t, int mode)
+{
+    std::atomic<int32_t>& lk = ps->lock[t];
+    const double t_end = now_s() + 600.0;
+    for (int spin = 0;; ++spin) {
+        int32_t v = lk.load(std::memory_order_acquire);
+        if (mode == MPI_LOCK_EXCLUSIVE ? v == 0 : v >= 0) {
+            const int32_t nv = mode == MPI_LOCK_EXCLUSIVE ? -1 : v + 1;
+            if (lk.compare_exchange_weak(v, nv, std::memory_order_acq_rel)) return MPI_SUCCESS;
+            continue;
+        }
+        if (now_s() > t_end) {
+            set_error("MPI_Win_lock: lock of rank %d not granted within 600 s", t);
+            return MPI_ERR_OTHER;
+        }
+        if (spin < 1000) sched_yield();
+        else futex_wait_ms(&lk, (uint32_t)v, 10);
+    }
+}
+
+void passive_unlock(PassiveState* ps, int t, int mode)
+{
+    std::atomic<int32_t>& lk = ps->lock[t];
+    if (mode == MPI_LOCK_EXCLUSIVE) lk.store(0, std::memory_order_release);
+    else lk.fetch_sub(1, std::memory_order_acq_rel);
+    futex_wake_all(&lk);
+}
+
+// Origin side: ship one queued operation to target t piece by piece (payload
+// slot capacity) and wait for each piece to be applied.
+int passive_ship(PassiveState* ps, int t, const RmaDesc& d0, const RmaLocal& l, const int64_t* blob, int64_t blob_n)
+{
+    const size_t S = ps->win.rma_slot();
+    const size_t blob_b = ((size_t)blob_n * sizeof(int64_t) + 255) & ~(size_t)255;
+    const bool sends = d0.kind == RMA_PUT || d0.kind == RMA_CAS ||
+                       ((d0.kind == RMA_ACC || d0.kind == RMA_GACC) && d0.opidx != O_NOOP);
+    const bool fetches = d0.kind == RMA_GET || d0.kind == RMA_GACC || d0.kind == RMA_CAS;
+    const size_t esz = (size_t)d0.usize;
+    const size_t unit_in = sends ? esz * (d0.kind == RMA_CAS ? 2 : 1) : 0;
+    if (blob_b + unit_in > S || esz > S) {
+        set_error("passive target: a %zu-byte unit does not fit the %zu-byte staging slot", esz, S);
+        return MPI_ERR_TYPE;
+    }
+    const int64_t n = d0.kind == RMA_CAS ? 1 : d0.count;
+    int64_t per = unit_in ? (int64_t)((S - blob_b) / unit_in) : n;
+    if (fetches) per = std::min<int64_t>(per, (int64_t)(S / esz));
+    per = std::max<int64_t>(per, 1);
+    char* dst = ps->win.rma_in(t, ps->me);
+    PassiveSlot& sl = ps->slots[(size_t)t * ps->p + ps->me];
+    int rc = MPI_SUCCESS;
+    for (int64_t lo = 0; lo < n && rc == MPI_SUCCESS; lo += per) {
+        const int64_t hi = std::min(n, lo + per);
+        if (blob_n) rc = copy_async(dst, blob, (size_t)blob_n * sizeof(int64_t), ps->os);
+        if (rc == MPI_SUCCESS && sends) {
+            if (d0.kind == RMA_CAS) {
+                rc = copy_async(dst + blob_b, l.origin, esz, ps->os);
+                if (rc == MPI_SUCCESS) rc = copy_async(dst + blob_b + esz, l.compare, esz, ps->os);
+            } else {
+                rc = copy_async(dst + blob_b, static_cast<const char*>(l.origin) + lo * esz, (size_t)(hi - lo) * esz,
+                                ps->os);
+            }
+        }
+        if (rc == MPI_SUCCESS) rc = sync_stream(ps->os, "passive payload");
+        if (rc != MPI_SUCCESS) break;
+        PassiveReq& r = sl.r;
+        r.d = d0;
+        r.d.count = d0.kind == RMA_CAS ? 1 : hi - lo;
+        r.d.tdisp = d0.tdisp + lo * d0.uext;
+        r.d.layout = blob_n ? 0 : -1;
+        r.blob_n = blob_n;
+        r.payload_off = (int64_t)blob_b;
+        r.has_fetch = fetches ? 1 : 0;
+        const uint32_t q = sl.req.load(std::memory_order_relaxed) + 1;
+        sl.req.store(q, std::memory_order_release);
+        ps->door[t].fetch_add(1, std::memory_order_acq_rel);
+        futex_wake_all(&ps->door[t]);
+        const double t_end = now_s() + 600.0;
+        for (int spin = 0;; ++spin) {
+            const uint32_t dn = sl.done.load(std::memory_order_acquire);
+            if (dn == q) break;
+            if (now_s() > t_end) {
+                set_error("passive target: rank %d did not apply within 600 s", t);
+                return MPI_ERR_OTHER;
+            }
+            if (spin < 2000) sched_yield();
+            else futex_wait_ms(&sl.done, dn, 10);
+        }
+        rc = sl.rc.load(std::memory_order_relaxed);
+        if (rc == MPI_SUCCESS && fetches)
+            rc = copy_async(static_cast<char*>(l.result) + lo * esz, ps->win.rma_fetch(ps->me, t),
+                            (size_t)(hi - lo) * esz, ps->os);
+        if (rc == MPI_SUCCESS && fetches) rc = sync_stream(ps->os, "passive fetch");
+    }
+    return rc;
+}
+
+int passive_init(RmaWin* w)
+{
+    Comm* c = w->comm;
+    auto* ps = new PassiveState();
+    ps->w = w;
+    ps->p = c->size;
+    ps->me = c->rank;
+    int rc = get_windows(c->tp, &ps->win);
+    const size_t p = (size_t)ps->p;
+    const size_t hdr = ((p * sizeof(std::atomic<uint32_t>) + p * sizeof(std::atomic<int32_t>)) + 63) & ~(size_t)63;
+    ps->shm_bytes = hdr + p * p * sizeof(PassiveSlot);
+    if (rc == MPI_SUCCESS) rc = shm_collective(c->tp, ps->shm_bytes, &ps->shm);
+    if (rc == MPI_SUCCESS && hipStreamCreateWithFlags(&ps->os, hipStreamNonBlocking) != hipSuccess) {
+        set_error("passive target: stream creation failed");
+        rc = MPI_ERR_OTHER;
+    }
+    if (rc != MPI_SUCCESS) {
+        if (ps->shm) munmap(ps->shm, ps->shm_bytes);
+        delete ps;
+        return rc;
+    }
+    char* base = static_cast<char*>(ps->shm);
+    ps->door = reinterpret_cast<std::atomic<uint32_t>*>(base);
+    ps->lock = reinterpret_cast<std::atomic<int32_t>*>(base + p * sizeof(std::atomic<uint32_t>));
+    ps->slots = reinterpret_cast<PassiveSlot*>(base + hdr);
+    ps->th = std::thread(passive_serve, ps);
+    w->passive = ps;
+    return MPI_SUCCESS;
+}
+
+}  // namespace
+
+int engine_rma_free(RmaWin* w)
+{
+    PassiveState* ps = w->passive;
+    if (!ps) return MPI_SUCCESS;
+    ps->stop.store(true, std::memory_order_release);
+    ps->door[ps->me].fetch_add(1, std::memory_order_acq_rel);
+    futex_wake_all(&ps->door[ps->me]);
+    if (ps->th.joinable()) ps->th.join();
+    if (ps->os) (void)hipStreamDestroy(ps->os);
+    munmap(ps->shm, ps->shm_bytes);
+    delete ps;
+    w->passive = nullptr;
+    return MPI_SUCCESS;
+}
+
+int engine_rma_lock(RmaWin* w, int target, int mode)
+{
+    return w->passive ? passive_lock(w->passive, target, mode) : MPI_SUCCESS;
+}
+
+int engine_rma_unlock_target(RmaWin* w, int target)
+{
+    if (w->passive && w->lock_held[(size_t)target]) passive_unlock(w->passive, target, w->lock_mode[(size_t)target]);
+    return MPI_SUCCESS;
+}
+
+int engine_rma_flush(RmaWin* w, int target)
+{
+    PassiveState* ps = w->passive;
+    if (!ps) return MPI_SUCCESS;                    // one rank: every operation was applied at its call
+    int rc = MPI_SUCCESS;
+    bool pending = false;
+    for (const RmaDesc& d : w->q) pending = pending || d.target == target;
+    if (!pending) return MPI_SUCCESS;
+    if (w->lock_mode[(size_t)target] && !w->lock_held[(size_t)target]) {
+        // the lazily requested lock is granted now
+        if ((rc = passive_lock(ps, target, w->lock_mode[(size_t)target])) != MPI_SUCCESS) return rc;
+        w->lock_held[(size_t)target] = 1;
+    }
+    std::vector<RmaDesc> keep_q;
+    std::vector<RmaLocal> keep_l;
+    for (size_t i = 0; i < w->q.size(); ++i) {
+        const RmaDesc& d = w->q[i];
+        if (d.target != target) {
+            keep_q.push_back(d);
+            keep_l.push_back(w->ql[i]);
+            continue;
+        }
+        int r2 = MPI_SUCCESS;
+        if (!rma_in_bounds(d, w->sizes[(size_t)target])) {
+            set_error("RMA operation outside the target window (target %d, disp %lld)", target, (long long)d.tdisp);
+            r2 = MPI_ERR_REQUEST;                   // packethandling.cpp:1339-1383
+        } else if (rc == MPI_SUCCESS) {
+            const int64_t* blob = d.layout >= 0 ? w->blob.data() + d.layout : nullptr;
+            const int64_t blob_n = d.layout >= 0 ? (int64_t)w->blob.size() - d.layout : 0;
+            r2 = passive_ship(ps, target, d, w->ql[i], blob, blob_n);
+        }
+        const int r3 = rma_local_complete(w->ql[i]);
+        if (rc == MPI_SUCCESS) rc = r2 != MPI_SUCCESS ? r2 : r3;
+    }
+    w->q.swap(keep_q);
+    w->ql.swap(keep_l);
+    if (w->q.empty()) w->blob.clear();
+    return rc;
+}
+
+void engine_rma_self_guard(RmaWin* w, bool enter)
+{
+    if (!w->passive) return;
+    if (enter) w->passive->apply_mu.lock();
+    else w->passive->apply_mu.unlock();
 }
 
 int engine_rma_fence(RmaWin* w)

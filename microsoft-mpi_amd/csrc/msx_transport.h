@@ -136,6 +136,7 @@ struct RmaLocal {                // origin-side addresses of a queued operation
     MPI_Datatype result_dt = 0;
     int64_t result_count = 0;
 };
+struct PassiveState;             // passive-target machinery of one window (engine side)
 struct RmaWin {
     int handle = 0;
     Comm* comm = nullptr;
@@ -148,6 +149,14 @@ struct RmaWin {
     std::vector<RmaDesc> q;      // queued remote operations, issue order
     std::vector<RmaLocal> ql;
     std::vector<int64_t> blob;   // serialized derived target layouts of the queued operations
+    // passive target (MPI_Win_lock ... MPI_Win_unlock): per target, the lock
+    // type of the open access epoch (0 = none) and whether it is acquired yet
+    // (remote locks are acquired lazily, at the first flush / unlock, like the
+    // reference's queued lock request, win.cpp:1018-1060)
+    std::vector<int> lock_mode;
+    std::vector<char> lock_held;
+    bool lock_all = false;
+    PassiveState* passive = nullptr;
 };
 // Finish an operation's origin side: unpack a derived result, free temporaries.
 int rma_local_complete(RmaLocal& l);
@@ -158,6 +167,21 @@ int rma_apply_self(RmaWin* w, const RmaDesc& d, const RmaLocal& l, const Dtype* 
 // target in (origin rank, issue) order; fetched values are delivered.  Collective.
 int engine_rma_fence(RmaWin* w);
 int engine_rma_create(RmaWin* w);    // exchange window sizes (collective)
+int engine_rma_free(RmaWin* w);      // stop the passive-target service (collective)
+// Passive target.  Operations of a lock epoch are queued at the origin; a
+// flush / unlock acquires the target's lock (a reader-writer word in shared
+// memory), ships each operation's payload into the target's engine window and
+// a request into the window's shared-memory mailbox, and waits: the TARGET's
+// service thread applies it to its window memory with the op kernels on its
+// own GPU (the target-side apply of packethandling.cpp:2917-3060, made
+// independent of the target's MPI calls) and returns fetched bytes into the
+// origin's window.  One service thread per window serialises all origins, so
+// concurrent accumulates under shared locks are element-wise atomic.
+int engine_rma_lock(RmaWin* w, int target, int mode);      // blocking acquire
+int engine_rma_unlock_target(RmaWin* w, int target);       // release
+int engine_rma_flush(RmaWin* w, int target);               // complete queued ops to target
+// serialises a self-target apply with the window's service thread
+void engine_rma_self_guard(RmaWin* w, bool enter);
 
 // Run `fn` on the collective worker thread, after every collective issued
 // before it (MPI issue order); re-entrant calls from the worker run inline.

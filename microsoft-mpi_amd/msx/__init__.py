@@ -99,6 +99,15 @@ def lib():
         "MPI_Win_create": (i, [p, i64, i, i, i, ctypes.POINTER(i)]),
         "MPI_Win_free": (i, [ctypes.POINTER(i)]),
         "MPI_Win_fence": (i, [i, i]),
+        "MPI_Win_lock": (i, [i, i, i, i]),
+        "MPI_Win_unlock": (i, [i, i]),
+        "MPI_Win_lock_all": (i, [i, i]),
+        "MPI_Win_unlock_all": (i, [i]),
+        "MPI_Win_flush": (i, [i, i]),
+        "MPI_Win_flush_all": (i, [i]),
+        "MPI_Win_flush_local": (i, [i, i]),
+        "MPI_Win_flush_local_all": (i, [i]),
+        "MPI_Win_sync": (i, [i]),
         "MPI_Win_set_errhandler": (i, [i, i]),
         "MPI_Win_get_errhandler": (i, [i, ctypes.POINTER(i)]),
         "MPI_Put": (i, [p, i, i, i, i64, i, i, i]),

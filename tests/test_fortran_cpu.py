@@ -39,6 +39,8 @@ ENTRIES = [
     "type_ub", "type_get_envelope", "type_get_contents", "get_address", "address", "pack", "unpack",
     "pack_size",
     "win_create", "win_free", "win_fence", "win_set_errhandler", "win_get_errhandler", "put", "get",
+    "win_lock", "win_unlock", "win_lock_all", "win_unlock_all", "win_flush", "win_flush_all", "win_flush_local",
+    "win_flush_local_all", "win_sync",
     "accumulate", "get_accumulate", "fetch_and_op", "compare_and_swap",
 ]
 
