@@ -217,3 +217,15 @@ def test_plain_c_program_builds_against_the_headers(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, env={**os.environ, "MSX_SIZE": "1"})
     assert r.returncode == C.MPI_ERR_OTHER
     assert "no usable MI355X" in r.stderr
+
+
+def test_collectives_demo_compiles_as_plain_c(tmp_path):
+    """examples/collectives_demo.c (the whole API surface an MPI application of
+    this path touches) compiles warning-free with gcc against include/mpi.h and
+    links the library; it runs in tests/test_gpu_c_demo.py."""
+    exe = str(tmp_path / "collectives_demo")
+    libdir = os.path.join(msx.REPO_ROOT, "microsoft-mpi_amd", "lib")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(msx.REPO_ROOT, "include"),
+                    os.path.join(msx.REPO_ROOT, "examples", "collectives_demo.c"), "-L", libdir,
+                    "-lmsmpi_mi355x", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    assert os.path.exists(exe)
