@@ -283,6 +283,12 @@ typedef int MPI_Info;
 MPI_METHOD MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info info,
                           MPI_Comm comm, MPI_Win* win);
 MPI_METHOD MPI_Win_free(MPI_Win* win);
+MPI_METHOD MPI_Win_allocate(MPI_Aint size, int disp_unit, MPI_Info info, MPI_Comm comm, void* baseptr,
+                            MPI_Win* win);
+/* memory for RMA and staging (api/mpi_env.cpp:841-945): pinned host memory,
+   which the GPU reads and writes in place over PCIe */
+MPI_METHOD MPI_Alloc_mem(MPI_Aint size, MPI_Info info, void* baseptr);
+MPI_METHOD MPI_Free_mem(void* base);
 MPI_METHOD MPI_Win_fence(int assert, MPI_Win win);
 /* passive-target synchronisation (api/mpi_win.cpp:1153-1990) */
 MPI_METHOD MPI_Win_lock(int lock_type, int rank, int assert, MPI_Win win);

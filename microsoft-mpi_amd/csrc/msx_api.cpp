@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <map>
 #include <chrono>
 #include <mutex>
 #include <stdio.h>
@@ -929,6 +930,71 @@ int rma_op(MPI_Op op, OpRef* r, bool allow_noop)
 
 }  // namespace
 
+// ---- MPI_Alloc_mem / MPI_Free_mem (api/mpi_env.cpp:841-945) ---------------------
+// The reference returns heap memory (MPID_Alloc_mem, mpid/env.cpp:1745).  Here
+// it is pinned host memory when a GPU is present: still ordinary CPU memory,
+// and the combine kernels read and write it in place over PCIe (the zero-copy
+// host path), instead of staging pageable pages.
+namespace {
+std::mutex g_mem_mu;
+std::map<void*, bool> g_mem;          // base -> pinned (hipHostMalloc) or heap
+
+int alloc_mem(MPI_Aint size, void** out)
+{
+    const size_t n = size > 0 ? (size_t)size : 1;
+    void* p = nullptr;
+    bool pinned = false;
+    if (device_count_noinit() > 0 && ensure_device() == MPI_SUCCESS &&
+        hipHostMalloc(&p, n, hipHostMallocDefault) == hipSuccess) {
+        pinned = true;
+    } else {
+        (void)hipGetLastError();
+        p = malloc(n);
+    }
+    if (!p) { set_error("MPI_Alloc_mem: %lld bytes not available (**allocmem)", (long long)size); return MPI_ERR_NO_MEM; }
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    g_mem[p] = pinned;
+    *out = p;
+    return MPI_SUCCESS;
+}
+
+int free_mem(void* base)
+{
+    bool pinned;
+    {
+        std::lock_guard<std::mutex> g(g_mem_mu);
+        auto it = g_mem.find(base);
+        if (it == g_mem.end()) { set_error("memory %p was not allocated by MPI_Alloc_mem", base); return MPI_ERR_BASE; }
+        pinned = it->second;
+        g_mem.erase(it);
+    }
+    if (pinned) (void)hipHostFree(base);
+    else free(base);
+    return MPI_SUCCESS;
+}
+}  // namespace
+
+MSX_EXPORT int MPI_Alloc_mem(MPI_Aint size, MPI_Info info, void* baseptr)
+{
+    MSX_REQUIRE_INIT("MPI_Alloc_mem");
+    int rc = MPI_SUCCESS;
+    if (size < 0) { set_error("negative size %lld (**argneg)", (long long)size); rc = MPI_ERR_ARG; }
+    else if (!baseptr) { set_error("null baseptr"); rc = MPI_ERR_ARG; }
+    else if (info != MPI_INFO_NULL) { set_error("only MPI_INFO_NULL is supported"); rc = MPI_ERR_INFO; }
+    void* p = nullptr;
+    if (rc == MPI_SUCCESS) rc = alloc_mem(size, &p);
+    if (rc == MPI_SUCCESS) *static_cast<void**>(baseptr) = p;
+    return err_return(nullptr, "MPI_Alloc_mem", rc);
+}
+
+// mpi_env.cpp:920-945: errors are returned, not raised through a handler
+MSX_EXPORT int MPI_Free_mem(void* base)
+{
+    MSX_REQUIRE_INIT("MPI_Free_mem");
+    if (!base) { set_error("null base"); return MPI_ERR_BASE; }
+    return free_mem(base);
+}
+
 MSX_EXPORT int MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info info, MPI_Comm comm,
                               MPI_Win* win)
 {
@@ -962,6 +1028,33 @@ MSX_EXPORT int MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info
     return MPI_SUCCESS;
 }
 
+// MPI_Win_allocate (api/mpi_win.cpp:295-380): MPI_Alloc_mem + MPI_Win_create,
+// the memory freed by MPI_Win_free
+MSX_EXPORT int MPI_Win_allocate(MPI_Aint size, int disp_unit, MPI_Info info, MPI_Comm comm, void* baseptr,
+                                MPI_Win* win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_allocate");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && info != MPI_INFO_NULL) { set_error("only MPI_INFO_NULL is supported"); rc = MPI_ERR_INFO; }
+    if (rc == MPI_SUCCESS && size < 0) { set_error("negative window size (**rmasize)"); rc = MPI_ERR_SIZE; }
+    if (rc == MPI_SUCCESS && disp_unit <= 0) { set_error("disp_unit must be positive"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS && (win == nullptr || baseptr == nullptr)) { set_error("null win / baseptr"); rc = MPI_ERR_ARG; }
+    void* p = nullptr;
+    if (rc == MPI_SUCCESS) rc = alloc_mem(size, &p);
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Win_allocate", rc);
+    rc = MPI_Win_create(p, size, disp_unit, info, comm, win);
+    if (rc != MPI_SUCCESS) {
+        (void)free_mem(p);
+        return rc;                    // already reported by MPI_Win_create
+    }
+    RmaWin* w;
+    (void)v_win(*win, &w);
+    w->owned = p;
+    *static_cast<void**>(baseptr) = p;
+    return MPI_SUCCESS;
+}
+
 MSX_EXPORT int MPI_Win_free(MPI_Win* win)
 {
     MSX_REQUIRE_INIT("MPI_Win_free");
@@ -975,6 +1068,7 @@ MSX_EXPORT int MPI_Win_free(MPI_Win* win)
     rc = coll_barrier(w->comm);       // every rank is done with the window
     if (rc != MPI_SUCCESS) return err_win(w, "MPI_Win_free", rc);
     engine_rma_free(w);               // no request can be in flight after the barrier
+    if (w->owned) (void)free_mem(w->owned);
     {
         std::lock_guard<std::mutex> g(g_win_mu);
         g_wins[(size_t)(*win & 0x03ffffff)] = nullptr;

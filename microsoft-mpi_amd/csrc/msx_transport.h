@@ -157,6 +157,7 @@ struct RmaWin {
     std::vector<char> lock_held;
     bool lock_all = false;
     PassiveState* passive = nullptr;
+    void* owned = nullptr;       // MPI_Win_allocate: memory freed with the window
 };
 // Finish an operation's origin side: unpack a derived result, free temporaries.
 int rma_local_complete(RmaLocal& l);

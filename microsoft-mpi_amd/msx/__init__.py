@@ -97,6 +97,9 @@ def lib():
         "MPI_Iscan": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
         "MPI_Iexscan": (i, [p, p, i, i, i, i, ctypes.POINTER(i)]),
         "MPI_Win_create": (i, [p, i64, i, i, i, ctypes.POINTER(i)]),
+        "MPI_Win_allocate": (i, [i64, i, i, i, p, ctypes.POINTER(i)]),
+        "MPI_Alloc_mem": (i, [i64, i, p]),
+        "MPI_Free_mem": (i, [p]),
         "MPI_Win_free": (i, [ctypes.POINTER(i)]),
         "MPI_Win_fence": (i, [i, i]),
         "MPI_Win_lock": (i, [i, i, i, i]),

@@ -229,3 +229,23 @@ def test_collectives_demo_compiles_as_plain_c(tmp_path):
                     os.path.join(msx.REPO_ROOT, "examples", "collectives_demo.c"), "-L", libdir,
                     "-lmsmpi_mi355x", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
     assert os.path.exists(exe)
+
+
+def test_alloc_mem_validation_without_gpu():
+    """MPI_Alloc_mem / MPI_Free_mem argument checks (api/mpi_env.cpp:841-945):
+    negative size -> MPI_ERR_ARG, null or foreign base -> MPI_ERR_BASE; the
+    memory itself is plain host memory the caller can use."""
+    import ctypes
+    L = msx.init(errors_return=True)
+    p = ctypes.c_void_p()
+    assert L.MPI_Alloc_mem(-1, C.MPI_INFO_NULL, ctypes.byref(p)) == C.MPI_ERR_ARG
+    assert L.MPI_Alloc_mem(64, C.MPI_INFO_NULL, None) == C.MPI_ERR_ARG
+    assert L.MPI_Alloc_mem(4096, C.MPI_INFO_NULL, ctypes.byref(p)) == 0 and p.value
+    buf = (ctypes.c_char * 4096).from_address(p.value)
+    buf[:] = b"\x5a" * 4096
+    assert bytes(buf[:4]) == b"ZZZZ"
+    assert L.MPI_Free_mem(None) == C.MPI_ERR_BASE
+    other = ctypes.create_string_buffer(16)
+    assert L.MPI_Free_mem(ctypes.addressof(other)) == C.MPI_ERR_BASE
+    assert L.MPI_Free_mem(p) == 0
+    assert L.MPI_Free_mem(p) == C.MPI_ERR_BASE          # not twice

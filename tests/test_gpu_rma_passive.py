@@ -161,6 +161,22 @@ if wonall[0] != 1:
     fails.append(f"{wonall[0]} CAS winners")
 L.MPI_Type_free(ctypes.byref(T))
 ok(L.MPI_Win_free(ctypes.byref(win)), "free")
+
+# MPI_Win_allocate: pinned host memory owned by the window; every rank adds 1
+# to its own element of every window under lock_all
+bp, w2 = ctypes.c_void_p(), ctypes.c_int()
+ok(L.MPI_Win_allocate(4 * 64, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(bp), ctypes.byref(w2)), "win_allocate")
+arr = np.ctypeslib.as_array((ctypes.c_int * 64).from_address(bp.value))
+arr[:] = 0
+L.MPI_Barrier(C.MPI_COMM_WORLD)
+ok(L.MPI_Win_lock_all(0, w2.value), "lock_all 2")
+for t in range(p):
+    ok(L.MPI_Accumulate(one.ctypes.data, 1, C.MPI_INT, t, rank, 1, C.MPI_INT, C.MPI_SUM, w2.value), "acc 2")
+ok(L.MPI_Win_unlock_all(w2.value), "unlock_all 2")
+L.MPI_Barrier(C.MPI_COMM_WORLD)
+if not (np.all(arr[:p] == 1) and np.all(arr[p:] == 0)):
+    fails.append(f"win_allocate contents {arr[:p + 1]}")
+ok(L.MPI_Win_free(ctypes.byref(w2)), "free 2")
 print("RESULT", rank, p, len(fails), fails[:6], flush=True)
 L.MPI_Finalize()
 '''
