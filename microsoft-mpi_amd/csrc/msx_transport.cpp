@@ -2337,7 +2337,7 @@ int shm_collective(Transport* tp, size_t bytes, void** out)
 }
 
 // Target side: apply one request of origin o to this rank's window memory.
-int passive_apply(PassiveState* ps, int o, const PassiveReq& r)
+int passive_apply(PassiveState* ps, int o, const PassiveReq& r, hipStream_t s)
 {
     std::lock_guard<std::mutex> g(ps->apply_mu);
     const RmaDesc& d = r.d;
@@ -2350,11 +2350,6 @@ int passive_apply(PassiveState* ps, int o, const PassiveReq& r)
         T = dtype_from_blob(blob.data(), r.blob_n);
         if (!T) { set_error("passive target: malformed datatype layout"); return MPI_ERR_INTERN; }
     }
-    static thread_local hipStream_t s = [] {
-        hipStream_t t = nullptr;
-        (void)hipStreamCreateWithFlags(&t, hipStreamNonBlocking);
-        return t;
-    }();
     const char* payload = slot + r.payload_off;
     char* fetch = r.has_fetch ? ps->win.rma_fetch(o, ps->me) : nullptr;
     int rc = rma_apply(d, T, payload, payload + d.usize, ps->w->base + d.tdisp, fetch, s);
@@ -2368,6 +2363,8 @@ int passive_apply(PassiveState* ps, int o, const PassiveReq& r)
 void passive_serve(PassiveState* ps)
 {
     (void)ensure_device();
+    hipStream_t s = nullptr;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     std::atomic<uint32_t>& door = ps->door[ps->me];
     for (;;) {
         const uint32_t d0 = door.load(std::memory_order_acquire);
@@ -2377,15 +2374,16 @@ void passive_serve(PassiveState* ps)
             const uint32_t q = sl.req.load(std::memory_order_acquire);
             if (q == sl.done.load(std::memory_order_relaxed)) continue;
             any = true;
-            const int rc = passive_apply(ps, o, sl.r);
+            const int rc = s ? passive_apply(ps, o, sl.r, s) : MPI_ERR_OTHER;
             sl.rc.store(rc, std::memory_order_relaxed);
             sl.done.store(q, std::memory_order_release);
             futex_wake_all(&sl.done);
         }
         if (any) continue;
-        if (ps->stop.load(std::memory_order_acquire)) return;
+        if (ps->stop.load(std::memory_order_acquire)) break;
         futex_wait_ms(&door, d0, 100);
     }
+    if (s) (void)hipStreamDestroy(s);
 }
 
 int passive_lock(PassiveState* ps, int t, int mode)
