@@ -213,6 +213,9 @@ double MPIAPI MPI_Wtime(void);
 MPI_METHOD MPI_Comm_rank(MPI_Comm comm, int* rank);
 MPI_METHOD MPI_Comm_size(MPI_Comm comm, int* size);
 MPI_METHOD MPI_Barrier(MPI_Comm comm);
+MPI_METHOD MPI_Comm_split(MPI_Comm comm, int color, int key, MPI_Comm* newcomm);
+MPI_METHOD MPI_Comm_dup(MPI_Comm comm, MPI_Comm* newcomm);
+MPI_METHOD MPI_Comm_free(MPI_Comm* comm);
 MPI_METHOD MPI_Comm_set_errhandler(MPI_Comm comm, MPI_Errhandler errhandler);
 MPI_METHOD MPI_Comm_get_errhandler(MPI_Comm comm, MPI_Errhandler* errhandler);
 MPI_METHOD MPI_Error_class(int errorcode, int* errorclass);

@@ -320,6 +320,58 @@ MSX_EXPORT int MPI_Comm_size(MPI_Comm comm, int* size)
     return MPI_SUCCESS;
 }
 
+// ---- derived communicators (api/mpi_comm.cpp: MPI_Comm_split / dup / free) ------
+// Reductions on sub-communicators need them: each group gets its own
+// transport (hub, shared-memory barrier, engine windows) and runs the same
+// reference-order schedules over its own ranks.
+MSX_EXPORT int MPI_Comm_split(MPI_Comm comm, int color, int key, MPI_Comm* newcomm)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_split");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !newcomm) { set_error("null newcomm"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS && color < 0 && color != MPI_UNDEFINED) {
+        set_error("color %d is negative and not MPI_UNDEFINED", color);
+        rc = MPI_ERR_ARG;
+    }
+    Comm* n = nullptr;
+    if (rc == MPI_SUCCESS) rc = engine_comm_split(c, color, key, &n);
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_split", rc);
+    *newcomm = n ? comm_register(n) : MPI_COMM_NULL;
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Comm_dup(MPI_Comm comm, MPI_Comm* newcomm)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_dup");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !newcomm) { set_error("null newcomm"); rc = MPI_ERR_ARG; }
+    Comm* n = nullptr;
+    if (rc == MPI_SUCCESS) rc = engine_comm_split(c, 0, c->rank, &n);   // same group, same order
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_dup", rc);
+    *newcomm = comm_register(n);
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Comm_free(MPI_Comm* comm)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_free");
+    if (!comm) { set_error("null comm"); return err_return(nullptr, "MPI_Comm_free", MPI_ERR_ARG); }
+    Comm* c;
+    int rc = v_comm(*comm, &c);
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_free", rc);
+    if (c == lookup_comm(MPI_COMM_WORLD) || c == lookup_comm(MPI_COMM_SELF)) {
+        set_error("a predefined communicator cannot be freed (**commperm)");
+        return err_return(c, "MPI_Comm_free", MPI_ERR_COMM);
+    }
+    rc = engine_comm_free(c);
+    comm_unregister(c);
+    delete c;
+    *comm = MPI_COMM_NULL;
+    return rc == MPI_SUCCESS ? MPI_SUCCESS : err_return(nullptr, "MPI_Comm_free", rc);
+}
+
 MSX_EXPORT int MPI_Barrier(MPI_Comm comm)
 {
     MSX_REQUIRE_INIT("MPI_Barrier");

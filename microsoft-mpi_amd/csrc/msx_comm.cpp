@@ -36,11 +36,40 @@ bool is_initialized() { return g_init.load(); }
 bool is_finalized() { return g_fini.load(); }
 Comm* world() { return g_init.load() ? &g_world : nullptr; }
 
+// Derived communicators: direct handles 0x84000000 | index (HANDLE_TYPE_DIRECT,
+// kind comm), as MS-MPI numbers them.
+namespace {
+std::mutex g_comm_mu;
+std::vector<Comm*> g_comms;
+constexpr unsigned kCommDirect = 0x84000000u;
+}  // namespace
+
 Comm* lookup_comm(MPI_Comm c)
 {
     if (c == MPI_COMM_WORLD) return &g_world;
     if (c == MPI_COMM_SELF) return &g_self;
-    return nullptr;
+    if (((unsigned)c & 0xfc000000u) != kCommDirect) return nullptr;
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    const size_t idx = (unsigned)c & 0x03ffffffu;
+    return idx < g_comms.size() ? g_comms[idx] : nullptr;
+}
+
+MPI_Comm comm_register(Comm* c)
+{
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    size_t idx = 0;
+    while (idx < g_comms.size() && g_comms[idx]) ++idx;
+    if (idx == g_comms.size()) g_comms.push_back(nullptr);
+    g_comms[idx] = c;
+    c->handle = (MPI_Comm)(kCommDirect | (unsigned)idx);
+    return c->handle;
+}
+
+void comm_unregister(Comm* c)
+{
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    const size_t idx = (unsigned)c->handle & 0x03ffffffu;
+    if (idx < g_comms.size() && g_comms[idx] == c) g_comms[idx] = nullptr;
 }
 
 static int env_int(const char* a, const char* b, int dflt)

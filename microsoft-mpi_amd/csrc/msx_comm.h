@@ -21,8 +21,10 @@ struct Comm {
     Transport* tp = nullptr;   // null when size == 1
 };
 
-// MPI_COMM_WORLD / MPI_COMM_SELF; nullptr for anything else.
+// MPI_COMM_WORLD, MPI_COMM_SELF or a derived communicator; nullptr otherwise.
 Comm* lookup_comm(MPI_Comm c);
+MPI_Comm comm_register(Comm* c);      // assigns c->handle
+void comm_unregister(Comm* c);
 
 // Resolved op (builtin kernel or user function), MPID_Op (include/op.h:82-134).
 struct OpRef {

@@ -166,6 +166,16 @@ FAPI void mpi_comm_size_(const MPI_Fint* comm, MPI_Fint* size, MPI_Fint* ierr) {
 FNAMES(comm_size, COMM_SIZE)
 FAPI void mpi_barrier_(const MPI_Fint* comm, MPI_Fint* ierr) { *ierr = MPI_Barrier(*comm); }
 FNAMES(barrier, BARRIER)
+FAPI void mpi_comm_split_(const MPI_Fint* comm, const MPI_Fint* color, const MPI_Fint* key, MPI_Fint* newcomm,
+                          MPI_Fint* ierr)
+{
+    *ierr = MPI_Comm_split(*comm, *color, *key, newcomm);
+}
+FNAMES(comm_split, COMM_SPLIT)
+FAPI void mpi_comm_dup_(const MPI_Fint* comm, MPI_Fint* newcomm, MPI_Fint* ierr) { *ierr = MPI_Comm_dup(*comm, newcomm); }
+FNAMES(comm_dup, COMM_DUP)
+FAPI void mpi_comm_free_(MPI_Fint* comm, MPI_Fint* ierr) { *ierr = MPI_Comm_free(comm); }
+FNAMES(comm_free, COMM_FREE)
 FAPI void mpi_comm_set_errhandler_(const MPI_Fint* comm, const MPI_Fint* eh, MPI_Fint* ierr)
 {
     *ierr = MPI_Comm_set_errhandler(*comm, *eh);

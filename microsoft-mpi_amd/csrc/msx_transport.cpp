@@ -89,12 +89,9 @@ public:
         if (lfd_ >= 0) close(lfd_);
     }
 
+    // MPI_COMM_WORLD: the hub address from the launcher's environment
     int init(int rank, int size)
     {
-        rank_ = rank;
-        size_ = size;
-        timeout_ = 600.0;
-        if (const char* t = getenv("MSX_BOOTSTRAP_TIMEOUT")) timeout_ = atof(t);
         const char* addr = getenv("MSX_BOOTSTRAP_ADDR");
         if (!addr) addr = getenv("MASTER_ADDR");
         if (!addr) addr = "127.0.0.1";
@@ -102,6 +99,17 @@ public:
         if (const char* v = getenv("MSX_BOOTSTRAP_PORT")) port = atoi(v);
         else if (const char* v = getenv("MASTER_PORT")) port = (atoi(v) + 97) % 65536;
         if (port < 1024) port += 1024;
+        return init_at(rank, size, addr, port, -1);
+    }
+
+    // A derived communicator: its rank 0 already listens on `lfd` (bound to
+    // an ephemeral port published through the parent); the others connect.
+    int init_at(int rank, int size, const char* addr, int port, int lfd)
+    {
+        rank_ = rank;
+        size_ = size;
+        timeout_ = 600.0;
+        if (const char* t = getenv("MSX_BOOTSTRAP_TIMEOUT")) timeout_ = atof(t);
 
         struct addrinfo hints = {}, *res = nullptr;
         hints.ai_family = AF_INET;
@@ -118,15 +126,19 @@ public:
         fd_.assign((size_t)size, -1);
 
         if (rank == 0) {
-            lfd_ = socket(AF_INET, SOCK_STREAM, 0);
             int one = 1;
-            setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-            struct sockaddr_in any = sa;
-            if (bind(lfd_, (struct sockaddr*)&any, sizeof(any)) != 0) {
-                set_error("bootstrap: bind %s:%d: %s", addr, port, strerror(errno));
-                return MPI_ERR_OTHER;
+            if (lfd >= 0) {
+                lfd_ = lfd;
+            } else {
+                lfd_ = socket(AF_INET, SOCK_STREAM, 0);
+                setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+                struct sockaddr_in any = sa;
+                if (bind(lfd_, (struct sockaddr*)&any, sizeof(any)) != 0) {
+                    set_error("bootstrap: bind %s:%d: %s", addr, port, strerror(errno));
+                    return MPI_ERR_OTHER;
+                }
+                listen(lfd_, size + 8);
             }
-            listen(lfd_, size + 8);
             const double t_end = now_s() + timeout_;
             for (int got = 1; got < size;) {
                 struct pollfd pf = {lfd_, POLLIN, 0};
@@ -294,11 +306,11 @@ public:
         if (stream_) (void)hipStreamDestroy(stream_);
     }
 
-    int init(int r, int s)
+    int init(int r, int s, int port = 0, int lfd = -1)
     {
         rank = r;
         size = s;
-        int rc = hub_.init(r, s);
+        int rc = port ? hub_.init_at(r, s, "127.0.0.1", port, lfd) : hub_.init(r, s);
         if (rc != MPI_SUCCESS) return rc;
         double t = 600.0;
         if (const char* v = getenv("MSX_BOOTSTRAP_TIMEOUT")) t = atof(v);
@@ -409,6 +421,75 @@ private:
 };
 
 }  // namespace
+
+// Listening socket on an ephemeral loopback port (a derived communicator's hub).
+static int listen_ephemeral(int* port)
+{
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) return -1;
+    struct sockaddr_in sa = {};
+    sa.sin_family = AF_INET;
+    sa.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    sa.sin_port = 0;
+    socklen_t len = sizeof(sa);
+    if (bind(fd, (struct sockaddr*)&sa, sizeof(sa)) != 0 || listen(fd, 64) != 0 ||
+        getsockname(fd, (struct sockaddr*)&sa, &len) != 0) {
+        close(fd);
+        return -1;
+    }
+    *port = ntohs(sa.sin_port);
+    return fd;
+}
+
+int transport_split(Transport* parent, int color, int key, int* new_rank, int* new_size, Transport** out)
+{
+    *out = nullptr;
+    *new_rank = -1;
+    *new_size = 0;
+    const int p = parent->size;
+    // MPIR_Comm_split: (color, key) of every rank; members of a color ordered
+    // by (key, parent rank)
+    int32_t mine[2] = {color, key};
+    std::vector<int32_t> all((size_t)p * 2);
+    int rc = parent->allgather(mine, sizeof(mine), all.data());
+    if (rc != MPI_SUCCESS) return rc;
+    std::vector<std::pair<std::pair<int, int>, int>> members;   // ((key, parent rank), parent rank)
+    if (color != MPI_UNDEFINED)
+        for (int r = 0; r < p; ++r)
+            if (all[(size_t)r * 2] == color) members.push_back({{all[(size_t)r * 2 + 1], r}, r});
+    std::sort(members.begin(), members.end());
+    for (size_t i = 0; i < members.size(); ++i)
+        if (members[i].second == parent->rank) *new_rank = (int)i;
+    *new_size = (int)members.size();
+    // the new rank 0 of every group of >= 2 opens the group's hub
+    int32_t port = 0;
+    int lfd = -1;
+    if (*new_rank == 0 && *new_size > 1) {
+        int pt = 0;
+        lfd = listen_ephemeral(&pt);
+        port = lfd >= 0 ? pt : -1;
+    }
+    std::vector<int32_t> ports((size_t)p);
+    rc = parent->allgather(&port, sizeof(port), ports.data());
+    if (rc != MPI_SUCCESS || *new_size <= 1) {
+        if (lfd >= 0) close(lfd);
+        return rc;
+    }
+    const int leader_port = ports[(size_t)members[0].second];
+    if (leader_port <= 0) {
+        if (lfd >= 0) close(lfd);
+        set_error("communicator split: the group's bootstrap socket could not be opened");
+        return MPI_ERR_OTHER;
+    }
+    auto* t = new IpcTransport();
+    rc = t->init(*new_rank, *new_size, leader_port, lfd);
+    if (rc != MPI_SUCCESS) {
+        delete t;
+        return rc;
+    }
+    *out = t;
+    return MPI_SUCCESS;
+}
 
 int transport_create(int rank, int size, Transport** out)
 {
@@ -2657,5 +2738,41 @@ const char* engine_transport_name(Transport* tp)
 }
 
 std::shared_future<int> engine_async(std::function<int()> fn) { return worker().submit(std::move(fn)); }
+
+int engine_comm_split(Comm* parent, int color, int key, Comm** out)
+{
+    *out = nullptr;
+    return worker().run([parent, color, key, out]() -> int {
+        int nr = 0, ns = 1;
+        Transport* t = nullptr;
+        if (parent->tp) {
+            const int rc = transport_split(parent->tp, color, key, &nr, &ns, &t);
+            if (rc != MPI_SUCCESS) return rc;
+        } else if (color == MPI_UNDEFINED) {
+            ns = 0;
+        }
+        if (ns == 0 || nr < 0) return MPI_SUCCESS;         // MPI_COMM_NULL
+        Comm* c = new Comm();
+        c->rank = nr;
+        c->size = ns;
+        c->errhandler = parent->errhandler;                 // inherited from the parent
+        c->tp = t;
+        *out = c;
+        return MPI_SUCCESS;
+    });
+}
+
+int engine_comm_free(Comm* c)
+{
+    return worker().run([c]() -> int {
+        int rc = MPI_SUCCESS;
+        if (c->tp) {
+            rc = c->tp->barrier();                          // no peer still uses its windows
+            transport_destroy(c->tp);
+            c->tp = nullptr;
+        }
+        return rc;
+    });
+}
 
 }  // namespace msx

@@ -47,6 +47,10 @@ public:
 };
 
 int transport_create(int rank, int size, Transport** out);
+// MPI_Comm_split over `parent` (collective): this rank's place in its color's
+// group and, for groups of two or more, the group's own transport (hub,
+// shared-memory barrier, engine windows).  color MPI_UNDEFINED: no group.
+int transport_split(Transport* parent, int color, int key, int* new_rank, int* new_size, Transport** out);
 // window-allreduce phase timers (seconds): stage+scatter, collect wait+barrier A,
 // reduce+push, barrier B, last collect, chunks, calls; returns 7
 int engine_stats(double* out, int n, int reset);
@@ -187,5 +191,12 @@ void engine_rma_self_guard(RmaWin* w, bool enter);
 // Run `fn` on the collective worker thread, after every collective issued
 // before it (MPI issue order); re-entrant calls from the worker run inline.
 std::shared_future<int> engine_async(std::function<int()> fn);
+
+// MPI_Comm_split / MPI_Comm_dup (collective over `parent`, in issue order with
+// its collectives): *out = the new communicator, or nullptr for
+// MPI_COMM_NULL (color MPI_UNDEFINED).  The handle is assigned by the caller.
+int engine_comm_split(Comm* parent, int color, int key, Comm** out);
+// MPI_Comm_free (collective): tears down the communicator's transport.
+int engine_comm_free(Comm* c);
 
 }  // namespace msx

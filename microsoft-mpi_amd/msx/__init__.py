@@ -76,6 +76,9 @@ def lib():
         "MPI_Comm_rank": (i, [i, ctypes.POINTER(i)]),
         "MPI_Comm_size": (i, [i, ctypes.POINTER(i)]),
         "MPI_Barrier": (i, [i]),
+        "MPI_Comm_split": (i, [i, i, i, ctypes.POINTER(i)]),
+        "MPI_Comm_dup": (i, [i, ctypes.POINTER(i)]),
+        "MPI_Comm_free": (i, [ctypes.POINTER(i)]),
         "MPI_Comm_set_errhandler": (i, [i, i]),
         "MPI_Error_class": (i, [i, ctypes.POINTER(i)]),
         "MPI_Type_size": (i, [i, ctypes.POINTER(i)]),

@@ -400,3 +400,87 @@ def test_four_mpi_processes_user_op_scan_follows_reference_task_order():
     assert rsv[0] == 30.0 and rsv[1] == -30.0
     assert [got[k][0] for k in range(4)] == [10.0, -10.0, -40.0, 0.0]
     assert [got[k][1] for k in range(4)] == [7.0, 10.0, -10.0, -40.0]
+
+
+SPLIT_WORKER = r'''
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
+import numpy as np
+import msx
+C = msx.C
+L = msx.init(errors_return=True)
+r = ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r))
+rank = r.value
+UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+def sub(a, b, n, dt):   # non-commutative: inout = in - inout
+    x = np.ctypeslib.as_array((ctypes.c_double * n[0]).from_address(a))
+    y = np.ctypeslib.as_array((ctypes.c_double * n[0]).from_address(b))
+    y[:] = x - y
+fn = UF(sub)
+op = ctypes.c_int()
+assert L.MPI_Op_create(fn, 0, ctypes.byref(op)) == 0
+for f in (L.MPI_Allreduce, L.MPI_Scan):
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+# split WORLD (5 ranks) by parity, keys reversing the order: odd = {3, 1},
+# even = {4, 2, 0}; rank 4 is then rank 0 of the even group
+sub_c = ctypes.c_int()
+assert L.MPI_Comm_split(C.MPI_COMM_WORLD, rank % 2, -rank, ctypes.byref(sub_c)) == 0, msx.last_error()
+sr, ss = ctypes.c_int(), ctypes.c_int()
+L.MPI_Comm_rank(sub_c.value, ctypes.byref(sr)); L.MPI_Comm_size(sub_c.value, ctypes.byref(ss))
+x = np.array([float(10 * (rank + 1))])
+inc, out = np.zeros(1), np.zeros(1)
+assert L.MPI_Scan(x.ctypes.data, inc.ctypes.data, 1, C.MPI_DOUBLE, op.value, sub_c.value) == 0, msx.last_error()
+assert L.MPI_Allreduce(x.ctypes.data, out.ctypes.data, 1, C.MPI_DOUBLE, op.value, sub_c.value) == 0
+# a duplicate of WORLD, and MPI_UNDEFINED -> MPI_COMM_NULL
+dup, none = ctypes.c_int(), ctypes.c_int()
+assert L.MPI_Comm_dup(C.MPI_COMM_WORLD, ctypes.byref(dup)) == 0
+ds = ctypes.c_int(); L.MPI_Comm_size(dup.value, ctypes.byref(ds))
+allw = np.zeros(1)
+assert L.MPI_Allreduce(x.ctypes.data, allw.ctypes.data, 1, C.MPI_DOUBLE, op.value, dup.value) == 0
+assert L.MPI_Comm_split(C.MPI_COMM_WORLD, 0 if rank == 2 else C.MPI_UNDEFINED, 0, ctypes.byref(none)) == 0
+solo = none.value
+if rank == 2:
+    s1 = ctypes.c_int(); L.MPI_Comm_size(solo, ctypes.byref(s1)); assert s1.value == 1
+    assert L.MPI_Comm_free(ctypes.byref(none)) == 0
+else:
+    assert solo == C.MPI_COMM_NULL
+errs = [L.MPI_Comm_split(C.MPI_COMM_WORLD, -5, 0, ctypes.byref(none)),
+        L.MPI_Comm_free(ctypes.byref(ctypes.c_int(C.MPI_COMM_WORLD)))]
+assert L.MPI_Comm_free(ctypes.byref(sub_c)) == 0 and sub_c.value == C.MPI_COMM_NULL
+assert L.MPI_Comm_free(ctypes.byref(dup)) == 0
+print("OUT", rank, sr.value, ss.value, inc[0], out[0], ds.value, allw[0], errs[0], errs[1], flush=True)
+assert L.MPI_Finalize() == 0
+'''
+
+
+def test_comm_split_dup_free_with_user_ops():
+    """MPI_Comm_split / dup / free (api/mpi_comm.cpp): groups ordered by
+    (key, rank), each with its own transport; a non-commutative user op pins
+    the group order through the reference's scan and allreduce associations.
+    The negative-color split is collective (all 5 ranks call it) and rejected
+    on every rank before any exchange."""
+    port = _free_port()
+    outs = _spawn(SPLIT_WORKER, 5, lambda r: {"MSX_SIZE": "5", "MSX_RANK": str(r),
+                                              "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1"})
+    got = {}
+    for rc, o, e in outs:
+        assert rc == 0, e[-3000:]
+        f = [l for l in o.splitlines() if l.startswith("OUT")][0].split()[1:]
+        got[int(f[0])] = f[1:]
+    x = {r: 10.0 * (r + 1) for r in range(5)}
+    # even group in sub-rank order: world 4, 2, 0 (values 50, 30, 10); odd: 3, 1 (40, 20)
+    exp_sub = {4: (0, 3), 2: (1, 3), 0: (2, 3), 3: (0, 2), 1: (1, 2)}
+    for r in range(5):
+        sr, ss = int(got[r][0]), int(got[r][1])
+        assert (sr, ss) == exp_sub[r], (r, got[r])
+    # scan, a op b = a - b, recursive doubling: sub-rank 1 -> y0 - y1, sub-rank 2 -> (y0 - y1) - y2
+    assert float(got[4][2]) == 50.0 and float(got[2][2]) == 50.0 - 30.0 and float(got[0][2]) == (50.0 - 30.0) - 10.0
+    assert float(got[3][2]) == 40.0 and float(got[1][2]) == 40.0 - 20.0
+    # allreduce in the odd group (p = 2): y0 - y1 = 20 on both ranks
+    assert float(got[3][3]) == 20.0 and float(got[1][3]) == 20.0
+    for r in range(5):
+        assert int(got[r][4]) == 5
+        assert int(got[r][6]) == C.MPI_ERR_ARG and int(got[r][7]) == C.MPI_ERR_COMM
+    # the duplicate of WORLD reduces like WORLD: every rank gets the same value
+    assert len({got[r][5] for r in range(5)}) == 1

@@ -26,7 +26,7 @@ FLANG = "/opt/rocm/lib/llvm/bin/flang"
 
 ENTRIES = [
     "init", "init_thread", "finalize", "initialized", "finalized", "abort", "wtime", "comm_rank",
-    "comm_size", "barrier", "comm_set_errhandler", "comm_get_errhandler", "error_class", "error_string",
+    "comm_size", "barrier", "comm_split", "comm_dup", "comm_free", "comm_set_errhandler", "comm_get_errhandler", "error_class", "error_string",
     "op_create", "op_commutative", "op_free",
     "reduce_local", "reduce", "ireduce", "allreduce", "iallreduce", "reduce_scatter", "ireduce_scatter",
     "reduce_scatter_block", "ireduce_scatter_block", "scan", "iscan", "exscan", "iexscan",
