@@ -62,6 +62,13 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
 // barrier-free small allreduce, posted after the data kernel on the same stream.
 hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned long long seq, hipStream_t s);
 
+// The barrier-free allreduce's push: copy nseg ranges (one grid row each) and,
+// once every workgroup's stores are visible system-wide, store `seq` to every
+// flags[i] -- one launch, the flag ordered after the data by the kernel itself.
+hipError_t launch_push_post(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
+                            unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
+                            hipStream_t s);
+
 // Copy nseg independent byte ranges in one launch (one grid row per segment),
 // used to pull allgather blocks from every peer concurrently.
 hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size_t* nbytes,

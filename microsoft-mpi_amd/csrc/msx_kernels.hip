@@ -384,6 +384,43 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
     if (c.sys) release_system();
 }
 
+// The small-allreduce push with its arrival flags in one launch: every
+// workgroup copies its part of its segment, waits until its stores are
+// complete, and counts itself done; the last one posts `seq` into every
+// peer's flag slot (the threadFenceReduction pattern: the flag can never
+// overtake the data).  The windows are uncached, so store completion is
+// visibility; with cached windows (sys) each workgroup also writes its L2
+// back at system scope.
+__global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
+                                                   int sys)
+{
+    const int sg = blockIdx.y;
+    const char* src = static_cast<const char*>(c.src[sg]);
+    char* dst = static_cast<char*>(c.dst[sg]);
+    const size_t nb = c.nbytes[sg];
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t done = 0;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const size_t nv = nb / 16;
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride)
+            reinterpret_cast<u32x4*>(dst)[i] = reinterpret_cast<const u32x4*>(src)[i];
+        done = nv * 16;
+    }
+    for (size_t i = done + (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
+    if (sys) __threadfence_system();
+    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");    // this wave's stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == total - 1) {
+            if (sys) __threadfence_system();
+            for (int k = 0; k < f.n; ++k)
+                __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
+        }
+    }
+}
+
 }  // namespace dev
 
 // =====================================================================================
@@ -730,6 +767,39 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     case O_MINLOC: return tree_loc<O_MINLOC>(k, a, ns, out, n, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_push_post(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
+                            unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
+                            hipStream_t s)
+{
+    static unsigned* counter = [] {
+        unsigned* c = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&c), sizeof(unsigned)) != hipSuccess) return (unsigned*)nullptr;
+        (void)hipMemset(c, 0, sizeof(unsigned));
+        (void)hipDeviceSynchronize();
+        return c;
+    }();
+    if (!counter || nseg <= 0 || nseg > kMaxSegs || nflags > 64 || nflags < 0) return hipErrorInvalidValue;
+    CopySegs c{};
+    c.n = nseg;
+    size_t maxb = 0;
+    for (int i = 0; i < nseg; ++i) {
+        c.src[i] = src[i];
+        c.dst[i] = dst[i];
+        c.nbytes[i] = nbytes[i];
+        if (nbytes[i] > maxb) maxb = nbytes[i];
+    }
+    PostFlags f{};
+    for (int i = 0; i < nflags; ++i) f.dst[i] = flags[i];
+    f.n = nflags;
+    f.seq = seq;
+    size_t gx = (maxb / 16 + 255) / 256;
+    if (gx < 1) gx = 1;
+    if (gx > 16) gx = 16;
+    hipLaunchKernelGGL(k_push_post, dim3((unsigned)gx, (unsigned)nseg), dim3(256), 0, s, c, f, counter,
+                       (unsigned)(gx * (size_t)nseg), sys ? 1 : 0);
+    return hipGetLastError();
 }
 
 hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned long long seq, hipStream_t s)

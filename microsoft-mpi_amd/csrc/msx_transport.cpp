@@ -1491,7 +1491,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // recursive doubling -> all ranks evaluate their own lineage's tree;
         // binomial reduce -> only the root evaluates
         const RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
-        if (rd_single && root < 0 && p <= 64 && rd_flags()) {
+        if (rd_single && root < 0 && p <= 32 && rd_flags()) {
             // Allreduce: no host barrier at all.  Each rank pushes its vector
             // into every peer's IN half, then posts the call's sequence number
             // into the peers' flag slots (a second kernel on the same stream:
@@ -1517,9 +1517,13 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             int* err_dev = wait_err_word(&err_host);
             if (!err_dev) { set_error("allreduce: arrival word allocation failed"); return MPI_ERR_NO_MEM; }
             *err_host = 0;
-            if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
-            if (rc == MPI_SUCCESS) {
-                hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);
+            if (rc == MPI_SUCCESS && !sg.src.empty()) {
+                // data and flags in one kernel (the flag ordered after the data)
+                hipError_t e = launch_push_post(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
+                                                fl.data(), (int)fl.size(), seq, sys_fences(), s);
+                if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
+            } else if (rc == MPI_SUCCESS) {
+                hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);   // nothing to push
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce arrival flags");
             }
             if (rc == MPI_SUCCESS) {
