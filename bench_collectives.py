@@ -135,6 +135,19 @@ def main(out_path, scale):
         curve[str(nbytes)] = {"us": round(t * 1e6, 1), "busbw_GB_s": round(nbytes / t / 1e9 * 2 * (p - 1) / p, 2),
                               "correct": bool(torch.equal(b, want))}
     res["allreduce_curve_f32"] = curve
+    # small rooted reduce latency (barrier-free binomial path), same method
+    m = 1024
+    a, out = torch.ones(m, device=dev), torch.zeros(m, device=dev)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(3):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(50):
+            L.MPI_Reduce(a.data_ptr(), out.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, 0, C.MPI_COMM_WORLD)
+        ts.append((time.perf_counter() - t0) / 50)
+    res["reduce_4096B_root0_us"] = {"us": round(sorted(ts)[1] * 1e6, 1),
+                                     "correct": bool(torch.all(out == p).item()) if rank == 0 else None}
     del send, recv, exp
     torch.cuda.empty_cache()
 

@@ -205,10 +205,15 @@ private:
 // on one node: the IPC engine requires it).  Sense-reversing counter: a few
 // microseconds instead of a TCP round trip through the hub.
 // ===========================================================================
+constexpr int kDoneSlots = 480;
 struct ShmBar {
     std::atomic<uint32_t> count;
     std::atomic<uint32_t> gen;
+    // per rank: sequence number of the last barrier-free call it has finished
+    // (its tree has read its IN half), see do_allreduce
+    std::atomic<uint64_t> done[kDoneSlots];
 };
+static_assert(sizeof(ShmBar) <= 4096, "one page");
 
 class ShmBarrier {
 public:
@@ -258,6 +263,17 @@ public:
     }
 
     bool ready() const { return bar_ != nullptr; }
+    bool has_done() const { return bar_ && size_ <= kDoneSlots; }
+    void post_done(int rank, uint64_t v) { bar_->done[rank].store(v, std::memory_order_release); }
+    int wait_done(int rank, uint64_t v)
+    {
+        const double t_end = now_s() + timeout_;
+        for (int spin = 0; bar_->done[rank].load(std::memory_order_acquire) < v; ++spin) {
+            if (now_s() > t_end) { set_error("rank %d did not finish its previous call", rank); return MPI_ERR_OTHER; }
+            if (spin > 2000) sched_yield();
+        }
+        return MPI_SUCCESS;
+    }
 
     int wait()
     {
@@ -319,6 +335,10 @@ public:
     }
 
     int allgather(const void* mine, size_t n, void* all) override { return hub_.allgather(mine, n, all); }
+
+    bool has_done() const override { return shm_.has_done(); }
+    void post_done(uint64_t v) override { shm_.post_done(rank, v); }
+    int wait_done(int r, uint64_t v) override { return shm_.wait_done(r, v); }
 
     int barrier() override
     {
@@ -1491,28 +1511,29 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // recursive doubling -> all ranks evaluate their own lineage's tree;
         // binomial reduce -> only the root evaluates
         const RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
-        if (rd_single && root < 0 && p <= 32 && rd_flags()) {
-            // Allreduce: no host barrier at all.  Each rank pushes its vector
-            // into every peer's IN half, then posts the call's sequence number
-            // into the peers' flag slots (a second kernel on the same stream:
-            // the data stores completed first); the tree kernel waits on the
-            // GPU until all peers' flags reached the sequence.  The half is
-            // reused two calls later only after every peer's tree read it:
-            // a peer posts call k+1 after its call k returned, and this rank
-            // pushes call k+2 after its own call k+1 tree saw those flags.
+        if (rd_single && p <= 32 && rd_flags() && tp->has_done()) {
+            // No host barrier at all.  Each rank pushes its vector into the IN
+            // half of every rank that evaluates a tree (all peers for
+            // allreduce, the root for reduce) and posts the call's sequence
+            // number into their flag slots, in one kernel; the tree kernel
+            // waits on the GPU until all peers' flags reached the sequence.
+            // A half is reused two calls later: before pushing call s into
+            // rank r's half, this rank waits (host, shared memory) until r has
+            // posted that it finished call s-2 -- normally long since true.
             const size_t half = (size_t)tp->rd_parity * Qh;
             for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
             const char* mine = nullptr;
             rc = device_view(bs, src, 0, count * esz, stage, s, &mine);
+            const unsigned long long seq = ++tp->rd_seq;
             Segs sg;
             std::vector<unsigned long long*> fl;
-            for (int r = 0; r < p; ++r)
-                if (r != me) {
+            for (int r = 0; r < p && rc == MPI_SUCCESS; ++r)
+                if (r != me && (root < 0 || r == root)) {
+                    if (seq > 2) rc = tp->wait_done(r, seq - 2);
                     sg.add(mine, w.sub(r, me) + half, count * esz);
                     fl.push_back(w.flags(r) + me);
                 }
             subs[(size_t)me] = const_cast<char*>(mine);
-            const unsigned long long seq = ++tp->rd_seq;
             int* err_host = nullptr;
             int* err_dev = wait_err_word(&err_host);
             if (!err_dev) { set_error("allreduce: arrival word allocation failed"); return MPI_ERR_NO_MEM; }
@@ -1522,11 +1543,11 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 hipError_t e = launch_push_post(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
                                                 fl.data(), (int)fl.size(), seq, sys_fences(), s);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
-            } else if (rc == MPI_SUCCESS) {
+            } else if (rc == MPI_SUCCESS && !fl.empty()) {
                 hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);   // nothing to push
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce arrival flags");
             }
-            if (rc == MPI_SUCCESS) {
+            if (rc == MPI_SUCCESS && want) {
                 TreeWait tw;
                 tw.flags = w.flags(me);
                 tw.seq = seq;
@@ -1543,6 +1564,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 set_error("allreduce: a peer's contribution did not arrive within 20 s");
                 rc = MPI_ERR_OTHER;
             }
+            tp->post_done(seq);                   // this rank's tree no longer reads the half
             tp->rd_parity ^= 1;
             tp->window_open = true;
             trace("allreduce: done (GPU arrival flags, seq %llu) rc=%d", seq, rc);

@@ -38,6 +38,11 @@ public:
     // lock-step host collectives over the bootstrap hub (all ranks, same n)
     virtual int allgather(const void* mine, size_t n, void* all) = 0;
     virtual int barrier() = 0;
+    // Completion words of the barrier-free small calls (node shared memory):
+    // post_done(s) = this rank finished call s; wait_done(r, s) waits for rank r.
+    virtual bool has_done() const { return false; }
+    virtual void post_done(uint64_t) {}
+    virtual int wait_done(int, uint64_t) { return MPI_ERR_OTHER; }
     // Device pointers through which THIS process reads rank r's `ptr`
     // (ptr must be device memory of the calling rank).  Collective.
     virtual int map_peers(const void* ptr, std::vector<char*>& out) = 0;
