@@ -385,12 +385,13 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
 }
 
 // The small-allreduce push with its arrival flags in one launch: every
-// workgroup copies its part of its segment, waits until its stores are
+// workgroup copies its part of its segment with system-coherent stores
+// (sc0 sc1: written through to the owner's memory, never left dirty in this
+// GPU's L2, however the importer maps the peer window), waits until they are
 // complete, and counts itself done; the last one posts `seq` into every
 // peer's flag slot (the threadFenceReduction pattern: the flag can never
-// overtake the data).  The windows are uncached, so store completion is
-// visibility; with cached windows (sys) each workgroup also writes its L2
-// back at system scope.
+// overtake the data).  sys: cached windows, each workgroup also writes its
+// L2 back at system scope.
 __global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
                                                    int sys)
 {
@@ -400,14 +401,24 @@ __global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsi
     const size_t nb = c.nbytes[sg];
     const size_t stride = (size_t)gridDim.x * 256;
     size_t done = 0;
+    bool plain = false;
     if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
         const size_t nv = nb / 16;
-        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride)
-            reinterpret_cast<u32x4*>(dst)[i] = reinterpret_cast<const u32x4*>(src)[i];
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride) {
+            const u32x4 v = reinterpret_cast<const u32x4*>(src)[i];
+            unsigned long long* d = reinterpret_cast<unsigned long long*>(dst) + 2 * i;
+            __hip_atomic_store(d, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(d + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         done = nv * 16;
     }
-    for (size_t i = done + (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
-    if (sys) __threadfence_system();
+    for (size_t i = done + (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) {
+        dst[i] = src[i];
+        plain = true;
+    }
+    if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
     else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");    // this wave's stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
