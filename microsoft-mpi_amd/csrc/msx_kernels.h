@@ -65,9 +65,11 @@ hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned lon
 // The barrier-free allreduce's push: copy nseg ranges (one grid row each) and,
 // once every workgroup's stores are visible system-wide, store `seq` to every
 // flags[i] -- one launch, the flag ordered after the data by the kernel itself.
+// `counter`: a zeroed device word owned by the caller's transport (the kernel
+// leaves it zero again); launches sharing one counter must not overlap.
 hipError_t launch_push_post(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
-                            hipStream_t s);
+                            unsigned* counter, hipStream_t s);
 
 // Copy nseg independent byte ranges in one launch (one grid row per segment),
 // used to pull allgather blocks from every peer concurrently.

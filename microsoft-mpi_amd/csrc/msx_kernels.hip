@@ -204,6 +204,12 @@ __device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
                 __builtin_amdgcn_s_sleep(2);
             }
         }
+        // The acquire that pairs with the pusher's system-scope release of the
+        // flag: invalidates this CU's L1 and the XCD's L2 copies of peer-written
+        // lines, so the IN half is read fresh whatever cache type the window
+        // is mapped with (the UC mapping makes it a no-op for the data today,
+        // but the kernel no longer depends on that allocation property).
+        if (good) (void)__hip_atomic_load(a.wait_flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         ok = good;
     }
     __syncthreads();
@@ -387,11 +393,17 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
 // The small-allreduce push with its arrival flags in one launch: every
 // workgroup copies its part of its segment with system-coherent stores
 // (sc0 sc1: written through to the owner's memory, never left dirty in this
-// GPU's L2, however the importer maps the peer window), waits until they are
-// complete, and counts itself done; the last one posts `seq` into every
-// peer's flag slot (the threadFenceReduction pattern: the flag can never
-// overtake the data).  sys: cached windows, each workgroup also writes its
-// L2 back at system scope.
+// GPU's L2, however the importer maps the peer window).  EVERY lane then
+// fences (agent-scope release: s_waitcnt vmcnt(0), so its own write-through
+// stores have completed at the owner), the workgroup meets at a barrier, and
+// thread 0 counts the workgroup done with an acq_rel add; the last one
+// acquires all the others' completions and posts `seq` into every peer's flag
+// slot with a system-scope release (the threadFenceReduction pattern: no flag
+// can overtake any workgroup's data).  sys: cached windows, each lane writes
+// its L2 back at system scope instead.
+// `counter` belongs to the calling transport (one per communicator, reset by
+// the last workgroup); the transport's collectives are issued one at a time
+// on its stream, so two launches never share it concurrently.
 __global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
                                                    int sys)
 {
@@ -419,10 +431,10 @@ __global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsi
         plain = true;
     }
     if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
-    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");    // this wave's stores have completed
+    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // vmcnt(0): this lane's stores completed
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (old == total - 1) {
             if (sys) __threadfence_system();
             for (int k = 0; k < f.n; ++k)
@@ -782,15 +794,8 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
 
 hipError_t launch_push_post(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
-                            hipStream_t s)
+                            unsigned* counter, hipStream_t s)
 {
-    static unsigned* counter = [] {
-        unsigned* c = nullptr;
-        if (hipMalloc(reinterpret_cast<void**>(&c), sizeof(unsigned)) != hipSuccess) return (unsigned*)nullptr;
-        (void)hipMemset(c, 0, sizeof(unsigned));
-        (void)hipDeviceSynchronize();
-        return c;
-    }();
     if (!counter || nseg <= 0 || nseg > kMaxSegs || nflags > 64 || nflags < 0) return hipErrorInvalidValue;
     CopySegs c{};
     c.n = nseg;

@@ -319,6 +319,7 @@ public:
     {
         for (auto& kv : opened_) (void)hipIpcCloseMemHandle(kv.second);
         if (win_) (void)hipFree(win_);
+        if (counter_) (void)hipFree(counter_);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
 
@@ -352,6 +353,20 @@ public:
     {
         if (!stream_) (void)hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
         return stream_;
+    }
+
+    unsigned* push_counter() override
+    {
+        if (!counter_) {
+            void* c = nullptr;
+            if (hipMalloc(&c, sizeof(unsigned)) != hipSuccess) return nullptr;
+            if (hipMemset(c, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                (void)hipFree(c);
+                return nullptr;
+            }
+            counter_ = static_cast<unsigned*>(c);
+        }
+        return counter_;
     }
 
     int map_peers(const void* ptr, std::vector<char*>& out) override
@@ -434,6 +449,7 @@ private:
     Hub hub_;
     ShmBarrier shm_;
     hipStream_t stream_ = nullptr;
+    unsigned* counter_ = nullptr;
     std::map<std::string, void*> opened_;
     void* win_ = nullptr;
     size_t win_bytes_ = 0;
@@ -1540,8 +1556,10 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             *err_host = 0;
             if (rc == MPI_SUCCESS && !sg.src.empty()) {
                 // data and flags in one kernel (the flag ordered after the data)
+                unsigned* counter = tp->push_counter();
+                if (!counter) { set_error("allreduce: push counter allocation failed"); return MPI_ERR_NO_MEM; }
                 hipError_t e = launch_push_post(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
-                                                fl.data(), (int)fl.size(), seq, sys_fences(), s);
+                                                fl.data(), (int)fl.size(), seq, sys_fences(), counter, s);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
             } else if (rc == MPI_SUCCESS && !fl.empty()) {
                 hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);   // nothing to push

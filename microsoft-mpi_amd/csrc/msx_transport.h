@@ -49,6 +49,10 @@ public:
     // Per-rank device scratch, IPC-mapped once: out[r] = rank r's window.
     virtual int window(size_t bytes, std::vector<char*>& out) = 0;
     virtual hipStream_t stream() = 0;
+    // Completion counter of the fused push (k_push_post): one zeroed device
+    // word per transport, used only by launches on stream(), which the
+    // transport issues one collective at a time.  nullptr if allocation failed.
+    virtual unsigned* push_counter() = 0;
 };
 
 int transport_create(int rank, int size, Transport** out);

@@ -219,9 +219,11 @@ else:
 assert req.value == C.MPI_REQUEST_NULL
 
 # Back-to-back stress of the barrier-free small allreduce (GPU arrival flags,
-# alternating IN halves) interleaved with the other window users: rooted
-# reduce (host barrier), a chunked large allreduce (full barrier first),
-# non-blocking calls through the engine worker, in-place calls.
+# alternating IN halves; with MSX_RD_FLAGS=0 the host-barrier variant)
+# interleaved with the other window users: small rooted reduces (the same
+# arrival-flag path, non-roots push to the root only), a chunked large
+# allreduce (full barrier first), non-blocking calls through the engine
+# worker, in-place calls.
 def ivec(it, r, n):
     return ((np.arange(n, dtype=np.int64) * 7 + it * 31 + r * 1009) % 100003).astype(np.int32)
 
@@ -232,7 +234,7 @@ for it in range(240):
         n = 1 << 18
         tot = sum(ivec(it, r, n).astype(np.int64) for r in range(p)).astype(np.int32)
     sb = todev(ivec(it, rank, n))
-    if it % 7 == 3:                        # rooted reduce: host-barrier variant
+    if it % 7 == 3:                        # rooted reduce: arrival flags, push to the root only
         root = it % p
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
         rc = L.MPI_Reduce(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, root, C.MPI_COMM_WORLD)
@@ -274,10 +276,15 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("p,chunk,transport", [(2, None, None), (3, 65536, None), (4, 1 << 20, None),
-                                               (5, None, None), (3, 65536, "rccl"),
-                                               (8, None, None), (7, 1 << 20, None)])
-def test_collectives_p_ranks_on_one_gpu(p, chunk, transport):
+# Every case runs all p ranks on ONE GPU (the GPU box has one): same-HBM IPC,
+# so these pin the schedules and the flag/barrier protocol, not cross-GPU
+# (xGMI) memory ordering -- that needs the driver's multi-GPU node.
+@pytest.mark.parametrize("p,chunk,transport,rd_flags", [(2, None, None, None), (3, 65536, None, None),
+                                                        (4, 1 << 20, None, None), (5, None, None, None),
+                                                        (3, 65536, "rccl", None), (8, None, None, None),
+                                                        (7, 1 << 20, None, None), (3, None, None, "0"),
+                                                        (4, 65536, None, "0")])
+def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -292,6 +299,8 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport):
             env["MSX_CHUNK_BYTES"] = str(chunk)     # many chunks, pieces across block edges
         if transport:
             env["MSX_TRANSPORT"] = transport
+        if rd_flags is not None:
+            env["MSX_RD_FLAGS"] = rd_flags          # host-barrier small allreduce / reduce
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
