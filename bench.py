@@ -328,12 +328,19 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
         out[f"{opn}/{dtn}"] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1),
                                "frac": round(gbs / HBM_PEAK_GBS, 4)}
     # the collective combine (k_tree): p = 8 contributions of 32 MiB reduced in
-    # the reference's tree order into one output, (p + 1) x 32 MiB of traffic
+    # the reference's tree order into one output, (p + 1) x 32 MiB of traffic.
+    # Sources placed as the engine's window lays out its IN sub-slots (32 MiB
+    # + 68 KiB apart, msx_transport.cpp sub_skew); "tree8_pow2_stride" is the
+    # same call with the sources exactly 32 MiB apart.
     p, m = 8, nbytes // 8 // 4
-    srcs = (ctypes.c_void_p * p)(*[a.data_ptr() + r * m * 4 for r in range(p)])
+    skew = 68 << 10
+    del a
+    a = torch.empty(p * (m * 4 + skew), dtype=torch.uint8, device=dev)
     a.view(torch.float32).uniform_(-1, 1)
+    srcs = (ctypes.c_void_p * p)(*[a.data_ptr() + r * (m * 4 + skew) for r in range(p)])
+    srcs_pow2 = (ctypes.c_void_p * p)(*[a.data_ptr() + r * m * 4 for r in range(p)])
 
-    def time_tree():
+    def time_tree(srcs=srcs):
         ts = []
         for _ in range(3):
             L.msx_reduce_tree_dev(srcs, p, b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, sp)
@@ -353,6 +360,7 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
         return {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
     out["tree8/MPI_SUM/MPI_FLOAT"] = entry(time_tree())
+    out["tree8_pow2_stride/MPI_SUM/MPI_FLOAT"] = entry(time_tree(srcs_pow2))
     if tree_sweep:
         for mode, name in enumerate(("interleaved", "upfront", "upfront_nt", "interleaved_nt")):
             for cap in (1024, 2048, 4096, 8192, 65536):
@@ -437,6 +445,41 @@ def pack_roofline(L, C, torch, dev, stream):
     for t in (layouts[0][1], t3):
         L.MPI_Type_free(ctypes.byref(t))
     del typed
+    return out
+
+
+def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
+    """What this GPU's HBM delivers for other stream mixes under the combine's
+    own launch geometry (k_probe: 16 B per lane, 256-lane workgroups, one tile
+    each, XCD-contiguous, non-temporal loads), on the same 2 x 256 MiB
+    operands: 2 reads, 1 read, 1 write, 1 read + 1 write.  Median of 3 rounds
+    of 10 launches, HIP events on the launch stream.  Context for the
+    roofline's `frac` (which stays against the 8 TB/s spec peak)."""
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    with torch.cuda.stream(stream):
+        a.random_(0, 256)
+        b.random_(0, 256)
+    out = {}
+    for mode, name, streams in ((0, "read2", 2), (3, "read1", 1), (1, "write1", 1), (2, "copy_r1w1", 2)):
+        ts = []
+        for _ in range(3):
+            for _ in range(2):
+                L.msx_probe_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(10):
+                rc = L.msx_probe_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, sp)
+                if rc:
+                    raise RuntimeError(f"probe {name}: rc={rc}")
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 10)
+        ms = sorted(ts)[1]
+        gbs = streams * nbytes / ms / 1e6
+        out[name] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac_of_spec": round(gbs / HBM_PEAK_GBS, 4)}
+    del a, b
     return out
 
 
@@ -544,6 +587,30 @@ def main():
             sweep[key] = round(n * BYTES_PER_ELEM / ms / 1e6, 1)
             print(f"{key}: {ms * 1e3:.1f} us {sweep[key]:.0f} GB/s", file=sys.stderr)
         L.msx_tune_set(max(args.variant, 0), 0)
+        # operand placement: the default kernel with `in` and `inout` carved
+        # from one allocation at exactly 256 MiB apart vs skewed by a few KiB
+        # (HBM bank aliasing of two streams a power of two apart)
+        pool = torch.empty(2 * n * 4 + (2 << 20), dtype=torch.uint8, device=dev)
+        pool.view(torch.float32)[: (pool.numel() // 4)].uniform_(-1, 1)
+        atimes = {}
+        for _ in range(3):
+            for sk in (0, 4 << 10, 68 << 10, (1 << 20) + (68 << 10)):
+                pa, pb = pool.data_ptr(), pool.data_ptr() + n * 4 + sk
+                for _ in range(3):
+                    L.msx_reduce_local_dev(pa, pb, n, C.MPI_FLOAT, C.MPI_SUM, sp)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(10):
+                    L.msx_reduce_local_dev(pa, pb, n, C.MPI_FLOAT, C.MPI_SUM, sp)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                atimes.setdefault(sk, []).append(e0.elapsed_time(e1) / 10)
+        for sk, ts in atimes.items():
+            ms = sorted(ts)[1]
+            sweep[f"operand_gap_256MiB_plus_{sk}"] = round(n * BYTES_PER_ELEM / ms / 1e6, 1)
+            print(f"operands 256 MiB + {sk} B apart: {ms * 1e3:.1f} us {sweep[f'operand_gap_256MiB_plus_{sk}']:.0f} GB/s",
+                  file=sys.stderr)
+        del pool
 
     for _ in range(args.warmup):
         step()
@@ -596,8 +663,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_host_path:
         host = {}
         a_h = src.cpu()
-        for label, pin, mode in (("pageable", False, 0), ("pinned_zero_copy", True, 0),
-                                 ("pinned_staged", True, 1)):
+        for label, pin, mode in (("pageable", False, 0), ("pageable_staged", False, 2),
+                                 ("pinned_zero_copy", True, 0), ("pinned_staged", True, 1)):
             L.msx_set_host_mode(mode)
             ah = a_h.pin_memory() if pin else a_h.clone()
             bh = acc.cpu()
@@ -625,9 +692,10 @@ def main():
     pack = None
     if rank == 0 and world == 1 and not args.no_pack:
         pack = pack_roofline(L, C, torch, dev, stream)
-    rma = None
+    rma = probe = None
     if rank == 0 and world == 1 and not args.no_per_op:
         rma = rma_self_roofline(L, C, torch, dev, n)
+        probe = hbm_ceiling_probe(L, torch, dev, stream, n * 4)
 
     if rank == 0:
         total_bytes = world * args.steps * n * BYTES_PER_ELEM
@@ -675,6 +743,8 @@ def main():
             out["datatype_pack_roofline_hbm"] = pack
         if rma is not None:
             out["rma_self_accumulate_f32"] = rma
+        if probe is not None:
+            out["hbm_ceiling_probe"] = probe
         if sweep:
             out["variant_sweep_GB_s"] = sweep
         if world == 1:

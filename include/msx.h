@@ -93,12 +93,20 @@ int msx_tune_variant_count(void);
  * non-temporal; grid_cap 0 = default. */
 int msx_tune_tree(int mode, int grid_cap);
 const char* msx_tune_variant_name(int variant);
+/* HBM ceiling probe (measurement only): the default combine's launch geometry
+ * with another stream mix over `bytes` per stream (16-B aligned device
+ * pointers): mode 0 reads a and b, 1 writes b, 2 copies a -> b, 3 reads a.
+ * Stream-ordered; b's contents are unspecified afterwards. */
+int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream);
 
 /* host staging chunk size (bytes) for MPI_Reduce_local on host buffers */
 int msx_set_staging_chunk(int64_t bytes);
 /* host operands of MPI_Reduce_local: 0 (default) = pinned host memory is
- * combined in place by the kernel over PCIe (zero-copy), pageable memory is
- * staged through HBM; 1 = every host operand is staged */
+ * combined in place by the kernel over PCIe (zero-copy), pageable memory of
+ * at least MSX_HOST_PIN_MIN bytes (1 MiB) is pinned for the call and combined
+ * the same way (staged through HBM if the driver refuses to pin it);
+ * 1 = every host operand is staged through HBM; 2 = pinned memory in place,
+ * pageable memory staged */
 int msx_set_host_mode(int mode);
 
 /* schedule introspection for host-side tests of the collective engine

@@ -1535,6 +1535,15 @@ MSX_EXPORT int msx_tune_tree(int mode, int grid_cap)
     return tree_tune_set(mode, grid_cap) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
 }
 
+MSX_EXPORT int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream)
+{
+    if (mode < 0 || mode > 3 || bytes < 0 || !b || (mode != 1 && !a)) return MPI_ERR_ARG;
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    hipError_t e = launch_probe(mode, a, b, (size_t)bytes, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "probe launch");
+}
+
 MSX_EXPORT int msx_tune_variant_count(void) { return combine_variant_count(); }
 MSX_EXPORT const char* msx_tune_variant_name(int v) { return combine_variant_name(v); }
 
@@ -1547,7 +1556,7 @@ MSX_EXPORT int msx_set_staging_chunk(int64_t bytes)
 
 MSX_EXPORT int msx_set_host_mode(int mode)
 {
-    if (mode != 0 && mode != 1) { set_error("host mode must be 0 or 1"); return MPI_ERR_ARG; }
+    if (mode < 0 || mode > 2) { set_error("host mode must be 0, 1 or 2"); return MPI_ERR_ARG; }
     set_host_mode(mode);
     return MPI_SUCCESS;
 }

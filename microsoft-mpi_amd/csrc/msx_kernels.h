@@ -84,6 +84,10 @@ hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size
 struct TreeTune { int mode = 0; int grid_cap = 0; };
 int tree_tune_set(int mode, int grid_cap);
 
+// HBM ceiling probe (measurement only, see k_probe): mode 0 reads a and b,
+// 1 writes b, 2 copies a -> b, 3 reads a; `bytes` per stream, 16-B aligned.
+hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s);
+
 // Number of tuning variants compiled for the fp32 SUM hot path.
 int combine_variant_count();
 const char* combine_variant_name(int v);

@@ -118,6 +118,82 @@ __global__ __launch_bounds__(BLOCK) void k_combine_host(const T* __restrict__ in
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
 }
 
+// Tuning variant: KT consecutive tiles per workgroup (one contiguous run of
+// KT*BLOCK vectors per operand) instead of one tile per workgroup; UNR = the
+// KT tiles' loads may all be in flight together (else one tile at a time).
+template <int OP, class T, class VT, int BLOCK, int KT, bool UNR>
+__global__ __launch_bounds__(BLOCK) void k_combine_kt(const T* __restrict__ in, T* __restrict__ io, size_t head,
+                                                      size_t nvec, size_t tail)
+{
+    constexpr size_t EPV = 16 / sizeof(T);
+    const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in + head);
+    u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
+    const size_t t0 = (size_t)xcd_tile(blockIdx.x, gridDim.x) * KT * BLOCK + threadIdx.x;
+    if constexpr (UNR) {
+        u32x4 a[KT], b[KT];
+#pragma unroll
+        for (int j = 0; j < KT; ++j) {
+            const size_t i = t0 + (size_t)j * BLOCK;
+            if (i < nvec) { a[j] = ld<true>(vin + i); b[j] = ld<true>(vio + i); }
+        }
+#pragma unroll
+        for (int j = 0; j < KT; ++j) issued_together(a[j], b[j]);
+#pragma unroll
+        for (int j = 0; j < KT; ++j) {
+            const size_t i = t0 + (size_t)j * BLOCK;
+            if (i < nvec) vio[i] = apply_vec<OP, VT>(b[j], a[j]);
+        }
+    } else {
+#pragma unroll 1
+        for (int j = 0; j < KT; ++j) {
+            const size_t i = t0 + (size_t)j * BLOCK;
+            if (i < nvec) {
+                u32x4 x = ld<true>(vin + i), y = ld<true>(vio + i);
+                issued_together(x, y);
+                vio[i] = apply_vec<OP, VT>(y, x);
+            }
+        }
+    }
+    const size_t nscalar = head + tail;
+    if (nscalar) {
+        const size_t body_end = head + nvec * EPV;
+        for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nscalar; s += (size_t)gridDim.x * BLOCK) {
+            const size_t e = s < head ? s : body_end + (s - head);
+            io[e] = Fn<OP>::apply(io[e], in[e]);
+        }
+    }
+}
+
+// ---- HBM ceiling probe (measurement only) ----------------------------------------
+// The default combine's launch geometry (one 16-B vector per lane, 256-lane
+// workgroups, one tile each, XCD-contiguous tiles, non-temporal loads) with
+// other stream mixes, so the bench can say how close the 2-read + 1-write
+// combine gets to what this GPU's HBM actually delivers for each mix:
+//   MODE 0: read a and b (2R)   MODE 1: write b (1W)
+//   MODE 2: copy a -> b (1R1W)  MODE 3: read a (1R)
+// Reads feed a conditional store on a value random data essentially never
+// produces (`key`), so the compiler cannot drop them.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_probe(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t nvec,
+                                               unsigned key)
+{
+    const size_t i = (size_t)xcd_tile(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
+    if (i >= nvec) return;
+    if constexpr (MODE == 0) {
+        u32x4 x = ld<true>(a + i), y = ld<true>(b + i);
+        issued_together(x, y);
+        const u32x4 r = x ^ y;
+        if ((r.x ^ r.y ^ r.z ^ r.w) == key) b[i] = r;
+    } else if constexpr (MODE == 1) {
+        b[i] = u32x4{key, key ^ (unsigned)i, key, (unsigned)(i >> 32)};
+    } else if constexpr (MODE == 2) {
+        b[i] = ld<true>(a + i);
+    } else {
+        const u32x4 x = ld<true>(a + i);
+        if ((x.x ^ x.y ^ x.z ^ x.w) == key) b[i] = x;
+    }
+}
+
 // ---- LDS-staged variant (measurement only) ---------------------------------------
 // The north star's "LDS staging of the incoming chunk": the `in` tile goes
 // global -> LDS -> registers before the combine.  Each element is used once,
@@ -514,6 +590,22 @@ hipError_t run_combine_rr(const void* in, void* io, size_t count, hipStream_t s,
     return hipGetLastError();
 }
 
+template <int OP, class T, class VT, int BLOCK, int KT, bool UNR>
+hipError_t run_combine_kt(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg&)
+{
+    size_t head, nvec, tail;
+    split<T>(in, io, count, head, nvec, tail);
+    const size_t tile = (size_t)BLOCK * KT;
+    size_t grid = (nvec + tile - 1) / tile;
+    const size_t sc = (head + tail + BLOCK - 1) / BLOCK;
+    if (grid < sc) grid = sc;
+    if (grid == 0) return hipSuccess;
+    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_combine_kt<OP, T, VT, BLOCK, KT, UNR>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
+                       static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail);
+    return hipGetLastError();
+}
+
 template <int OP, class T, int BLOCK>
 hipError_t run_combine_lds(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
 {
@@ -567,6 +659,11 @@ const Variant kF32SumVariants[] = {
     {"u1_b256_lds", run_combine_lds<O_SUM, float, 256>},
     {"u1_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 256, true, false>},
     {"u2_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 2, 256, true, false>},
+    {"k2_b256_ntld_seq", run_combine_kt<O_SUM, float, float, 256, 2, false>},
+    {"k4_b256_ntld_seq", run_combine_kt<O_SUM, float, float, 256, 4, false>},
+    {"k2_b256_ntld_unr", run_combine_kt<O_SUM, float, float, 256, 2, true>},
+    {"k4_b256_ntld_unr", run_combine_kt<O_SUM, float, float, 256, 4, true>},
+    {"k2_b128_ntld_unr", run_combine_kt<O_SUM, float, float, 128, 2, true>},
 };
 constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
 
@@ -790,6 +887,25 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     case O_MINLOC: return tree_loc<O_MINLOC>(k, a, ns, out, n, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s)
+{
+    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 3) return hipErrorInvalidValue;
+    const size_t nvec = bytes / 16;
+    const size_t grid = (nvec + 255) / 256;
+    if (grid == 0) return hipSuccess;
+    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+    const u32x4* va = static_cast<const u32x4*>(a);
+    u32x4* vb = static_cast<u32x4*>(b);
+    const unsigned key = 0x9E3779B9u;
+    switch (mode) {
+    case 0: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
+    case 1: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
+    case 2: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
+    default: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_push_post(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,

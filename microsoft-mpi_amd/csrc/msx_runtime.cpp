@@ -4,11 +4,14 @@
 // the combine always runs on the GPU; host-resident MPI buffers are streamed
 // through HBM in chunks: H2D(in), H2D(inout) -> combine -> D2H(inout), with two
 // HIP streams so chunk i+1's copies overlap chunk i's combine and copy-back;
-// pinned host operands are read and written in place by the kernel (zero-copy)
-// unless msx_set_host_mode(1) asks for staging.
+// pinned host operands are read and written in place by the kernel (zero-copy),
+// and pageable ones are pinned for the duration of the call and treated the
+// same way (host mode 0, the default); msx_set_host_mode(2) stages pageable
+// operands, msx_set_host_mode(1) stages every host operand.
 // There is no CPU fallback: without a GPU the call fails with MPI_ERR_OTHER.
 #include "msx_runtime.h"
 
+#include <algorithm>
 #include <atomic>
 #include <dlfcn.h>
 #include <mutex>
@@ -17,6 +20,8 @@
 #include <stdlib.h>
 #include <time.h>
 #include <unistd.h>
+#include <utility>
+#include <vector>
 
 namespace msx {
 
@@ -129,9 +134,134 @@ void set_staging_chunk(size_t bytes)
     s.chunk = bytes & ~(size_t)255;
 }
 
+// ---- call-scoped pinning of pageable operands ---------------------------------
+// MPI_Reduce_local on pageable host buffers pins them for the duration of the
+// call (hipHostRegister, page-rounded) and lets the kernel read and write them
+// in place over PCIe, both directions at once.  Measured on MI355X
+// (scripts/host_path_probe.cpp, 2 x 256 MiB fp32): 10.5 ms per call with the
+// register/unregister included, vs 14.5 ms staging through HBM with the
+// runtime's synchronous pageable copies.  Ranges pinned this way are listed
+// here and classify() reports them as pageable, so no other thread of the
+// library ever launches a kernel on an address this call is about to unpin
+// (memory copies retain the runtime's pin object until they complete).
+namespace {
+struct TempPins {
+    std::mutex mu;
+    std::atomic<int> n{0};
+    std::vector<std::pair<uintptr_t, uintptr_t>> ranges;   // [lo, hi)
+    bool covers(uintptr_t p)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto& r : ranges)
+            if (p >= r.first && p < r.second) return true;
+        return false;
+    }
+};
+TempPins& temp_pins()
+{
+    static TempPins t;
+    return t;
+}
+
+uintptr_t page_down(uintptr_t a)
+{
+    static const uintptr_t ps = (uintptr_t)sysconf(_SC_PAGESIZE);
+    return a & ~(ps - 1);
+}
+uintptr_t page_up(uintptr_t a)
+{
+    static const uintptr_t ps = (uintptr_t)sysconf(_SC_PAGESIZE);
+    return (a + ps - 1) & ~(ps - 1);
+}
+
+// One call-scoped pin of the pages covering [a, b).  pin() returns false, with
+// nothing pinned, when another call holds an overlapping pin or the driver
+// refuses the range (a read-only mapping, pages the user registered already).
+class CallPin {
+public:
+    CallPin() = default;
+    CallPin(const CallPin&) = delete;
+    CallPin& operator=(const CallPin&) = delete;
+    ~CallPin() { release(); }
+
+    bool pin(uintptr_t a, uintptr_t b)
+    {
+        lo_ = page_down(a);
+        hi_ = page_up(b);
+        TempPins& t = temp_pins();
+        {
+            std::lock_guard<std::mutex> g(t.mu);
+            for (auto& r : t.ranges)
+                if (lo_ < r.second && r.first < hi_) {
+                    lo_ = hi_ = 0;
+                    return false;
+                }
+            t.ranges.push_back({lo_, hi_});
+            t.n.fetch_add(1, std::memory_order_release);
+        }
+        listed_ = true;
+        hipError_t e = hipHostRegister(reinterpret_cast<void*>(lo_), hi_ - lo_, hipHostRegisterMapped);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            trace("call pin of %zu bytes refused: %s", (size_t)(hi_ - lo_), hipGetErrorString(e));
+            unlist();
+            return false;
+        }
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(lo_), 0) != hipSuccess || !d) {
+            (void)hipGetLastError();
+            (void)hipHostUnregister(reinterpret_cast<void*>(lo_));
+            unlist();
+            return false;
+        }
+        dev_ = static_cast<char*>(d);
+        return true;
+    }
+    // device alias of host address p (inside the pinned range)
+    void* dev(const void* p) const { return dev_ + ((uintptr_t)p - lo_); }
+    void release()
+    {
+        if (dev_) (void)hipHostUnregister(reinterpret_cast<void*>(lo_));
+        dev_ = nullptr;
+        unlist();
+    }
+
+private:
+    void unlist()
+    {
+        if (!listed_) return;
+        TempPins& t = temp_pins();
+        std::lock_guard<std::mutex> g(t.mu);
+        for (size_t i = 0; i < t.ranges.size(); ++i)
+            if (t.ranges[i].first == lo_ && t.ranges[i].second == hi_) {
+                t.ranges.erase(t.ranges.begin() + (long)i);
+                break;
+            }
+        t.n.fetch_sub(1, std::memory_order_release);
+        listed_ = false;
+    }
+    uintptr_t lo_ = 0, hi_ = 0;
+    char* dev_ = nullptr;
+    bool listed_ = false;
+};
+
+// Smallest call (bytes per operand) worth pinning; below it the staged copies
+// are cheaper than two register/unregister round trips.  MSX_HOST_PIN_MIN.
+size_t pin_min_bytes()
+{
+    static const size_t v = [] {
+        size_t m = (size_t)1 << 20;
+        if (const char* e = getenv("MSX_HOST_PIN_MIN")) m = (size_t)atoll(e);
+        return m;
+    }();
+    return v;
+}
+}  // namespace
+
 BufInfo classify(const void* p)
 {
     BufInfo b;
+    if (temp_pins().n.load(std::memory_order_acquire) > 0 && temp_pins().covers((uintptr_t)p)) return b;
     hipPointerAttribute_t a;
     hipError_t e = hipPointerGetAttributes(&a, p);
     if (e != hipSuccess) {
@@ -208,18 +338,41 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
     const BufInfo bi = classify(in), bo = classify(inout);
     DevState& s = ds();
 
-    // Device memory, or (host mode 0) pinned host memory the kernel reads and
-    // writes in place over PCIe: reads and the write-back then use both PCIe
-    // directions at once, with no staging copies.
+    // Device memory, or (host modes 0 and 2) pinned host memory the kernel
+    // reads and writes in place over PCIe: reads and the write-back then use
+    // both PCIe directions at once, with no staging copies.
+    const int mode = g_host_mode.load();
     const bool direct = (bi.place == Place::Device && bo.place == Place::Device) ||
-                        (g_host_mode.load() == 0 && bi.dev && bo.dev);
-    if (direct) {
+                        (mode != 1 && bi.dev && bo.dev);
+    auto run_direct = [&](const void* din, void* dio) {
         LaunchCfg cfg = g_cfg;
         cfg.host = bi.place != Place::Device || bo.place != Place::Device;
-        hipError_t le = launch_combine(opidx, k, bi.dev, bo.dev, count, s.stream, cfg);   // device aliases
+        hipError_t le = launch_combine(opidx, k, din, dio, count, s.stream, cfg);   // device aliases
         if (le != hipSuccess) return hip_fail(le, "combine kernel launch");
         hipError_t e = hipStreamSynchronize(s.stream);
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "combine kernel");
+    };
+    if (direct) return run_direct(bi.dev, bo.dev);
+
+    // Host mode 0: pageable operands are pinned for this call and combined in
+    // place like pinned ones (see CallPin); if the driver refuses, staged.
+    const size_t bytes_all = count * (size_t)kind_size(k);
+    if (mode == 0 && bytes_all >= pin_min_bytes()) {
+        const bool pin_in = !bi.dev, pin_io = !bo.dev;
+        const uintptr_t ia = (uintptr_t)in, ib = ia + bytes_all, oa = (uintptr_t)inout, ob = oa + bytes_all;
+        CallPin p1, p2;
+        const void* din = bi.dev;
+        void* dio = bo.dev;
+        bool ok = true;
+        if (pin_in && pin_io && page_down(ia) < page_up(ob) && page_down(oa) < page_up(ib)) {
+            ok = p1.pin(std::min(ia, oa), std::max(ib, ob));          // operands share pages: one pin
+            if (ok) { din = p1.dev(in); dio = p1.dev(inout); }
+        } else {
+            if (pin_in) { ok = p1.pin(ia, ib); if (ok) din = p1.dev(in); }
+            if (ok && pin_io) { ok = p2.pin(oa, ob); if (ok) dio = p2.dev(inout); }
+        }
+        if (ok) return run_direct(din, dio);                          // pins released on return
+        trace("reduce_local: call pin refused, staging %zu bytes", bytes_all);
     }
 
     // At least one operand in host memory: chunked, double-buffered staging.

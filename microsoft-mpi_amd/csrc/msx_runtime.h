@@ -38,7 +38,8 @@ BufInfo classify(const void* p);
 LaunchCfg& launch_cfg();
 void set_staging_chunk(size_t bytes);
 // host operands: 0 = pinned memory combined in place by the kernel (zero-copy),
-// pageable staged; 1 = every host operand staged through HBM
+// pageable memory pinned for the call and combined the same way; 1 = every
+// host operand staged through HBM; 2 = pinned in place, pageable staged
 void set_host_mode(int mode);
 int host_mode();
 

@@ -1072,11 +1072,29 @@ constexpr size_t kFlagBytes = 64 << 10;
 // origin) then p fetch slots (written by each target), kRmaBytes / (2p) each.
 constexpr size_t kRmaBytes = (size_t)64 << 20;
 
+// Sub-slots are Q bytes long but S = Q + skew apart: the p-source tree reads
+// every sub-slot at the same offset, and sources a power of two apart lose
+// HBM bandwidth to channel aliasing (scripts/tree_skew_probe.py on MI355X,
+// profiles/r01/tree_skew_probe.log: 8 x 32 MiB, 6.27 TB/s at a 32 MiB stride,
+// 6.51-6.56 TB/s with 4-68 KiB added).
+size_t sub_skew(size_t per_rank)
+{
+    if (per_rank >= ((size_t)16 << 20)) return (size_t)68 << 10;
+    return (per_rank / 16) & ~(size_t)255;
+}
+
+// usable bytes of one sub-slot of a window with chunk C over p ranks
+size_t sub_len(size_t C, int p)
+{
+    const size_t per = C / (size_t)p;
+    return (per - sub_skew(per)) & ~(size_t)255;
+}
+
 struct Windows {
     std::vector<char*> base;
-    size_t C = 0, Q = 0;
+    size_t C = 0, Q = 0, S = 0;
     char* in(int r) const { return base[(size_t)r]; }
-    char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * Q; }
+    char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * S; }
     char* out(int r) const { return base[(size_t)r] + C; }
     unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + 2 * C); }
     size_t rma_slot() const { return (kRmaBytes / (2 * base.size())) & ~(size_t)255; }
@@ -1120,7 +1138,8 @@ int* wait_err_word(int** host)
 int get_windows(Transport* tp, Windows* w, bool rd_single = false)
 {
     w->C = chunk_bytes();
-    w->Q = (w->C / (size_t)tp->size) & ~(size_t)255;
+    w->Q = sub_len(w->C, tp->size);
+    w->S = w->Q + sub_skew(w->C / (size_t)tp->size);
     int rc = tp->window(2 * w->C + kFlagBytes + kRmaBytes, w->base);
     if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
         // the last recursive-doubling call left without its closing barrier:
@@ -1328,13 +1347,14 @@ int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf,
     const BufInfo bs = classify(src), bd = classify(dst);
     size_t qmax = (chunk_bytes() / (size_t)p) / esz;
     qmax -= qmax % 16;
-    // scratch: [IN: p sub-slots of qmax][OUT: p*qmax][stage: p*qmax]
+    // scratch: [IN: p sub-slots of qmax, skewed apart (sub_skew)][OUT: p*qmax][stage: p*qmax]
     const size_t sub_b = qmax * esz, area = (size_t)p * sub_b;
-    char* scratch = dev_scratch(3 * area);
+    const size_t sub_s = sub_b + sub_skew(chunk_bytes() / (size_t)p);
+    char* scratch = dev_scratch((size_t)p * sub_s + 2 * area);
     if (!scratch) { set_error("allreduce: scratch allocation failed"); return MPI_ERR_NO_MEM; }
     char* inb = scratch;
-    char* outb = scratch + area;
-    char* stage = scratch + 2 * area;
+    char* outb = scratch + (size_t)p * sub_s;
+    char* stage = outb + area;
     std::vector<char*> srcs((size_t)p);
     const int pof2 = pof2_floor(p);
     const int n = newrank_of(me, p);
@@ -1351,11 +1371,11 @@ int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf,
             for (int r = 0; r < p; ++r) {
                 if (r == me) continue;
                 if (root < 0 || r == root) x.send(mine, len * esz, r);
-                if (want) x.recv(inb + (size_t)r * sub_b, len * esz, r);
+                if (want) x.recv(inb + (size_t)r * sub_s, len * esz, r);
             }
             if (rc == MPI_SUCCESS) rc = x.run(comm, s, "allreduce exchange");
             if (rc == MPI_SUCCESS && want) {
-                for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(mine) : inb + (size_t)r * sub_b;
+                for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(mine) : inb + (size_t)r * sub_s;
                 char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz : outb;
                 rc = run_rank_tree(op.opidx, k, t, srcs, esz, 0, len, out, s);
                 if (rc == MPI_SUCCESS && out == outb) rc = copy_async(dst + o * esz, out, len * esz, s);
@@ -1377,10 +1397,10 @@ int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf,
         for (int r = 0; r < p; ++r) {
             if (r == me) continue;
             x.send(mine + lo_of(r) * esz, (hi_of(r) - lo_of(r)) * esz, r);
-            x.recv(inb + (size_t)r * sub_b, (phi - plo) * esz, r);
+            x.recv(inb + (size_t)r * sub_s, (phi - plo) * esz, r);
         }
         if (rc == MPI_SUCCESS) rc = x.run(comm, s, "allreduce scatter");
-        for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(mine) + plo * esz : inb + (size_t)r * sub_b;
+        for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(mine) + plo * esz : inb + (size_t)r * sub_s;
         char* outp = (want && bd.place == Place::Device) ? static_cast<char*>(bd.dev) + o * esz : outb;
         for (size_t e0 = plo; e0 < phi && rc == MPI_SUCCESS;) {
             const size_t ge = o + e0;
@@ -1432,13 +1452,14 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
     const size_t mycnt = (size_t)recvcounts[me];
     const BufInfo bs = classify(src), bd = classify(recvbuf);
     char* dst = static_cast<char*>(recvbuf);
-    // scratch: [IN: p*qe][OUT: qe][stage: p*qe][hold: mycnt if in place]
+    // scratch: [IN: p sub-slots of qe, skewed apart][OUT: qe][stage: p*qe][hold: mycnt if in place]
     const size_t sub_b = qe * esz, area = (size_t)p * sub_b;
+    const size_t sub_s = sub_b + sub_skew(chunk_bytes() / (size_t)p);
     const size_t hold_b = in_place ? mycnt * esz : 0;
-    char* scratch = dev_scratch(2 * area + sub_b + hold_b);
+    char* scratch = dev_scratch((size_t)p * sub_s + area + sub_b + hold_b);
     if (!scratch) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
     char* inb = scratch;
-    char* outb = scratch + area;
+    char* outb = scratch + (size_t)p * sub_s;
     char* stage = outb + sub_b;
     char* hold = stage + area;
     std::vector<char*> srcs((size_t)p);
@@ -1458,10 +1479,10 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
         }
         const size_t len = o < mycnt ? std::min(qe, mycnt - o) : 0;
         for (int r = 0; r < p; ++r)
-            if (r != me) x.recv(inb + (size_t)r * sub_b, len * esz, r);
+            if (r != me) x.recv(inb + (size_t)r * sub_s, len * esz, r);
         if (rc == MPI_SUCCESS) rc = x.run(comm, s, "reduce_scatter exchange");
         if (rc == MPI_SUCCESS && len) {
-            for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(myseg) : inb + (size_t)r * sub_b;
+            for (int r = 0; r < p; ++r) srcs[r] = (r == me) ? const_cast<char*>(myseg) : inb + (size_t)r * sub_s;
             char* out = in_place ? hold + o * esz
                                  : (bd.place == Place::Device ? static_cast<char*>(bd.dev) + o * esz : outb);
             rc = run_rank_tree(op.opidx, k, t, srcs, esz, 0, len, out, s);
@@ -1500,7 +1521,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     // call.  Pushing into a peer's half P again (two calls later) happens only
     // after this rank passed the previous call's barrier A, which that peer
     // reached only after finishing its tree on half P.
-    const size_t Qh = ((chunk_bytes() / (size_t)p) & ~(size_t)255) / 2;
+    const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
     const bool rd_single = (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) &&
                            count * esz <= (Qh & ~(size_t)(16 * esz - 1));
     Windows w;

@@ -173,6 +173,7 @@ def lib():
         "msx_tune_tree": (i, [i, i]),
         "msx_tune_variant_count": (i, []),
         "msx_tune_variant_name": (ctypes.c_char_p, [i]),
+        "msx_probe_hbm": (i, [i, p, p, i64, p]),
         "msx_set_staging_chunk": (i, [i64]),
         "msx_set_host_mode": (i, [i]),
     }

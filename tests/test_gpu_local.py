@@ -158,10 +158,12 @@ def test_known_answer_vectors_on_gpu(L):
     assert np.array_equal(_host(tb, 0, b).view(np.uint32), to_f(case["expect_f32_hex"]).view(np.uint32))
 
 
-@pytest.mark.parametrize("pinned,mode", [(False, 0), (True, 0), (True, 1)])
+@pytest.mark.parametrize("pinned,mode", [(False, 0), (True, 0), (True, 1), (False, 1), (False, 2), (True, 2)])
 def test_mpi_reduce_local_host_buffers_staged(L, pinned, mode):
     # the MPI path starts and ends in host memory: staged through HBM in chunks
-    # (mode 1, and pageable memory), or pinned memory combined in place (mode 0)
+    # (mode 1; pageable memory in mode 2), or combined in place over PCIe
+    # (pinned memory in modes 0 and 2; pageable memory pinned for the call in
+    # mode 0)
     assert L.msx_set_staging_chunk(1 << 20) == 0      # force many chunks
     assert L.msx_set_host_mode(mode) == 0
     rng = np.random.default_rng(11)
@@ -184,6 +186,57 @@ def test_mpi_reduce_local_host_buffers_staged(L, pinned, mode):
         assert got.tobytes() == exp.tobytes()
     assert L.msx_set_staging_chunk(64 << 20) == 0
     assert L.msx_set_host_mode(0) == 0
+
+
+def test_mpi_reduce_local_call_pin_edges(L):
+    # host mode 0 pins pageable operands for the call: operands that share
+    # pages (one pin of the union), unaligned starts and ragged ends, one
+    # operand on the device, sizes either side of MSX_HOST_PIN_MIN, repeated
+    # calls on the same buffers (the pin is released every time), and a
+    # read-only `in` mapping the driver refuses to pin (staged instead)
+    import mmap
+    assert L.msx_set_host_mode(0) == 0
+    rng = np.random.default_rng(21)
+    big = rng.uniform(-1, 1, (5 << 20) // 4 + 77).astype(np.float32)
+    for k in range(3):                                   # shared pages, odd offsets
+        lo, n = 3 + k, (2 << 20) // 4 + 1001 * k + 5
+        a = big[lo:lo + n]
+        b = big[lo + n:lo + 2 * n].copy() if k == 2 else big[lo + n:lo + 2 * n]
+        exp = b.copy()
+        oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a.copy(), exp)
+        assert L.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, n, C.MPI_FLOAT, C.MPI_SUM) == 0, msx.last_error()
+        assert b.tobytes() == exp.tobytes()
+    for n in (1000, (1 << 20) // 8 - 1, (1 << 20) // 8, (3 << 20) // 8 + 3):   # around the 1 MiB threshold
+        a = rng.integers(0, 2**63, n, dtype=np.uint64)
+        b = rng.integers(0, 2**63, n, dtype=np.uint64)
+        exp = b.copy()
+        oracle.reduce_local(C.MPI_BXOR, C.MPI_UINT64_T, a, exp)
+        for rep in range(2):                             # twice: pins released in between
+            if rep:
+                oracle.reduce_local(C.MPI_BXOR, C.MPI_UINT64_T, a, exp)
+            assert L.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, n, C.MPI_UINT64_T, C.MPI_BXOR) == 0
+            assert np.array_equal(b, exp)
+    n = (4 << 20) // 4                                   # device `in`, pageable `inout`
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = rng.uniform(-1, 1, n).astype(np.float32)
+    exp = b.copy()
+    oracle.reduce_local(C.MPI_MAX, C.MPI_FLOAT, a, exp)
+    ta, pa = _dev(a)
+    assert L.MPI_Reduce_local(pa, b.ctypes.data, n, C.MPI_FLOAT, C.MPI_MAX) == 0
+    assert b.tobytes() == exp.tobytes()
+    src = rng.integers(-2**31, 2**31, (8 << 20) // 4, dtype=np.int64).astype(np.int32)
+    ro = mmap.mmap(-1, 8 << 20)                          # read-only `in`
+    ro.write(src.tobytes())
+    import ctypes as ct
+    libc = ct.CDLL(None)
+    addr = ct.addressof(ct.c_char.from_buffer(ro))
+    assert libc.mprotect(ct.c_void_p(addr), ct.c_size_t(8 << 20), 1) == 0   # PROT_READ
+    b = rng.integers(-2**31, 2**31, src.size, dtype=np.int64).astype(np.int32)
+    exp = b.copy()
+    oracle.reduce_local(C.MPI_SUM, C.MPI_INT, src, exp)
+    assert L.MPI_Reduce_local(addr, b.ctypes.data, src.size, C.MPI_INT, C.MPI_SUM) == 0, msx.last_error()
+    assert np.array_equal(b, exp)
+    assert libc.mprotect(ct.c_void_p(addr), ct.c_size_t(8 << 20), 3) == 0
 
 
 def test_mpi_reduce_local_device_and_mixed(L):
