@@ -151,6 +151,36 @@ def main(out_path, scale):
     del send, recv, exp
     torch.cuda.empty_cache()
 
+    # ---- c3 on host memory: the MPI path starts and ends in (pageable) host
+    # buffers; 256 MiB per rank, PCIe-inclusive (pinned for the call and read /
+    # written in place by the kernels)
+    import numpy as np
+    nh = int((64 << 20) * scale)
+    ih = np.arange(nh, dtype=np.int64)
+    hsend = (((ih * 7 + rank * 13) % 17) - 8).astype(np.float32)
+    hexp = np.zeros(nh, np.float32)
+    for r in range(p):
+        hexp += (((ih * 7 + r * 13) % 17) - 8).astype(np.float32)
+    del ih
+    hrecv = np.empty_like(hsend)
+    ts = []
+    for it in range(4):
+        barrier()
+        t0 = time.perf_counter()
+        rc = L.MPI_Allreduce(hsend.ctypes.data, hrecv.ctypes.data, nh, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+        ts.append(time.perf_counter() - t0)
+        if rc:
+            res["c3_host_error"] = f"rc={rc} {msx.last_error()}"
+            break
+    if "c3_host_error" not in res:
+        t = sorted(ts[1:])[len(ts[1:]) // 2]
+        res["c3_host_pageable_allreduce_sum_f32"] = {
+            "bytes_per_rank": nh * 4, "seconds": round(t, 5), "algbw_GB_s": round(nh * 4 / t / 1e9, 2),
+            "busbw_GB_s": round(nh * 4 / t / 1e9 * 2 * (p - 1) / p, 2),
+            "correct": bool(np.array_equal(hrecv, hexp))}
+    log(f"c3 host done {res.get('c3_host_pageable_allreduce_sum_f32', res.get('c3_host_error'))}")
+    del hsend, hrecv, hexp
+
     # ---- c4: reduce_scatter MAX fp64, 4 GiB per rank sendbuf ----------------
     per = int((512 << 20) * scale) // p                  # recvcount per rank (c4: 2^29 / p)
     tot = per * p

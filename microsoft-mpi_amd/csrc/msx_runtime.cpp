@@ -219,6 +219,7 @@ public:
     }
     // device alias of host address p (inside the pinned range)
     void* dev(const void* p) const { return dev_ + ((uintptr_t)p - lo_); }
+    bool active() const { return dev_ != nullptr; }
     void release()
     {
         if (dev_) (void)hipHostUnregister(reinterpret_cast<void*>(lo_));
@@ -257,6 +258,56 @@ size_t pin_min_bytes()
     return v;
 }
 }  // namespace
+
+struct PinHold::Impl {
+    CallPin pins[2];
+    std::vector<hipStream_t> streams;
+};
+
+PinHold::PinHold() : impl_(new Impl) {}
+
+PinHold::~PinHold()
+{
+    // work still queued on these streams may read or write the pinned pages
+    if (impl_->pins[0].active() || impl_->pins[1].active())
+        for (hipStream_t st : impl_->streams) (void)hipStreamSynchronize(st);
+}
+
+void PinHold::sync_before_release(hipStream_t s) { impl_->streams.push_back(s); }
+
+bool alias_host_operands(PinHold& hold, bool pin_pageable, const void* a, size_t na, BufInfo* ia, const void* b,
+                         size_t nb, BufInfo* ib)
+{
+    auto promote = [](BufInfo* x) {
+        if (x && x->place == Place::Host && x->dev) {
+            x->place = Place::Device;
+            x->pinned_host = true;
+        }
+    };
+    promote(ia);
+    promote(ib);
+    auto wants = [&](const void* p, size_t n, BufInfo* x) {
+        return pin_pageable && p && x && n && n >= pin_min_bytes() && x->place == Place::Host && !x->dev;
+    };
+    const bool wa = wants(a, na, ia), wb = wants(b, nb, ib);
+    CallPin* pins = hold.impl_->pins;
+    auto set = [](BufInfo* x, void* d) {
+        x->place = Place::Device;
+        x->dev = d;
+        x->pinned_host = true;
+    };
+    const uintptr_t a0 = (uintptr_t)a, a1 = a0 + na, b0 = (uintptr_t)b, b1 = b0 + nb;
+    if (wa && wb && page_down(a0) < page_up(b1) && page_down(b0) < page_up(a1)) {
+        if (pins[0].pin(std::min(a0, b0), std::max(a1, b1))) {   // operands share pages: one pin
+            set(ia, pins[0].dev(a));
+            set(ib, pins[0].dev(b));
+        }
+    } else {
+        if (wa && pins[0].pin(a0, a1)) set(ia, pins[0].dev(a));
+        if (wb && pins[1].pin(b0, b1)) set(ib, pins[1].dev(b));
+    }
+    return (!ia || ia->place == Place::Device) && (!ib || ib->place == Place::Device);
+}
 
 BufInfo classify(const void* p)
 {
@@ -335,45 +386,28 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
 {
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
-    const BufInfo bi = classify(in), bo = classify(inout);
+    BufInfo bi = classify(in), bo = classify(inout);
     DevState& s = ds();
 
     // Device memory, or (host modes 0 and 2) pinned host memory the kernel
     // reads and writes in place over PCIe: reads and the write-back then use
-    // both PCIe directions at once, with no staging copies.
+    // both PCIe directions at once, with no staging copies.  Host mode 0 also
+    // pins pageable operands for the call (PinHold); if the driver refuses,
+    // they are staged.
     const int mode = g_host_mode.load();
-    const bool direct = (bi.place == Place::Device && bo.place == Place::Device) ||
-                        (mode != 1 && bi.dev && bo.dev);
-    auto run_direct = [&](const void* din, void* dio) {
+    const size_t bytes_all = count * (size_t)kind_size(k);
+    PinHold hold;
+    hold.sync_before_release(s.stream);
+    if (mode != 1) alias_host_operands(hold, mode == 0, in, bytes_all, &bi, inout, bytes_all, &bo);
+    if (bi.place == Place::Device && bo.place == Place::Device) {
         LaunchCfg cfg = g_cfg;
-        cfg.host = bi.place != Place::Device || bo.place != Place::Device;
-        hipError_t le = launch_combine(opidx, k, din, dio, count, s.stream, cfg);   // device aliases
+        cfg.host = bi.pinned_host || bo.pinned_host;
+        hipError_t le = launch_combine(opidx, k, bi.dev, bo.dev, count, s.stream, cfg);   // device aliases
         if (le != hipSuccess) return hip_fail(le, "combine kernel launch");
         hipError_t e = hipStreamSynchronize(s.stream);
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "combine kernel");
-    };
-    if (direct) return run_direct(bi.dev, bo.dev);
-
-    // Host mode 0: pageable operands are pinned for this call and combined in
-    // place like pinned ones (see CallPin); if the driver refuses, staged.
-    const size_t bytes_all = count * (size_t)kind_size(k);
-    if (mode == 0 && bytes_all >= pin_min_bytes()) {
-        const bool pin_in = !bi.dev, pin_io = !bo.dev;
-        const uintptr_t ia = (uintptr_t)in, ib = ia + bytes_all, oa = (uintptr_t)inout, ob = oa + bytes_all;
-        CallPin p1, p2;
-        const void* din = bi.dev;
-        void* dio = bo.dev;
-        bool ok = true;
-        if (pin_in && pin_io && page_down(ia) < page_up(ob) && page_down(oa) < page_up(ib)) {
-            ok = p1.pin(std::min(ia, oa), std::max(ib, ob));          // operands share pages: one pin
-            if (ok) { din = p1.dev(in); dio = p1.dev(inout); }
-        } else {
-            if (pin_in) { ok = p1.pin(ia, ib); if (ok) din = p1.dev(in); }
-            if (ok && pin_io) { ok = p2.pin(oa, ob); if (ok) dio = p2.dev(inout); }
-        }
-        if (ok) return run_direct(din, dio);                          // pins released on return
-        trace("reduce_local: call pin refused, staging %zu bytes", bytes_all);
     }
+    if (mode == 0 && bytes_all >= pin_min_bytes()) trace("reduce_local: call pin refused, staging %zu bytes", bytes_all);
 
     // At least one operand in host memory: chunked, double-buffered staging.
     std::lock_guard<std::mutex> g(s.stage_mu);

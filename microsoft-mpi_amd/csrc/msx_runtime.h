@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <memory>
 #include <string>
 
 #include "msx_kernels.h"
@@ -18,6 +19,7 @@ struct BufInfo {
     Place place = Place::Host;
     void* dev = nullptr;     // device-accessible alias (device/managed/pinned), or nullptr
     int device = -1;
+    bool pinned_host = false;   // Device designation of a host buffer's mapped alias
 };
 
 // MSX_TRACE=1: timestamped engine trace on stderr
@@ -34,6 +36,34 @@ hipStream_t internal_stream();
 int device_count_noinit();
 
 BufInfo classify(const void* p);
+
+// Call-scoped device aliases of host operands.  Pageable ranges are pinned
+// (hipHostRegister, page-rounded) for the lifetime of the hold and listed so
+// that classify() on any thread keeps reporting them as pageable: no other
+// path of the library launches a kernel on pages this call will unpin.  The
+// destructor synchronises the streams registered with sync_before_release()
+// before it unpins, so error paths cannot leave work running on them.
+class PinHold {
+public:
+    PinHold();
+    ~PinHold();
+    PinHold(const PinHold&) = delete;
+    PinHold& operator=(const PinHold&) = delete;
+    void sync_before_release(hipStream_t s);
+    struct Impl;
+private:
+    std::unique_ptr<Impl> impl_;
+    friend bool alias_host_operands(PinHold&, bool, const void*, size_t, BufInfo*, const void*, size_t, BufInfo*);
+};
+
+// Operands a (na bytes) and b (nb bytes; b may be a, or null): pinned host
+// memory is used through its mapped alias; with pin_pageable, pageable memory
+// of at least MSX_HOST_PIN_MIN bytes (default 1 MiB) is pinned for the hold's
+// lifetime (one pin when the operands share pages).  Each operand aliased this
+// way becomes {Place::Device, alias, pinned_host}.  Returns true when no
+// operand is left in host memory.
+bool alias_host_operands(PinHold& hold, bool pin_pageable, const void* a, size_t na, BufInfo* ia, const void* b,
+                         size_t nb, BufInfo* ib);
 
 LaunchCfg& launch_cfg();
 void set_staging_chunk(size_t bytes);

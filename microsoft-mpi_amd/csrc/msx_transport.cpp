@@ -1526,7 +1526,12 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                            count * esz <= (Qh & ~(size_t)(16 * esz - 1));
     Windows w;
     if ((rc = get_windows(tp, &w, rd_single)) != MPI_SUCCESS) return rc;
-    const BufInfo bs = classify(src), bd = classify(dst);
+    // host buffers: device aliases for the call (pinned in place of staging)
+    BufInfo bs = classify(src), bd = classify(dst);
+    PinHold pins;
+    pins.sync_before_release(s);
+    pins.sync_before_release(aux_stream());
+    alias_host_operands(pins, true, src, count * esz, &bs, want ? dst : nullptr, want ? count * esz : 0, &bd);
     // elements per sub-slot, whole 16-element granules
     size_t qmax = w.Q / esz;
     qmax -= qmax % 16;
@@ -1796,7 +1801,11 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
                                                : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
     trace("reduce_scatter: total=%zu esz=%zu algo=%d round=%zu", total, esz, algo, qe);
     const size_t mycnt = (size_t)recvcounts[me];
-    const BufInfo bs = classify(src), bd = classify(recvbuf);
+    BufInfo bs = classify(src), bd = classify(recvbuf);
+    PinHold pins;                        // host buffers: device aliases for the call
+    pins.sync_before_release(s);
+    alias_host_operands(pins, true, src, total * esz, &bs, in_place ? nullptr : recvbuf, in_place ? 0 : mycnt * esz,
+                        &bd);
     char* dst = static_cast<char*>(recvbuf);
     // scratch: [hold: in-place results][stage: host-resident input pieces]
     const size_t hold_b = in_place ? ((mycnt * esz + 255) & ~(size_t)255) : 0;
@@ -1998,8 +2007,14 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     char* partial = dev_scratch(2 * bytes + 256);
     if (!partial) { set_error("scan: scratch allocation failed"); return MPI_ERR_NO_MEM; }
     char* res = partial + ((bytes + 255) & ~(size_t)255);
-    rc = copy_async(partial, src, bytes, s);
-    if (rc == MPI_SUCCESS && !exclusive) rc = copy_async(res, src, bytes, s);
+    BufInfo bs = classify(src), bd = classify(recvbuf);
+    PinHold pins;                        // host buffers: device aliases for the call
+    pins.sync_before_release(s);
+    alias_host_operands(pins, true, src, bytes, &bs, recvbuf, bytes, &bd);
+    const char* srcv = bs.place == Place::Device ? static_cast<const char*>(bs.dev) : src;
+    void* dstv = bd.place == Place::Device ? bd.dev : recvbuf;
+    rc = copy_async(partial, srcv, bytes, s);
+    if (rc == MPI_SUCCESS && !exclusive) rc = copy_async(res, srcv, bytes, s);
     if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan init");
     bool have = !exclusive;
     int slot = 0;
@@ -2033,7 +2048,7 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     }
     if (rc == MPI_SUCCESS) rc = tp->barrier();
     if (rc == MPI_SUCCESS && have) {
-        rc = copy_async(recvbuf, res, bytes, s);
+        rc = copy_async(dstv, res, bytes, s);
         if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan result");
     }
     return rc;

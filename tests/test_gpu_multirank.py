@@ -159,6 +159,50 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
         elif not (excl and rank == 0):
             check(f"iscan {opn} {dtn} excl={excl}", fromdev(rb2, xs[rank]), exp[rank])
 
+# Host (pageable) buffers above MSX_HOST_PIN_MIN: pinned for the call and used
+# in place by the kernels (allreduce send/recv and in place, reduce_scatter,
+# reduce at the last rank, scan), checked against the reference schedules
+cnt = (3 << 20) // 4 + 5
+xs = inputs("MPI_SUM", "MPI_FLOAT", cnt, 7000)
+exp = [raw(x.copy()) for x in xs]
+assert oracle.allreduce(C.MPI_SUM, C.MPI_FLOAT, xs, exp) == 0
+hb = raw(np.zeros_like(xs[rank]))
+rc = L.MPI_Allreduce(xs[rank].ctypes.data, hb.ctypes.data, cnt, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+if rc: fails.append(f"host allreduce rc={rc} {msx.last_error()}")
+else: check("host allreduce pinned", hb, exp[rank])
+hi = raw(xs[rank].copy())
+rc = L.MPI_Allreduce(ctypes.c_void_p(-1 & 0xffffffffffffffff), hi.ctypes.data, cnt, C.MPI_FLOAT, C.MPI_SUM,
+                     C.MPI_COMM_WORLD)
+if rc: fails.append(f"host allreduce in place rc={rc} {msx.last_error()}")
+else: check("host allreduce in place pinned", hi, exp[rank])
+er = raw(np.zeros_like(xs[0]))
+assert oracle.reduce(C.MPI_SUM, C.MPI_FLOAT, p - 1, xs, er) == 0
+hr = raw(np.zeros_like(xs[rank]))
+rc = L.MPI_Reduce(xs[rank].ctypes.data, hr.ctypes.data, cnt, C.MPI_FLOAT, C.MPI_SUM, p - 1, C.MPI_COMM_WORLD)
+if rc: fails.append(f"host reduce rc={rc} {msx.last_error()}")
+elif rank == p - 1: check("host reduce pinned", hr, er)
+counts_h = [(1 << 20) // 8 + 3 * k for k in range(p)]
+xh = inputs("MPI_MAX", "MPI_DOUBLE", sum(counts_h), 7001)
+eh = [raw(np.zeros(c, xh[0].dtype)) for c in counts_h]
+assert oracle.reduce_scatter(C.MPI_MAX, C.MPI_DOUBLE, counts_h, xh, eh) == 0
+ch = (ctypes.c_int * p)(*counts_h)
+rh = raw(np.zeros(counts_h[rank], xh[0].dtype))
+rc = L.MPI_Reduce_scatter(xh[rank].ctypes.data, rh.ctypes.data, ch, C.MPI_DOUBLE, C.MPI_MAX, C.MPI_COMM_WORLD)
+if rc: fails.append(f"host reduce_scatter rc={rc} {msx.last_error()}")
+else: check("host reduce_scatter pinned", rh, eh[rank])
+ih = raw(xh[rank].copy())
+rc = L.MPI_Reduce_scatter(ctypes.c_void_p(-1 & 0xffffffffffffffff), ih.ctypes.data, ch, C.MPI_DOUBLE, C.MPI_MAX,
+                          C.MPI_COMM_WORLD)
+if rc: fails.append(f"host reduce_scatter in place rc={rc} {msx.last_error()}")
+else: check("host reduce_scatter in place pinned", ih[:counts_h[rank]], eh[rank])
+es = [raw(np.zeros_like(xs[0])) for _ in range(p)]
+assert oracle.scan(C.MPI_SUM, C.MPI_FLOAT, xs, es, exclusive=False) == 0
+hs = raw(np.zeros_like(xs[rank]))
+L.MPI_Scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+rc = L.MPI_Scan(xs[rank].ctypes.data, hs.ctypes.data, cnt, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+if rc: fails.append(f"host scan rc={rc} {msx.last_error()}")
+else: check("host scan pinned", hs, es[rank])
+
 # MPI_Ireduce / MPI_Ireduce_scatter_block / MPI_Ireduce_scatter in flight together,
 # completed by one MPI_Waitall (issue order = execution order on every rank)
 cnt = 30001
