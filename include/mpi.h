@@ -266,6 +266,19 @@ MPI_METHOD MPI_Wait(MPI_Request* request, MPI_Status* status);
 MPI_METHOD MPI_Test(MPI_Request* request, int* flag, MPI_Status* status);
 MPI_METHOD MPI_Waitall(int count, MPI_Request array_of_requests[],
                        MPI_Status array_of_statuses[]);
+/* api/mpi_completion.cpp:226,453,663,1176,1385; api/mpi_request.cpp:52,170 */
+MPI_METHOD MPI_Testall(int count, MPI_Request array_of_requests[], int* flag,
+                       MPI_Status array_of_statuses[]);
+MPI_METHOD MPI_Testany(int count, MPI_Request array_of_requests[], int* index, int* flag,
+                       MPI_Status* status);
+MPI_METHOD MPI_Testsome(int incount, MPI_Request array_of_requests[], int* outcount,
+                        int array_of_indices[], MPI_Status array_of_statuses[]);
+MPI_METHOD MPI_Waitany(int count, MPI_Request array_of_requests[], int* index,
+                       MPI_Status* status);
+MPI_METHOD MPI_Waitsome(int incount, MPI_Request array_of_requests[], int* outcount,
+                        int array_of_indices[], MPI_Status array_of_statuses[]);
+MPI_METHOD MPI_Request_free(MPI_Request* request);
+MPI_METHOD MPI_Request_get_status(MPI_Request request, int* flag, MPI_Status* status);
 
 /* ---- one-sided communication, fence synchronisation (mpi.h:394-395,
  *      434, 500, 5246-5250; api/mpi_win.cpp, api/mpi_rma.cpp) ------------- */
@@ -274,6 +287,9 @@ typedef int MPI_Win;
 typedef int MPI_Info;
 #define MPI_INFO_NULL       ((MPI_Info)0x1c000000)
 #define MPI_PROC_NULL       (-1)
+#define MPI_ANY_SOURCE      (-2)
+#define MPI_ROOT            (-3)
+#define MPI_ANY_TAG         (-1)
 #define MPI_MODE_NOCHECK    1024
 #define MPI_MODE_NOSTORE    2048
 #define MPI_MODE_NOPUT      4096
@@ -482,6 +498,18 @@ MPI_METHOD PMPI_Get_accumulate(const void* origin_addr, int origin_count,
                                MPI_Datatype target_datatype, MPI_Op op, MPI_Win win);
 MPI_METHOD PMPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Datatype datatype,
                              int target_rank, MPI_Aint target_disp, MPI_Op op, MPI_Win win);
+MPI_METHOD PMPI_Testall(int count, MPI_Request array_of_requests[], int* flag,
+                        MPI_Status array_of_statuses[]);
+MPI_METHOD PMPI_Testany(int count, MPI_Request array_of_requests[], int* index, int* flag,
+                        MPI_Status* status);
+MPI_METHOD PMPI_Testsome(int incount, MPI_Request array_of_requests[], int* outcount,
+                         int array_of_indices[], MPI_Status array_of_statuses[]);
+MPI_METHOD PMPI_Waitany(int count, MPI_Request array_of_requests[], int* index,
+                        MPI_Status* status);
+MPI_METHOD PMPI_Waitsome(int incount, MPI_Request array_of_requests[], int* outcount,
+                         int array_of_indices[], MPI_Status array_of_statuses[]);
+MPI_METHOD PMPI_Request_free(MPI_Request* request);
+MPI_METHOD PMPI_Request_get_status(MPI_Request request, int* flag, MPI_Status* status);
 MPI_METHOD PMPI_Op_create(MPI_User_function* user_fn, int commute, MPI_Op* op);
 MPI_METHOD PMPI_Op_free(MPI_Op* op);
 MPI_METHOD PMPI_Op_commutative(MPI_Op op, int* commute);

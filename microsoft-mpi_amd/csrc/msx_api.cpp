@@ -11,6 +11,7 @@
 //   MPI_Op_create/free/commutative  api/mpi_op.cpp:48-260
 //   validators MpiaOpValidate / MpiaDatatypeValidate  api/mpi_api.h:113-212, 707-775
 //   error return               mpid/error.cpp:85-134 (ERRORS_ARE_FATAL default)
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -769,22 +770,275 @@ MSX_EXPORT int MPI_Test(MPI_Request* request, int* flag, MPI_Status* status)
     return err_return(nullptr, "MPI_Test", request_test(request, flag, status));
 }
 
+// ---- multi-request completion (api/mpi_completion.cpp, api/mpi_request.cpp) ----
+// Argument checks, the handling of MPI_REQUEST_NULL entries, MPI_ERR_IN_STATUS
+// / MPI_ERR_PENDING reporting and which outcomes go through the error handler
+// follow the reference function by function.
+namespace {
+MPI_Status* status_at(MPI_Status* statuses, int i)
+{
+    return statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &statuses[i];
+}
+void status_set_error(MPI_Status* st, int rc)
+{
+    if (st != MPI_STATUS_IGNORE && st != nullptr) st->MPI_ERROR = rc;
+}
+}  // namespace
+
+// mpi_completion.cpp:1022-1140: an error completes nothing further (the rest
+// get MPI_ERR_PENDING); MPI_ERR_IN_STATUS is returned without the handler
 MSX_EXPORT int MPI_Waitall(int count, MPI_Request reqs[], MPI_Status statuses[])
 {
     MSX_REQUIRE_INIT("MPI_Waitall");
-    int rc = MPI_SUCCESS;
-    for (int i = 0; i < count; ++i) {
-        MPI_Status* st = (statuses == MPI_STATUSES_IGNORE || statuses == nullptr) ? MPI_STATUS_IGNORE
-                                                                                  : &statuses[i];
-        int r = request_wait(&reqs[i], st);
-        if (r != MPI_SUCCESS && rc == MPI_SUCCESS) rc = r;
+    if (count < 0) { set_error("negative count %d", count); return err_return(nullptr, "MPI_Waitall", MPI_ERR_COUNT); }
+    if (count != 0 && (!reqs || !statuses)) {
+        set_error("null %s", !reqs ? "array_of_requests" : "array_of_statuses");
+        return err_return(nullptr, "MPI_Waitall", MPI_ERR_ARG);
     }
-    return err_return(nullptr, "MPI_Waitall", rc);
+    int rc = MPI_SUCCESS;
+    bool have_errors = false;
+    for (int i = 0; i < count; ++i) {
+        MPI_Status* st = status_at(statuses, i);
+        if (reqs[i] == MPI_REQUEST_NULL) { status_set_empty(st); continue; }
+        int v = request_validate(reqs[i]);
+        if (v != MPI_SUCCESS) {
+            rc = MPI_ERR_IN_STATUS;
+            status_set_error(st, v);
+            have_errors = true;
+            continue;
+        }
+        if (have_errors) { status_set_error(st, MPI_ERR_PENDING); continue; }
+        int r = request_wait(&reqs[i], st);
+        status_set_error(st, r);
+        if (r != MPI_SUCCESS) { rc = MPI_ERR_IN_STATUS; have_errors = true; }
+    }
+    return rc;
+}
+
+// mpi_completion.cpp:226-417
+MSX_EXPORT int MPI_Testall(int count, MPI_Request reqs[], int* flag, MPI_Status statuses[])
+{
+    MSX_REQUIRE_INIT("MPI_Testall");
+    if (count < 0) { set_error("negative count %d", count); return err_return(nullptr, "MPI_Testall", MPI_ERR_COUNT); }
+    if (!flag) { set_error("null flag"); return err_return(nullptr, "MPI_Testall", MPI_ERR_ARG); }
+    if (count != 0 && (!reqs || !statuses)) {
+        set_error("null %s", !reqs ? "array_of_requests" : "array_of_statuses");
+        return err_return(nullptr, "MPI_Testall", MPI_ERR_ARG);
+    }
+    for (int i = 0; i < count; ++i)
+        if (reqs[i] != MPI_REQUEST_NULL && request_validate(reqs[i]) != MPI_SUCCESS)
+            return err_return(nullptr, "MPI_Testall", MPI_ERR_REQUEST);
+    int n_completed = 0, rc = MPI_SUCCESS;
+    std::vector<char> done((size_t)count, 0);
+    for (int i = 0; i < count; ++i) {
+        if (reqs[i] == MPI_REQUEST_NULL) { ++n_completed; continue; }
+        if (!request_done(reqs[i])) continue;
+        done[(size_t)i] = 1;
+        ++n_completed;
+        if (request_error(reqs[i]) != MPI_SUCCESS) rc = MPI_ERR_IN_STATUS;
+    }
+    if (n_completed == count || rc == MPI_ERR_IN_STATUS) {
+        n_completed = 0;
+        for (int i = 0; i < count; ++i) {
+            MPI_Status* st = status_at(statuses, i);
+            if (reqs[i] == MPI_REQUEST_NULL) {
+                ++n_completed;
+                status_set_empty(st);
+            } else if (done[(size_t)i]) {
+                ++n_completed;
+                int f = 0;
+                const int r = request_test(&reqs[i], &f, st);
+                if (rc == MPI_ERR_IN_STATUS) status_set_error(st, r);
+            } else if (rc == MPI_ERR_IN_STATUS) {
+                status_set_error(st, MPI_ERR_PENDING);
+            }
+        }
+    }
+    *flag = n_completed == count;
+    return err_return(nullptr, "MPI_Testall", rc);
+}
+
+// mpi_completion.cpp:453-625: the completed request's code is returned
+// without the handler
+MSX_EXPORT int MPI_Testany(int count, MPI_Request reqs[], int* index, int* flag, MPI_Status* status)
+{
+    MSX_REQUIRE_INIT("MPI_Testany");
+    if (count < 0) { set_error("negative count %d", count); return err_return(nullptr, "MPI_Testany", MPI_ERR_COUNT); }
+    if ((count != 0 && (!reqs || !status)) || !index || !flag) {
+        set_error("null argument");
+        return err_return(nullptr, "MPI_Testany", MPI_ERR_ARG);
+    }
+    int n_inactive = 0;
+    for (int i = 0; i < count; ++i) {
+        if (reqs[i] == MPI_REQUEST_NULL) { ++n_inactive; continue; }
+        if (request_validate(reqs[i]) != MPI_SUCCESS) return err_return(nullptr, "MPI_Testany", MPI_ERR_REQUEST);
+    }
+    *index = MPI_UNDEFINED;
+    if (n_inactive == count) {
+        *flag = 1;
+        if (status) status_set_empty(status);
+        return MPI_SUCCESS;
+    }
+    *flag = 0;
+    for (int i = 0; i < count; ++i) {
+        if (reqs[i] == MPI_REQUEST_NULL || !request_done(reqs[i])) continue;
+        int f = 0;
+        const int r = request_test(&reqs[i], &f, status);
+        *flag = 1;
+        *index = i;
+        return r;
+    }
+    return MPI_SUCCESS;
+}
+
+// mpi_completion.cpp:1176-1333
+MSX_EXPORT int MPI_Waitany(int count, MPI_Request reqs[], int* index, MPI_Status* status)
+{
+    MSX_REQUIRE_INIT("MPI_Waitany");
+    if (count < 0) { set_error("negative count %d", count); return err_return(nullptr, "MPI_Waitany", MPI_ERR_COUNT); }
+    if ((count != 0 && (!reqs || !status)) || !index) {
+        set_error("null argument");
+        return err_return(nullptr, "MPI_Waitany", MPI_ERR_ARG);
+    }
+    int n_inactive = 0;
+    for (int i = 0; i < count; ++i) {
+        if (reqs[i] == MPI_REQUEST_NULL) { ++n_inactive; continue; }
+        if (request_validate(reqs[i]) != MPI_SUCCESS) return err_return(nullptr, "MPI_Waitany", MPI_ERR_REQUEST);
+    }
+    if (n_inactive == count) {
+        *index = MPI_UNDEFINED;
+        status_set_empty(status);
+        return MPI_SUCCESS;
+    }
+    for (int it = 0;; ++it) {
+        for (int i = 0; i < count; ++i) {
+            if (reqs[i] == MPI_REQUEST_NULL || !request_done(reqs[i])) continue;
+            int f = 0;
+            const int r = request_test(&reqs[i], &f, status);
+            *index = i;
+            return r;
+        }
+        progress_pause(it);
+    }
+}
+
+namespace {
+// the completion pass shared by MPI_Testsome and MPI_Waitsome
+// (mpi_completion.cpp:765-837, 1491-1566)
+int complete_some(int incount, MPI_Request reqs[], int* outcount, int indices[], MPI_Status statuses[],
+                  int* n_inactive)
+{
+    int n_active = 0, rc = MPI_SUCCESS;
+    std::vector<int> failed;
+    for (int i = 0; i < incount; ++i) {
+        if (reqs[i] == MPI_REQUEST_NULL || !request_done(reqs[i])) continue;
+        MPI_Status* st = status_at(statuses, n_active);
+        int f = 0;
+        const int r = request_test(&reqs[i], &f, st);
+        indices[n_active] = i;
+        if (r != MPI_SUCCESS) {
+            rc = MPI_ERR_IN_STATUS;
+            status_set_error(st, r);
+            failed.push_back(n_active);
+        }
+        ++n_active;
+    }
+    (void)n_inactive;
+    if (rc == MPI_ERR_IN_STATUS && statuses != MPI_STATUSES_IGNORE)
+        for (int k = 0; k < n_active; ++k)
+            if (std::find(failed.begin(), failed.end(), k) == failed.end()) statuses[k].MPI_ERROR = MPI_SUCCESS;
+    *outcount = n_active;
+    return rc;
+}
+}  // namespace
+
+// mpi_completion.cpp:663-862: MPI_ERR_IN_STATUS goes through the handler
+MSX_EXPORT int MPI_Testsome(int incount, MPI_Request reqs[], int* outcount, int indices[], MPI_Status statuses[])
+{
+    MSX_REQUIRE_INIT("MPI_Testsome");
+    if (incount < 0) { set_error("negative count %d", incount); return err_return(nullptr, "MPI_Testsome", MPI_ERR_COUNT); }
+    if ((incount != 0 && (!reqs || !indices || !statuses)) || !outcount) {
+        set_error("null argument");
+        return err_return(nullptr, "MPI_Testsome", MPI_ERR_ARG);
+    }
+    *outcount = 0;
+    int n_inactive = 0;
+    for (int i = 0; i < incount; ++i) {
+        if (reqs[i] == MPI_REQUEST_NULL) { ++n_inactive; continue; }
+        if (request_validate(reqs[i]) != MPI_SUCCESS) return err_return(nullptr, "MPI_Testsome", MPI_ERR_REQUEST);
+    }
+    if (n_inactive == incount) { *outcount = MPI_UNDEFINED; return MPI_SUCCESS; }
+    const int rc = complete_some(incount, reqs, outcount, indices, statuses, &n_inactive);
+    return err_return(nullptr, "MPI_Testsome", rc);
+}
+
+// mpi_completion.cpp:1385-1595: blocks until at least one completes;
+// MPI_ERR_IN_STATUS is returned without the handler
+MSX_EXPORT int MPI_Waitsome(int incount, MPI_Request reqs[], int* outcount, int indices[], MPI_Status statuses[])
+{
+    MSX_REQUIRE_INIT("MPI_Waitsome");
+    if (incount < 0) { set_error("negative count %d", incount); return err_return(nullptr, "MPI_Waitsome", MPI_ERR_COUNT); }
+    if ((incount != 0 && (!reqs || !indices || !statuses)) || !outcount) {
+        set_error("null argument");
+        return err_return(nullptr, "MPI_Waitsome", MPI_ERR_ARG);
+    }
+    *outcount = 0;
+    int n_inactive = 0;
+    for (int i = 0; i < incount; ++i) {
+        if (reqs[i] == MPI_REQUEST_NULL) { ++n_inactive; continue; }
+        if (request_validate(reqs[i]) != MPI_SUCCESS) return err_return(nullptr, "MPI_Waitsome", MPI_ERR_REQUEST);
+    }
+    if (n_inactive == incount) { *outcount = MPI_UNDEFINED; return MPI_SUCCESS; }
+    for (int it = 0;; ++it) {
+        const int rc = complete_some(incount, reqs, outcount, indices, statuses, &n_inactive);
+        if (*outcount > 0) return rc;
+        progress_pause(it);
+    }
+}
+
+// mpi_request.cpp:52-141: the reference frees only point-to-point, RMA,
+// persistent and generalized requests; a collective (NBC) request is an
+// invalid kind there (MPI_ERR_OTHER, "**request_invalid_kind")
+MSX_EXPORT int MPI_Request_free(MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Request_free");
+    if (!request) { set_error("null request"); return err_return(nullptr, "MPI_Request_free", MPI_ERR_ARG); }
+    int rc = request_validate(*request);
+    if (rc == MPI_SUCCESS) {
+        set_error("request 0x%x: invalid kind (a nonblocking collective request cannot be freed)",
+                  (unsigned)*request);
+        rc = MPI_ERR_OTHER;
+    }
+    return err_return(nullptr, "MPI_Request_free", rc);
+}
+
+// mpi_request.cpp:170-330: non-destructive; an NBC request's status is left
+// as the caller passed it
+MSX_EXPORT int MPI_Request_get_status(MPI_Request request, int* flag, MPI_Status* status)
+{
+    MSX_REQUIRE_INIT("MPI_Request_get_status");
+    if (!flag || !status) { set_error("null argument"); return err_return(nullptr, "MPI_Request_get_status", MPI_ERR_ARG); }
+    if (request == MPI_REQUEST_NULL) {
+        status_set_empty(status);
+        *flag = 1;
+        return MPI_SUCCESS;
+    }
+    const int rc = request_validate(request);
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Request_get_status", rc);
+    *flag = request_done(request) ? 1 : 0;
+    return MPI_SUCCESS;
 }
 
 // ---- PMPI_ profiling aliases (dll/msmpi.def) --------------------------------
 #define MSX_ALIAS(name) extern "C" __attribute__((visibility("default"), alias(#name)))
 MSX_ALIAS(MPI_Reduce_local) int PMPI_Reduce_local(const void*, void*, int, MPI_Datatype, MPI_Op);
+MSX_ALIAS(MPI_Testall) int PMPI_Testall(int, MPI_Request[], int*, MPI_Status[]);
+MSX_ALIAS(MPI_Testany) int PMPI_Testany(int, MPI_Request[], int*, int*, MPI_Status*);
+MSX_ALIAS(MPI_Testsome) int PMPI_Testsome(int, MPI_Request[], int*, int[], MPI_Status[]);
+MSX_ALIAS(MPI_Waitany) int PMPI_Waitany(int, MPI_Request[], int*, MPI_Status*);
+MSX_ALIAS(MPI_Waitsome) int PMPI_Waitsome(int, MPI_Request[], int*, int[], MPI_Status[]);
+MSX_ALIAS(MPI_Request_free) int PMPI_Request_free(MPI_Request*);
+MSX_ALIAS(MPI_Request_get_status) int PMPI_Request_get_status(MPI_Request, int*, MPI_Status*);
 MSX_ALIAS(MPI_Reduce) int PMPI_Reduce(const void*, void*, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
 MSX_ALIAS(MPI_Allreduce) int PMPI_Allreduce(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);
 MSX_ALIAS(MPI_Reduce_scatter_block) int PMPI_Reduce_scatter_block(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);

@@ -9,6 +9,7 @@
 
 #include <atomic>
 #include <deque>
+#include <thread>
 #include <chrono>
 #include <functional>
 #include <future>
@@ -380,6 +381,54 @@ int request_test(MPI_Request* req, int* flag, MPI_Status* st)
     *req = MPI_REQUEST_NULL;
     fill_status(st, rc);
     return rc;
+}
+
+// MpiaRequestValidate (api/mpi_api.h): a live request handle of this process
+int request_validate(MPI_Request h)
+{
+    if (!req_lookup(h)) {
+        set_error("invalid request handle 0x%x", (unsigned)h);
+        return MPI_ERR_REQUEST;
+    }
+    return MPI_SUCCESS;
+}
+
+// request_ptr->test_complete(): non-destructive; the request stays live
+bool request_done(MPI_Request h)
+{
+    Request* r = req_lookup(h);
+    if (!r) return true;
+    if (!r->done && r->has_fut) {
+        if (r->fut.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return false;
+        r->rc = r->fut.get();
+        r->done = true;
+    }
+    return true;
+}
+
+// MPIR_Request_get_error: the completed request's error code
+int request_error(MPI_Request h)
+{
+    Request* r = req_lookup(h);
+    return r ? r->rc : MPI_ERR_REQUEST;
+}
+
+// MPIR_Status_set_empty (include/mpierror.h): source ANY, tag ANY, no error
+void status_set_empty(MPI_Status* st)
+{
+    if (st == MPI_STATUS_IGNORE || st == nullptr) return;
+    st->MPI_SOURCE = -2;    // MPI_ANY_SOURCE
+    st->MPI_TAG = -1;       // MPI_ANY_TAG
+    st->MPI_ERROR = MPI_SUCCESS;
+    st->internal[0] = st->internal[1] = 0;
+}
+
+// MPID_Progress_wait: the engine worker makes the progress; the caller
+// spins briefly, then yields its core in short sleeps
+void progress_pause(int iter)
+{
+    if (iter < 2000) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(20));
 }
 
 int request_wait(MPI_Request* req, MPI_Status* st)

@@ -70,5 +70,11 @@ int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req,
                           MPI_Datatype hold = MPI_DATATYPE_NULL);
 int request_wait(MPI_Request* req, MPI_Status* st);
 int request_test(MPI_Request* req, int* flag, MPI_Status* st);
+// completion helpers of the multi-request calls (api/mpi_completion.cpp)
+int request_validate(MPI_Request h);         // MPI_SUCCESS or MPI_ERR_REQUEST
+bool request_done(MPI_Request h);            // non-destructive completion test
+int request_error(MPI_Request h);            // error code of a completed request
+void status_set_empty(MPI_Status* st);
+void progress_pause(int iter);
 
 }  // namespace msx

@@ -315,6 +315,55 @@ FAPI void mpi_waitall_(const MPI_Fint* n, MPI_Fint* reqs, MPI_Fint* sts, MPI_Fin
     *ierr = MPI_Waitall(*n, reqs, statuses(sts));
 }
 FNAMES(waitall, WAITALL)
+FAPI void mpi_testall_(const MPI_Fint* n, MPI_Fint* reqs, MPI_Fint* flag, MPI_Fint* sts, MPI_Fint* ierr)
+{
+    int f = 0;
+    *ierr = MPI_Testall(*n, reqs, &f, statuses(sts));
+    *flag = to_flog(f);
+}
+FNAMES(testall, TESTALL)
+// indices are 1-based in Fortran (mpif.cpp:190-263); MPI_UNDEFINED stays as is
+FAPI void mpi_waitany_(const MPI_Fint* n, MPI_Fint* reqs, MPI_Fint* index, MPI_Fint* st, MPI_Fint* ierr)
+{
+    int i = 0;
+    *ierr = MPI_Waitany(*n, reqs, &i, status(st));
+    *index = i >= 0 ? i + 1 : i;
+}
+FNAMES(waitany, WAITANY)
+FAPI void mpi_testany_(const MPI_Fint* n, MPI_Fint* reqs, MPI_Fint* index, MPI_Fint* flag, MPI_Fint* st,
+                       MPI_Fint* ierr)
+{
+    int i = 0, f = 0;
+    *ierr = MPI_Testany(*n, reqs, &i, &f, status(st));
+    *index = i >= 0 ? i + 1 : i;
+    *flag = to_flog(f);
+}
+FNAMES(testany, TESTANY)
+FAPI void mpi_waitsome_(const MPI_Fint* n, MPI_Fint* reqs, MPI_Fint* outcount, MPI_Fint* indices, MPI_Fint* sts,
+                        MPI_Fint* ierr)
+{
+    *ierr = MPI_Waitsome(*n, reqs, outcount, indices, statuses(sts));
+    for (int k = 0; k < *outcount; ++k)
+        if (indices[k] >= 0) indices[k] += 1;
+}
+FNAMES(waitsome, WAITSOME)
+FAPI void mpi_testsome_(const MPI_Fint* n, MPI_Fint* reqs, MPI_Fint* outcount, MPI_Fint* indices, MPI_Fint* sts,
+                        MPI_Fint* ierr)
+{
+    *ierr = MPI_Testsome(*n, reqs, outcount, indices, statuses(sts));
+    for (int k = 0; k < *outcount; ++k)
+        if (indices[k] >= 0) indices[k] += 1;
+}
+FNAMES(testsome, TESTSOME)
+FAPI void mpi_request_free_(MPI_Fint* req, MPI_Fint* ierr) { *ierr = MPI_Request_free(req); }
+FNAMES(request_free, REQUEST_FREE)
+FAPI void mpi_request_get_status_(const MPI_Fint* req, MPI_Fint* flag, MPI_Fint* st, MPI_Fint* ierr)
+{
+    int f = 0;
+    *ierr = MPI_Request_get_status(*req, &f, status(st));
+    *flag = to_flog(f);
+}
+FNAMES(request_get_status, REQUEST_GET_STATUS)
 
 // ---- datatypes (mpif.cpp:401-548, 3253-3300, 3800-3815) ---------------------------
 FAPI void mpi_type_size_(const MPI_Fint* dt, MPI_Fint* size, MPI_Fint* ierr) { *ierr = MPI_Type_size(*dt, size); }

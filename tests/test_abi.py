@@ -128,6 +128,89 @@ def test_no_gpu_fails_loudly_not_silently(msxlib):
                                        None) == C.MPI_ERR_OTHER
 
 
+class _Status(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_int * 2), ("MPI_SOURCE", ctypes.c_int), ("MPI_TAG", ctypes.c_int),
+                ("MPI_ERROR", ctypes.c_int)]
+
+
+def test_request_completion_semantics(msxlib):
+    """MPI_Waitall/Testall/Waitany/Testany/Waitsome/Testsome/Request_free/
+    Request_get_status as api/mpi_completion.cpp and api/mpi_request.cpp
+    define them: REQUEST_NULL entries, MPI_UNDEFINED results, 1 request
+    completed per *any call, MPI_ERR_IN_STATUS with MPI_ERR_PENDING for the
+    entries after a bad handle, argument errors.  One-rank nonblocking
+    collectives complete at the call (host buffers: no GPU involved)."""
+    L = msxlib
+    UNDEF, NULLREQ = -32766, C.MPI_REQUEST_NULL
+    src = np.arange(4, dtype=np.int32)
+    outs = []
+
+    def start():
+        out = np.zeros(4, np.int32)
+        outs.append(out)
+        r = ctypes.c_int()
+        assert L.MPI_Iallreduce(src.ctypes.data, out.ctypes.data, 4, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD,
+                                ctypes.byref(r)) == 0
+        return r.value
+
+    IGN = ctypes.c_void_p(1)                  # MPI_STATUS(ES)_IGNORE
+    reqs = (ctypes.c_int * 3)(start(), NULLREQ, start())
+    sts = (_Status * 3)()
+    assert L.MPI_Waitall(3, reqs, sts) == 0
+    assert list(reqs) == [NULLREQ] * 3
+    assert (sts[1].MPI_SOURCE, sts[1].MPI_TAG, sts[1].MPI_ERROR) == (-2, -1, 0)
+    assert all((o == src).all() for o in outs)
+    # a bad handle: MPI_ERR_IN_STATUS, later entries MPI_ERR_PENDING and untouched
+    reqs = (ctypes.c_int * 3)(start(), 0x2C00FFF0, start())
+    live = reqs[2]
+    assert L.MPI_Waitall(3, reqs, sts) == C.MPI_ERR_IN_STATUS
+    assert reqs[0] == NULLREQ and sts[0].MPI_ERROR == 0
+    assert sts[1].MPI_ERROR == C.MPI_ERR_REQUEST and sts[2].MPI_ERROR == 18 and reqs[2] == live
+    r = ctypes.c_int(live)
+    assert L.MPI_Wait(ctypes.byref(r), IGN) == 0 and r.value == NULLREQ
+    # Testall: flag and all handles released
+    reqs = (ctypes.c_int * 2)(start(), start())
+    flag = ctypes.c_int(-1)
+    assert L.MPI_Testall(2, reqs, ctypes.byref(flag), IGN) == 0 and flag.value == 1
+    assert list(reqs) == [NULLREQ] * 2
+    # Testany / Waitany: one request per call, MPI_UNDEFINED when none is active
+    reqs = (ctypes.c_int * 3)(NULLREQ, start(), start())
+    idx, st = ctypes.c_int(-1), _Status()
+    assert L.MPI_Testany(3, reqs, ctypes.byref(idx), ctypes.byref(flag), ctypes.byref(st)) == 0
+    assert (idx.value, flag.value, reqs[1]) == (1, 1, NULLREQ) and reqs[2] != NULLREQ
+    assert L.MPI_Waitany(3, reqs, ctypes.byref(idx), ctypes.byref(st)) == 0 and idx.value == 2
+    assert L.MPI_Waitany(3, reqs, ctypes.byref(idx), ctypes.byref(st)) == 0 and idx.value == UNDEF
+    assert (st.MPI_SOURCE, st.MPI_TAG, st.MPI_ERROR) == (-2, -1, 0)
+    assert L.MPI_Testany(3, reqs, ctypes.byref(idx), ctypes.byref(flag), ctypes.byref(st)) == 0
+    assert (idx.value, flag.value) == (UNDEF, 1)
+    # Testsome / Waitsome: every completed request, outcount MPI_UNDEFINED when none active
+    reqs = (ctypes.c_int * 3)(start(), NULLREQ, start())
+    n, ind = ctypes.c_int(-1), (ctypes.c_int * 3)()
+    assert L.MPI_Testsome(3, reqs, ctypes.byref(n), ind, IGN) == 0
+    assert n.value == 2 and list(ind)[:2] == [0, 2] and list(reqs) == [NULLREQ] * 3
+    assert L.MPI_Waitsome(3, reqs, ctypes.byref(n), ind, IGN) == 0 and n.value == UNDEF
+    reqs[0] = start()
+    assert L.MPI_Waitsome(3, reqs, ctypes.byref(n), ind, sts) == 0 and n.value == 1 and ind[0] == 0
+    # Request_get_status is non-destructive; Request_free refuses an NBC request
+    r = ctypes.c_int(start())
+    h0 = r.value
+    assert L.MPI_Request_get_status(r.value, ctypes.byref(flag), ctypes.byref(st)) == 0
+    assert flag.value == 1 and r.value == h0
+    assert L.MPI_Request_free(ctypes.byref(r)) == C.MPI_ERR_OTHER and r.value == h0
+    assert L.MPI_Test(ctypes.byref(r), ctypes.byref(flag), IGN) == 0 and r.value == NULLREQ
+    assert L.MPI_Request_get_status(NULLREQ, ctypes.byref(flag), ctypes.byref(st)) == 0 and flag.value == 1
+    assert L.MPI_Request_get_status(h0, ctypes.byref(flag), ctypes.byref(st)) == C.MPI_ERR_REQUEST
+    # argument errors
+    assert L.MPI_Waitall(-1, reqs, sts) == C.MPI_ERR_COUNT
+    assert L.MPI_Waitall(1, None, sts) == C.MPI_ERR_ARG
+    assert L.MPI_Testall(1, reqs, None, sts) == C.MPI_ERR_ARG
+    assert L.MPI_Waitany(1, reqs, None, ctypes.byref(st)) == C.MPI_ERR_ARG
+    assert L.MPI_Testsome(1, reqs, None, ind, sts) == C.MPI_ERR_ARG
+    assert L.MPI_Request_free(None) == C.MPI_ERR_ARG
+    bad = (ctypes.c_int * 1)(0x2C00FFF0)
+    assert L.MPI_Testany(1, bad, ctypes.byref(idx), ctypes.byref(flag), ctypes.byref(st)) == C.MPI_ERR_REQUEST
+
+
 def _run_py(code, env=None):
     e = dict(os.environ)
     e.update(env or {})
