@@ -262,7 +262,7 @@ def main(out_path, scale):
     rc2 = L.MPI_Iallreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD,
                            ctypes.byref(req))
     host_work(K)
-    rc3 = L.MPI_Wait(ctypes.byref(req), None)
+    rc3 = L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1))
     t_total = time.perf_counter() - t0
     log(f"c5 done rc={rc},{rc2},{rc3} comm={t_comm:.4f} host={t_host:.4f} total={t_total:.4f}")
     if rc or rc2 or rc3:

@@ -759,14 +759,21 @@ MSX_EXPORT int MPI_Ireduce_scatter_block(const void* sendbuf, void* recvbuf, int
 MSX_EXPORT int MPI_Wait(MPI_Request* request, MPI_Status* status)
 {
     MSX_REQUIRE_INIT("MPI_Wait");
-    if (!request) { set_error("null request"); return err_return(nullptr, "MPI_Wait", MPI_ERR_ARG); }
+    // mpi_completion.cpp:907-920: MPI_STATUS_IGNORE is not NULL; NULL is an error
+    if (!request || !status) {
+        set_error("null %s", !request ? "request" : "status");
+        return err_return(nullptr, "MPI_Wait", MPI_ERR_ARG);
+    }
     return err_return(nullptr, "MPI_Wait", request_wait(request, status));
 }
 
 MSX_EXPORT int MPI_Test(MPI_Request* request, int* flag, MPI_Status* status)
 {
     MSX_REQUIRE_INIT("MPI_Test");
-    if (!request || !flag) { set_error("null argument"); return err_return(nullptr, "MPI_Test", MPI_ERR_ARG); }
+    if (!request || !flag || !status) {
+        set_error("null %s", !request ? "request" : (!flag ? "flag" : "status"));
+        return err_return(nullptr, "MPI_Test", MPI_ERR_ARG);
+    }
     return err_return(nullptr, "MPI_Test", request_test(request, flag, status));
 }
 

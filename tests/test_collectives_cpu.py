@@ -343,9 +343,9 @@ assert L.MPI_Exscan(send.ctypes.data, exc.ctypes.data, 3, C.MPI_DOUBLE, op.value
 # non-blocking forms give the same results
 inc2, exc2, req = np.zeros(3), np.full(3, 7.0), ctypes.c_int()
 assert L.MPI_Iscan(send.ctypes.data, inc2.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD, ctypes.byref(req)) == 0
-assert L.MPI_Wait(ctypes.byref(req), None) == 0 and req.value == C.MPI_REQUEST_NULL
+assert L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)) == 0 and req.value == C.MPI_REQUEST_NULL
 assert L.MPI_Iexscan(send.ctypes.data, exc2.ctypes.data, 3, C.MPI_DOUBLE, op.value, C.MPI_COMM_WORLD, ctypes.byref(req)) == 0
-assert L.MPI_Wait(ctypes.byref(req), None) == 0
+assert L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)) == 0
 assert (inc2 == inc).all() and (exc2 == exc).all()
 # MPI_Reduce with user ops: the reference's binomial tree (reduce.cpp:440-540)
 opc = ctypes.c_int()

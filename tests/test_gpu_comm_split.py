@@ -78,7 +78,7 @@ if not np.array_equal(host(blk), tot[sr.value * 4096:(sr.value + 1) * 4096]): fa
 req = ctypes.c_int()
 res = dev(np.zeros(n, np.int32))
 ok(L.MPI_Iallreduce(send.data_ptr(), res.data_ptr(), n, C.MPI_INT, C.MPI_SUM, S, ctypes.byref(req)), "sub iallreduce")
-ok(L.MPI_Wait(ctypes.byref(req), None), "wait")
+ok(L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)), "wait")
 if not np.array_equal(host(res), tot): fails.append("sub iallreduce")
 
 ok(L.MPI_Comm_free(ctypes.byref(sub)), "free sub")

@@ -330,7 +330,7 @@ def test_type_freed_while_nonblocking_op_pending(L):
     assert L.MPI_Iallreduce(a.data_ptr(), b.data_ptr(), 2, h, op.value, C.MPI_COMM_WORLD, ctypes.byref(req)) == 0
     x = c_int(h)
     assert L.MPI_Type_free(ctypes.byref(x)) == 0            # user frees it while pending
-    assert L.MPI_Wait(ctypes.byref(req), None) == 0, msx.last_error()
+    assert L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)) == 0, msx.last_error()
     idx = [i * t["map"].extent // 4 + d // 4 for i in range(2) for d, _ in t["map"].typemap]
     exp = np.full(64, -1, np.int32)
     exp[idx] = np.arange(64, dtype=np.int32)[idx]

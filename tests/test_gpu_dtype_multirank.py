@@ -112,7 +112,7 @@ ip = dev(contrib(rank))
 req = ctypes.c_int()
 ok(L.MPI_Iallreduce(ctypes.c_void_p(C.MPI_IN_PLACE), ip.data_ptr(), COUNT, t.value, op.value, C.MPI_COMM_WORLD,
                     ctypes.byref(req)), "iallreduce")
-ok(L.MPI_Wait(ctypes.byref(req), None), "wait")
+ok(L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)), "wait")
 ei = contrib(rank).copy(); ei[K] = total[K]
 chk("iallreduce in place", ip.cpu().numpy(), ei)
 

@@ -153,7 +153,7 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
         rc = fi(ctypes.c_void_p(sb.data_ptr()), ctypes.c_void_p(rb2.data_ptr()), count, dt, op, C.MPI_COMM_WORLD,
                 ctypes.byref(req))
         if rc == 0:
-            rc = L.MPI_Wait(ctypes.byref(req), None)
+            rc = L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1))
         if rc != 0:
             fails.append(f"iscan {opn} excl={excl} rc={rc} {msx.last_error()}")
         elif not (excl and rank == 0):
@@ -231,7 +231,7 @@ rcs = [L.MPI_Ireduce(d_r.data_ptr(), o_r.data_ptr(), cnt, C.MPI_FLOAT, C.MPI_SUM
 if any(rcs):
     fails.append(f"nbc start rc={rcs} {msx.last_error()}")
 else:
-    rc = L.MPI_Waitall(3, reqs, None)
+    rc = L.MPI_Waitall(3, reqs, ctypes.c_void_p(1))
     if rc:
         fails.append(f"waitall rc={rc} {msx.last_error()}")
     else:
@@ -254,13 +254,50 @@ host = np.random.default_rng(1).random(1 << 20)
 flag, polls = ctypes.c_int(0), 0
 while rc == 0 and not flag.value:
     host = 1.0001 * host + 0.5           # host work between tests
-    rc = L.MPI_Test(ctypes.byref(req), ctypes.byref(flag), None)
+    rc = L.MPI_Test(ctypes.byref(req), ctypes.byref(flag), ctypes.c_void_p(1))
     polls += 1
 if rc != 0:
     fails.append(f"iallreduce rc={rc} {msx.last_error()}")
 else:
     check("iallreduce band u64", fromdev(rb, xs[rank]), exp[rank])
 assert req.value == C.MPI_REQUEST_NULL
+
+# Two nonblocking allreduces in flight, completed by MPI_Waitany (one per call,
+# indices in issue order) and a Testsome/Testall poll (api/mpi_completion.cpp)
+xa = inputs("MPI_SUM", "MPI_INT", 200003, 4100)
+xb = inputs("MPI_MAX", "MPI_DOUBLE", 77777, 4101)
+ea, eb = [raw(x.copy()) for x in xa], [raw(x.copy()) for x in xb]
+oracle.allreduce(C.MPI_SUM, C.MPI_INT, xa, ea)
+oracle.allreduce(C.MPI_MAX, C.MPI_DOUBLE, xb, eb)
+sa, ra = todev(xa[rank]), dzeros(xa[rank].nbytes, dtype=torch.uint8, device="cuda")
+sb2, rb2 = todev(xb[rank]), dzeros(xb[rank].nbytes, dtype=torch.uint8, device="cuda")
+reqs = (ctypes.c_int * 2)()
+rcs = [L.MPI_Iallreduce(sa.data_ptr(), ra.data_ptr(), 200003, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD,
+                        ctypes.cast(ctypes.addressof(reqs), ctypes.POINTER(ctypes.c_int))),
+       L.MPI_Iallreduce(sb2.data_ptr(), rb2.data_ptr(), 77777, C.MPI_DOUBLE, C.MPI_MAX, C.MPI_COMM_WORLD,
+                        ctypes.cast(ctypes.addressof(reqs) + 4, ctypes.POINTER(ctypes.c_int)))]
+seen = []
+if any(rcs):
+    fails.append(f"waitany start rc={rcs} {msx.last_error()}")
+else:
+    idx = ctypes.c_int(-1)
+    for _ in range(2):
+        rc = L.MPI_Waitany(2, reqs, ctypes.byref(idx), ctypes.c_void_p(1))
+        if rc: fails.append(f"waitany rc={rc} {msx.last_error()}")
+        seen.append(idx.value)
+    rc = L.MPI_Waitany(2, reqs, ctypes.byref(idx), ctypes.c_void_p(1))
+    if rc or idx.value != -32766 or sorted(seen) != [0, 1]:
+        fails.append(f"waitany order {seen} last={idx.value} rc={rc}")
+    check("waitany allreduce int", fromdev(ra, xa[rank]), ea[rank])
+    check("waitany allreduce dbl", fromdev(rb2, xb[rank]), eb[rank])
+rc = L.MPI_Iallreduce(sa.data_ptr(), ra.data_ptr(), 200003, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD,
+                      ctypes.cast(ctypes.addressof(reqs), ctypes.POINTER(ctypes.c_int)))
+flag, polls = ctypes.c_int(0), 0
+while rc == 0 and not flag.value:
+    rc = L.MPI_Testall(1, reqs, ctypes.byref(flag), ctypes.c_void_p(1))
+    polls += 1
+if rc: fails.append(f"testall rc={rc} {msx.last_error()}")
+else: check("testall allreduce int", fromdev(ra, xa[rank]), ea[rank])
 
 # Back-to-back stress of the barrier-free small allreduce (GPU arrival flags,
 # alternating IN halves; with MSX_RD_FLAGS=0 the host-barrier variant)
@@ -292,7 +329,7 @@ for it in range(240):
         req = ctypes.c_int()
         rc = L.MPI_Iallreduce(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD,
                               ctypes.byref(req))
-        rc = rc or L.MPI_Wait(ctypes.byref(req), None)
+        rc = rc or L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1))
     elif it % 5 == 2:                      # in place
         rb = sb
         rc = L.MPI_Allreduce(ctypes.c_void_p(C.MPI_IN_PLACE), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM,
