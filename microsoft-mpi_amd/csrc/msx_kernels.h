@@ -54,6 +54,20 @@ struct TreeSpec {
     int wait_n = 0;
     int wait_skip = -1;
     int* wait_err = nullptr;
+    // Fused push (the barrier-free small allreduce in one launch): extra
+    // workgroups copy push_n[i] bytes push_src[i] -> push_dst[i] with
+    // system-coherent stores and, once all of them completed, store push_seq
+    // to every push_flags[j] -- k_push_post's work, in the tree's launch.
+    // push_counter: the transport's zeroed completion word (left zero again).
+    int push_nseg = 0;
+    const void* push_src[32] = {};
+    void* push_dst[32] = {};
+    size_t push_n[32] = {};
+    int push_nflags = 0;
+    unsigned long long* push_flags[64] = {};
+    unsigned long long push_seq = 0;
+    unsigned* push_counter = nullptr;
+    bool push_sys = false;
 };
 hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t count,
                             hipStream_t s);

@@ -230,6 +230,63 @@ __global__ __launch_bounds__(BLOCK) void k_combine_lds(const T* __restrict__ in,
     }
 }
 
+// ---- copy-segment and flag descriptors (k_copy_segs, k_push_post, k_tree) -------
+constexpr int kMaxSegs = 32;
+struct CopySegs {
+    const void* src[kMaxSegs];
+    void* dst[kMaxSegs];
+    size_t nbytes[kMaxSegs];
+    int n;
+    int sys;
+};
+
+struct PostFlags {
+    unsigned long long* dst[64];
+    unsigned long long seq;
+    int n;
+};
+
+// The small-allreduce push (k_push_post, and the first workgroups of a fused
+// k_tree launch): see the comment at k_push_post.
+__device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
+                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
+{
+    const char* src = static_cast<const char*>(c.src[sg]);
+    char* dst = static_cast<char*>(c.dst[sg]);
+    const size_t nb = c.nbytes[sg];
+    const size_t stride = (size_t)gx * 256;
+    size_t done = 0;
+    bool plain = false;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const size_t nv = nb / 16;
+        for (size_t i = (size_t)bx * 256 + threadIdx.x; i < nv; i += stride) {
+            const u32x4 v = reinterpret_cast<const u32x4*>(src)[i];
+            unsigned long long* d = reinterpret_cast<unsigned long long*>(dst) + 2 * i;
+            __hip_atomic_store(d, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(d + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        done = nv * 16;
+    }
+    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) {
+        dst[i] = src[i];
+        plain = true;
+    }
+    if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
+    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // vmcnt(0): this lane's stores completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == total - 1) {
+            if (sys) __threadfence_system();
+            for (int k = 0; k < f.n; ++k)
+                __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
+        }
+    }
+}
+
 // ---- reference-order multi-input combine ----------------------------------------
 // One pass over up to 2*kMaxLeaves inputs that reproduces the association AND
 // the inout/in roles of the reference's multi-step schedules:
@@ -256,6 +313,15 @@ struct TreeArgs {
     int wait_n;
     int wait_skip;
     int* wait_err;
+    // fused push (barrier-free small allreduce): the first npush workgroups
+    // copy this rank's contribution into the peers' IN halves and post the
+    // arrival flags (push_post_body) instead of evaluating the tree
+    unsigned npush;
+    unsigned push_gx;     // workgroups per push segment
+    int push_sys;
+    unsigned* push_counter;
+    CopySegs push;
+    PostFlags flags;
 };
 
 // Arrival wait of the barrier-free small allreduce: thread 0 of every
@@ -389,8 +455,20 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
                                                 size_t tail, int vec_ok)
 {
     constexpr size_t EPV = 16 / sizeof(T);
-    const size_t stride = (size_t)gridDim.x * BLOCK;
-    const size_t bid = xcd_tile(blockIdx.x, gridDim.x);      // XCD-contiguous (see combine_body)
+    unsigned b = blockIdx.x, nb = gridDim.x;
+    if (a.npush) {
+        // fused push: the first npush workgroups push this rank's vector and
+        // post its flags; they never wait, so the peers' trees always progress
+        if (b < a.npush) {
+            push_post_body(a.push, a.flags, a.push_counter, a.npush, a.push_sys, b % a.push_gx, a.push_gx,
+                           (int)(b / a.push_gx));
+            return;
+        }
+        b -= a.npush;
+        nb -= a.npush;
+    }
+    const size_t stride = (size_t)nb * BLOCK;
+    const size_t bid = xcd_tile(b, nb);      // XCD-contiguous (see combine_body)
     if (a.wait_flags && !arrival_wait(a)) return;
     if (a.sys) acquire_system();
     if (vec_ok) {
@@ -408,7 +486,7 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
     }
     const size_t first = vec_ok ? nvec * EPV : 0;
     const size_t nsc = vec_ok ? tail : tail + nvec * EPV;
-    for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nsc; s += stride) {
+    for (size_t s = (size_t)b * BLOCK + threadIdx.x; s < nsc; s += stride) {
         auto load = [&](int k) { return reinterpret_cast<const T*>(a.s[k])[first + s]; };
         const T r = tree_eval<Fn<OP>, T>(a, load);
         out[first + s] = r;
@@ -418,21 +496,6 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
 }
 
 // ---- multi-segment copy (allgather phase: blocks pulled from peers) -------------
-constexpr int kMaxSegs = 32;
-struct CopySegs {
-    const void* src[kMaxSegs];
-    void* dst[kMaxSegs];
-    size_t nbytes[kMaxSegs];
-    int n;
-    int sys;
-};
-
-struct PostFlags {
-    unsigned long long* dst[64];
-    unsigned long long seq;
-    int n;
-};
-
 __global__ __launch_bounds__(64) void k_post_flags(PostFlags f)
 {
     if (threadIdx.x < (unsigned)f.n)
@@ -483,41 +546,7 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
 __global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
                                                    int sys)
 {
-    const int sg = blockIdx.y;
-    const char* src = static_cast<const char*>(c.src[sg]);
-    char* dst = static_cast<char*>(c.dst[sg]);
-    const size_t nb = c.nbytes[sg];
-    const size_t stride = (size_t)gridDim.x * 256;
-    size_t done = 0;
-    bool plain = false;
-    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
-        const size_t nv = nb / 16;
-        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += stride) {
-            const u32x4 v = reinterpret_cast<const u32x4*>(src)[i];
-            unsigned long long* d = reinterpret_cast<unsigned long long*>(dst) + 2 * i;
-            __hip_atomic_store(d, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(d + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        done = nv * 16;
-    }
-    for (size_t i = done + (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) {
-        dst[i] = src[i];
-        plain = true;
-    }
-    if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
-    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // vmcnt(0): this lane's stores completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == total - 1) {
-            if (sys) __threadfence_system();
-            for (int k = 0; k < f.n; ++k)
-                __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
-        }
-    }
+    push_post_body(c, f, counter, total, sys, blockIdx.x, gridDim.x, blockIdx.y);
 }
 
 }  // namespace dev
@@ -726,6 +755,7 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
     const size_t cap = g_tree_tune.grid_cap > 0 ? (size_t)g_tree_tune.grid_cap : (size_t)kTreeGridCap;
     if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
+    grid += a.npush;                         // fused push workgroups come first
     hipLaunchKernelGGL((k_tree<OP, T, VT, kBlock, UPFRONT, NT>), dim3((unsigned)grid), dim3(kBlock), 0, s, a,
                        static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
     return hipGetLastError();
@@ -860,7 +890,29 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     a.wait_skip = t.wait_skip;
     a.wait_err = t.wait_err;
     if (t.wait_flags && (!t.wait_err || t.wait_n < 0)) return hipErrorInvalidValue;
-    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.wait_flags) {
+    if (t.push_nseg > 0) {
+        if (t.push_nseg > kMaxSegs || t.push_nflags < 0 || t.push_nflags > 64 || !t.push_counter)
+            return hipErrorInvalidValue;
+        size_t maxb = 0;
+        a.push.n = t.push_nseg;
+        for (int i = 0; i < t.push_nseg; ++i) {
+            a.push.src[i] = t.push_src[i];
+            a.push.dst[i] = t.push_dst[i];
+            a.push.nbytes[i] = t.push_n[i];
+            if (t.push_n[i] > maxb) maxb = t.push_n[i];
+        }
+        a.flags.n = t.push_nflags;
+        a.flags.seq = t.push_seq;
+        for (int i = 0; i < t.push_nflags; ++i) a.flags.dst[i] = t.push_flags[i];
+        size_t gx = (maxb / 16 + 255) / 256;          // as launch_push_post
+        if (gx < 1) gx = 1;
+        if (gx > 16) gx = 16;
+        a.push_gx = (unsigned)gx;
+        a.npush = (unsigned)(gx * (size_t)t.push_nseg);
+        a.push_counter = t.push_counter;
+        a.push_sys = t.push_sys ? 1 : 0;
+    }
+    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.wait_flags && !t.push_nseg) {
         if (t.src[0] == out) return hipSuccess;
         return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
     }

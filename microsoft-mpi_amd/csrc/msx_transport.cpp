@@ -848,6 +848,13 @@ struct TreeWait {
     unsigned long long seq = 0;
     int n = 0, skip = -1;
     int* err = nullptr;                          // device view of a pinned host word
+    // fused push (TreeSpec::push_*): this rank's contribution to the peers and
+    // its arrival flags, done by the first workgroups of the same launch
+    const std::vector<const void*>* push_src = nullptr;
+    const std::vector<void*>* push_dst = nullptr;
+    const std::vector<size_t>* push_n = nullptr;
+    const std::vector<unsigned long long*>* push_flags = nullptr;
+    unsigned* push_counter = nullptr;
 };
 
 int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>& srcs, size_t esz,
@@ -862,6 +869,21 @@ int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>
         spec.wait_n = wait->n;
         spec.wait_skip = wait->skip;
         spec.wait_err = wait->err;
+        if (wait->push_src && !wait->push_src->empty()) {
+            const size_t ns = wait->push_src->size(), nf = wait->push_flags->size();
+            if (ns > 32 || nf > 64) { set_error("fused push: too many peers"); return MPI_ERR_INTERN; }
+            spec.push_nseg = (int)ns;
+            for (size_t i = 0; i < ns; ++i) {
+                spec.push_src[i] = (*wait->push_src)[i];
+                spec.push_dst[i] = (*wait->push_dst)[i];
+                spec.push_n[i] = (*wait->push_n)[i];
+            }
+            spec.push_nflags = (int)nf;
+            for (size_t i = 0; i < nf; ++i) spec.push_flags[i] = (*wait->push_flags)[i];
+            spec.push_seq = wait->seq;
+            spec.push_counter = wait->push_counter;
+            spec.push_sys = sys_fences();
+        }
     }
     if (extra_outs.size() > 31) { set_error("tree combine: too many destinations"); return MPI_ERR_INTERN; }
     spec.nextra = (int)extra_outs.size();
@@ -1105,6 +1127,17 @@ struct Windows {
         return base[(size_t)r] + 2 * C + kFlagBytes + (base.size() + (size_t)t) * rma_slot();
     }
 };
+
+// The barrier-free small allreduce pushes and reduces in one launch
+// (MSX_FUSED_PUSH=0: a separate push launch first).
+bool fused_push()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_FUSED_PUSH");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
 
 // The barrier-free small allreduce synchronises on GPU arrival flags
 // (MSX_RD_FLAGS=0: host barrier instead).
@@ -1580,14 +1613,26 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             int* err_dev = wait_err_word(&err_host);
             if (!err_dev) { set_error("allreduce: arrival word allocation failed"); return MPI_ERR_NO_MEM; }
             *err_host = 0;
+            // Data and flags in one kernel (the flag ordered after the data);
+            // a rank that also evaluates a tree does both in ONE launch: the
+            // push workgroups come first in the tree kernel's grid
+            // (MSX_FUSED_PUSH=0: separate k_push_post launch).
+            // Not when the result overwrites the vector being pushed (in place):
+            // the tree workgroups wait only for the PEERS' flags, so they could
+            // store the result while this rank's push still reads its input.
+            char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
+            const bool disjoint = out + count * esz <= mine || mine + count * esz <= out;
+            const bool fuse = want && fused_push() && !sg.src.empty() && disjoint;
+            unsigned* counter = nullptr;
             if (rc == MPI_SUCCESS && !sg.src.empty()) {
-                // data and flags in one kernel (the flag ordered after the data)
-                unsigned* counter = tp->push_counter();
+                counter = tp->push_counter();
                 if (!counter) { set_error("allreduce: push counter allocation failed"); return MPI_ERR_NO_MEM; }
+            }
+            if (rc == MPI_SUCCESS && !sg.src.empty() && !fuse) {
                 hipError_t e = launch_push_post(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
                                                 fl.data(), (int)fl.size(), seq, sys_fences(), counter, s);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
-            } else if (rc == MPI_SUCCESS && !fl.empty()) {
+            } else if (rc == MPI_SUCCESS && sg.src.empty() && !fl.empty()) {
                 hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);   // nothing to push
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce arrival flags");
             }
@@ -1598,7 +1643,13 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 tw.n = p;
                 tw.skip = me;
                 tw.err = err_dev;
-                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
+                if (fuse) {
+                    tw.push_src = &sg.src;
+                    tw.push_dst = &sg.dst;
+                    tw.push_n = &sg.n;
+                    tw.push_flags = &fl;
+                    tw.push_counter = counter;
+                }
                 rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s, {}, &tw);
                 if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
             }

@@ -364,7 +364,7 @@ def _free_port():
                                                         (4, 1 << 20, None, None), (5, None, None, None),
                                                         (3, 65536, "rccl", None), (8, None, None, None),
                                                         (7, 1 << 20, None, None), (3, None, None, "0"),
-                                                        (4, 65536, None, "0")])
+                                                        (4, 65536, None, "0"), (3, None, None, "unfused")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -380,7 +380,9 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             env["MSX_CHUNK_BYTES"] = str(chunk)     # many chunks, pieces across block edges
         if transport:
             env["MSX_TRANSPORT"] = transport
-        if rd_flags is not None:
+        if rd_flags == "unfused":
+            env["MSX_FUSED_PUSH"] = "0"             # flag path with a separate push launch
+        elif rd_flags is not None:
             env["MSX_RD_FLAGS"] = rd_flags          # host-barrier small allreduce / reduce
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
