@@ -105,17 +105,37 @@ __device__ __forceinline__ int64_t typed_off(const CopyArgs& a, int64_t g)
     }
 }
 
+// Granules per lane in flight: every lane issues kUnroll independent loads
+// before its first store (a lone load -> store chain per lane leaves too few
+// bytes in flight per CU to cover HBM latency).
+constexpr int kUnroll = 4;
+
 template <int G, bool REG, bool NARROW, bool UNPACK>
 __global__ __launch_bounds__(kPackBlock) void k_dt_pack(CopyArgs a)
 {
     typedef typename GranT<G>::T T;
     const int64_t stride = (int64_t)gridDim.x * kPackBlock;
     const int64_t bid = xcd_tile(blockIdx.x, gridDim.x);
-    for (int64_t g = bid * kPackBlock + threadIdx.x; g < a.ngran; g += stride) {
-        T* t = reinterpret_cast<T*>(a.typed + typed_off<G, REG, NARROW>(a, g));
-        T* p = reinterpret_cast<T*>(a.packed) + g;
-        if constexpr (UNPACK) *t = __builtin_nontemporal_load(p);
-        else __builtin_nontemporal_store(*t, p);
+    for (int64_t g0 = bid * kPackBlock + threadIdx.x; g0 < a.ngran; g0 += stride * kUnroll) {
+        T v[kUnroll];
+        int64_t off[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t g = g0 + u * stride;
+            if (g < a.ngran) {
+                off[u] = typed_off<G, REG, NARROW>(a, g);
+                if constexpr (UNPACK) v[u] = __builtin_nontemporal_load(reinterpret_cast<const T*>(a.packed) + g);
+                else v[u] = *reinterpret_cast<const T*>(a.typed + off[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t g = g0 + u * stride;
+            if (g < a.ngran) {
+                if constexpr (UNPACK) *reinterpret_cast<T*>(a.typed + off[u]) = v[u];
+                else __builtin_nontemporal_store(v[u], reinterpret_cast<T*>(a.packed) + g);
+            }
+        }
     }
 }
 
@@ -138,9 +158,24 @@ __global__ __launch_bounds__(kPackBlock) void k_dt_runs(CopyArgs a)
         const int64_t len = (a.poff[k + 1] - po) / G;
         T* t = reinterpret_cast<T*>(a.typed + i * a.extent + a.disp[k]);
         T* p = reinterpret_cast<T*>(a.packed + i * a.size + po);
-        for (int64_t j = lane; j < len; j += 64) {
-            if constexpr (UNPACK) t[j] = __builtin_nontemporal_load(p + j);
-            else __builtin_nontemporal_store(t[j], p + j);
+        for (int64_t j0 = lane; j0 < len; j0 += 64 * kUnroll) {
+            T v[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int64_t j = j0 + 64 * u;
+                if (j < len) {
+                    if constexpr (UNPACK) v[u] = __builtin_nontemporal_load(p + j);
+                    else v[u] = t[j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int64_t j = j0 + 64 * u;
+                if (j < len) {
+                    if constexpr (UNPACK) t[j] = v[u];
+                    else __builtin_nontemporal_store(v[u], p + j);
+                }
+            }
         }
     }
 }
