@@ -460,8 +460,9 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
         // fused push: the first npush workgroups push this rank's vector and
         // post its flags; they never wait, so the peers' trees always progress
         if (b < a.npush) {
-            push_post_body(a.push, a.flags, a.push_counter, a.npush, a.push_sys, b % a.push_gx, a.push_gx,
-                           (int)(b / a.push_gx));
+            // segment b % n: every peer's push starts at once (see k_copy_segs)
+            const unsigned ns = (unsigned)a.push.n;
+            push_post_body(a.push, a.flags, a.push_counter, a.npush, a.push_sys, b / ns, a.push_gx, (int)(b % ns));
             return;
         }
         b -= a.npush;
@@ -504,20 +505,24 @@ __global__ __launch_bounds__(64) void k_post_flags(PostFlags f)
 
 __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
 {
-    // blockIdx.y selects the segment so every source link is busy at once.
-    const int sg = blockIdx.y;
+    // One 1-D grid, workgroup b serving segment b % n: consecutive workgroups
+    // go to different segments, so the dispatcher starts every segment (every
+    // peer link, when the segments are remote) at once instead of filling the
+    // GPU with the first few segments' workgroups.
+    const int sg = (int)(blockIdx.x % (unsigned)c.n);
+    const size_t bx = blockIdx.x / (unsigned)c.n, gx = gridDim.x / (unsigned)c.n;
     if (c.sys) acquire_system();
     const char* src = static_cast<const char*>(c.src[sg]);
     char* dst = static_cast<char*>(c.dst[sg]);
     const size_t nb = c.nbytes[sg];
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    const size_t stride = (size_t)gridDim.x * 256;
+    const size_t stride = gx * 256;
     size_t done = 0;
     if (vec) {
         const size_t nv = nb / 16;
         const u32x4* s = reinterpret_cast<const u32x4*>(src);
         u32x4* d = reinterpret_cast<u32x4*>(dst);
-        size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+        size_t i = bx * 256 + threadIdx.x;
         for (; i + 3 * stride < nv; i += 4 * stride) {
             u32x4 a0 = s[i], a1 = s[i + stride], a2 = s[i + 2 * stride], a3 = s[i + 3 * stride];
             d[i] = a0; d[i + stride] = a1; d[i + 2 * stride] = a2; d[i + 3 * stride] = a3;
@@ -525,7 +530,7 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
         for (; i < nv; i += stride) d[i] = s[i];
         done = nv * 16;
     }
-    for (size_t i = done + (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
+    for (size_t i = done + bx * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
     if (c.sys) release_system();
 }
 
@@ -1016,7 +1021,7 @@ hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size
         size_t gx = (maxb / 16 + 1023) / 1024;
         if (gx < 1) gx = 1;
         if (gx > 512) gx = 512;
-        hipLaunchKernelGGL(k_copy_segs, dim3((unsigned)gx, (unsigned)c.n), dim3(256), 0, s, c);
+        hipLaunchKernelGGL(k_copy_segs, dim3((unsigned)(gx * (size_t)c.n)), dim3(256), 0, s, c);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
