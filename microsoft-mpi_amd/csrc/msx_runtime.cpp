@@ -18,6 +18,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <time.h>
 #include <unistd.h>
 #include <utility>
@@ -41,6 +42,9 @@ struct DevState {
     void* stage_io[2] = {nullptr, nullptr};
     hipStream_t stage_s[2] = {nullptr, nullptr};
     size_t stage_cap = 0;
+    // small host operands (reduce_local_any)
+    std::mutex bounce_mu;
+    Bounce bounce_in, bounce_io;
 };
 
 DevState& ds()
@@ -309,6 +313,40 @@ bool alias_host_operands(PinHold& hold, bool pin_pageable, const void* a, size_t
     return (!ia || ia->place == Place::Device) && (!ib || ib->place == Place::Device);
 }
 
+bool Bounce::get(size_t bytes)
+{
+    if (bytes <= cap && host) return true;
+    if (host) (void)hipHostFree(host);
+    host = dev = nullptr;
+    cap = 0;
+    size_t want = std::max(bytes, (size_t)64 << 10);
+    void* h = nullptr;
+    if (hipHostMalloc(&h, want, hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        return false;
+    }
+    host = static_cast<char*>(h);
+    dev = static_cast<char*>(d);
+    cap = want;
+    return true;
+}
+
+size_t bounce_max_bytes()
+{
+    static const size_t v = [] {
+        size_t m = (size_t)256 << 10;
+        if (const char* e = getenv("MSX_HOST_BOUNCE_MAX")) m = (size_t)atoll(e);
+        return m;
+    }();
+    return v;
+}
+
 BufInfo classify(const void* p)
 {
     BufInfo b;
@@ -408,6 +446,29 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "combine kernel");
     }
     if (mode == 0 && bytes_all >= pin_min_bytes()) trace("reduce_local: call pin refused, staging %zu bytes", bytes_all);
+
+    // Host mode 0, small host operands: the CPU copies them into pinned bounce
+    // buffers that the kernel reads and writes over PCIe -- one launch and one
+    // sync instead of three synchronous pageable copies.  Another thread
+    // holding the bounce buffers sends this call down the staged path.
+    if (mode == 0 && bytes_all <= bounce_max_bytes()) {
+        std::unique_lock<std::mutex> bg(s.bounce_mu, std::try_to_lock);
+        const bool need_in = bi.place != Place::Device, need_io = bo.place != Place::Device;
+        if (bg.owns_lock() && (!need_in || s.bounce_in.get(bytes_all)) && (!need_io || s.bounce_io.get(bytes_all))) {
+            const void* din = bi.dev;
+            void* dio = bo.dev;
+            if (need_in) { memcpy(s.bounce_in.host, in, bytes_all); din = s.bounce_in.dev; }
+            if (need_io) { memcpy(s.bounce_io.host, inout, bytes_all); dio = s.bounce_io.dev; }
+            LaunchCfg cfg = g_cfg;
+            cfg.host = true;
+            hipError_t e = launch_combine(opidx, k, din, dio, count, s.stream, cfg);
+            if (e != hipSuccess) return hip_fail(e, "combine kernel launch");
+            e = hipStreamSynchronize(s.stream);
+            if (e != hipSuccess) return hip_fail(e, "combine kernel");
+            if (need_io) memcpy(inout, s.bounce_io.host, bytes_all);
+            return MPI_SUCCESS;
+        }
+    }
 
     // At least one operand in host memory: chunked, double-buffered staging.
     std::lock_guard<std::mutex> g(s.stage_mu);

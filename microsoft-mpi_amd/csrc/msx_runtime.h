@@ -56,6 +56,20 @@ private:
     friend bool alias_host_operands(PinHold&, bool, const void*, size_t, BufInfo*, const void*, size_t, BufInfo*);
 };
 
+// A pinned host buffer the kernels read and write over PCIe, for small host
+// operands: the CPU copies the user's bytes in and out around one launch,
+// instead of synchronous pageable DMA copies.  Grows, never shrinks; not
+// thread-safe (one owner at a time).
+struct Bounce {
+    char* host = nullptr;
+    char* dev = nullptr;     // device alias of `host`
+    size_t cap = 0;
+    bool get(size_t bytes);  // false: allocation failed (use another path)
+};
+// Host operands up to this many bytes go through a bounce buffer
+// (MSX_HOST_BOUNCE_MAX, default 256 KiB; 0 disables it).
+size_t bounce_max_bytes();
+
 // Operands a (na bytes) and b (nb bytes; b may be a, or null): pinned host
 // memory is used through its mapped alias; with pin_pageable, pageable memory
 // of at least MSX_HOST_PIN_MIN bytes (default 1 MiB) is pinned for the hold's

@@ -1128,6 +1128,14 @@ struct Windows {
     }
 };
 
+// Pinned bounce buffers of the engine (engine worker, or the one inline
+// blocking call): 0 = this rank's contribution, 1 = the result.
+Bounce& engine_bounce(int i)
+{
+    static Bounce b[2];
+    return b[i];
+}
+
 // The barrier-free small allreduce pushes and reduces in one launch
 // (MSX_FUSED_PUSH=0: a separate push launch first).
 bool fused_push()
@@ -1597,8 +1605,21 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             // posted that it finished call s-2 -- normally long since true.
             const size_t half = (size_t)tp->rd_parity * Qh;
             for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
+            // small host buffers go through the engine's pinned bounce buffers
+            // (CPU copies in and out, the kernels read / write them over PCIe)
+            // instead of synchronous pageable copies through HBM staging
+            const size_t nbytes = count * esz;
+            const bool bounce_src = bs.place != Place::Device && nbytes <= bounce_max_bytes() &&
+                                    engine_bounce(0).get(nbytes);
+            const bool bounce_dst = want && bd.place != Place::Device && nbytes <= bounce_max_bytes() &&
+                                    engine_bounce(1).get(nbytes);
             const char* mine = nullptr;
-            rc = device_view(bs, src, 0, count * esz, stage, s, &mine);
+            if (bounce_src) {
+                memcpy(engine_bounce(0).host, src, nbytes);
+                mine = engine_bounce(0).dev;
+            } else {
+                rc = device_view(bs, src, 0, nbytes, stage, s, &mine);
+            }
             const unsigned long long seq = ++tp->rd_seq;
             Segs sg;
             std::vector<unsigned long long*> fl;
@@ -1620,7 +1641,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             // Not when the result overwrites the vector being pushed (in place):
             // the tree workgroups wait only for the PEERS' flags, so they could
             // store the result while this rank's push still reads its input.
-            char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
+            char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev)
+                                                  : (bounce_dst ? engine_bounce(1).dev : w.out(me));
             const bool disjoint = out + count * esz <= mine || mine + count * esz <= out;
             const bool fuse = want && fused_push() && !sg.src.empty() && disjoint;
             unsigned* counter = nullptr;
@@ -1655,6 +1677,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             }
             const int rs = sync_stream(s, "allreduce tree");
             if (rc == MPI_SUCCESS) rc = rs;
+            if (rc == MPI_SUCCESS && bounce_dst) memcpy(dst, engine_bounce(1).host, nbytes);
             if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
                 set_error("allreduce: a peer's contribution did not arrive within 20 s");
                 rc = MPI_ERR_OTHER;

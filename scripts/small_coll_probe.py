@@ -45,6 +45,40 @@ for nbytes in (8, 4096, 65536):
             L.MPI_Reduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, 0, C.MPI_COMM_WORLD)
         ts.append((time.perf_counter() - t0) / 200)
     out[f"reduce_{nbytes}B_us"] = round(sorted(ts)[2] * 1e6, 2)
+# host (pageable) buffers: the common case of a CPU application
+import numpy as np  # noqa: E402
+for nbytes in (8, 4096, 65536):
+    m = max(1, nbytes // 4)
+    ha = np.ones(m, np.float32)
+    hb = np.zeros(m, np.float32)
+    for _ in range(20):
+        L.MPI_Allreduce(ha.ctypes.data, hb.ctypes.data, m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+    ts = []
+    for _ in range(5):
+        L.MPI_Barrier(C.MPI_COMM_WORLD)
+        t0 = time.perf_counter()
+        for _ in range(200):
+            L.MPI_Allreduce(ha.ctypes.data, hb.ctypes.data, m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+        ts.append((time.perf_counter() - t0) / 200)
+    out[f"host_allreduce_{nbytes}B_us"] = [round(sorted(ts)[2] * 1e6, 2), bool((hb == p).all())]
+    hc = np.ones(m, np.float32)
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        for _ in range(200):
+            L.MPI_Reduce_local(ha.ctypes.data, hc.ctypes.data, m, C.MPI_FLOAT, C.MPI_SUM)
+        ts.append((time.perf_counter() - t0) / 200)
+    out[f"host_reduce_local_{nbytes}B_us"] = round(sorted(ts)[2] * 1e6, 2)
+    da = torch.ones(m, device="cuda")
+    db = torch.ones(m, device="cuda")
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        for _ in range(200):
+            L.MPI_Reduce_local(da.data_ptr(), db.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM)
+        ts.append((time.perf_counter() - t0) / 200)
+    out[f"device_reduce_local_{nbytes}B_us"] = round(sorted(ts)[2] * 1e6, 2)
 if rank == 0:
     print(json.dumps(out), flush=True)
 L.MPI_Finalize()

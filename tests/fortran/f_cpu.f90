@@ -23,6 +23,7 @@ program fcpu
   integer(kind=MPI_ADDRESS_KIND) lb, ext, a1, a3, addrs(4)
   integer(kind=MPI_COUNT_KIND) szx
   integer a(10), b(10), c(10)
+  integer reqs(3), idx, nout, idxs(3), st(MPI_STATUS_SIZE)
   logical flag, comm
   double precision t
   character(len=600) msg
@@ -114,6 +115,34 @@ program fcpu
   ! count 0 succeeds before op validation
   call MPI_REDUCE_LOCAL(a, b, 0, MPI_DOUBLE_PRECISION, MPI_BAND, ierr)
   print '(A,I0)', 'COUNT0 ', ierr
+
+  ! request completion (mpif.cpp:186-263): one-rank nonblocking calls complete
+  ! at the call; indices come back 1-based, MPI_UNDEFINED stays as is
+  call MPI_IALLREDUCE(a, c, 10, MPI_INTEGER, MPI_SUM, MPI_COMM_WORLD, reqs(1), ierr)
+  reqs(2) = MPI_REQUEST_NULL
+  call MPI_IALLREDUCE(a, c, 10, MPI_INTEGER, MPI_SUM, MPI_COMM_WORLD, reqs(3), ierr)
+  call MPI_WAITANY(3, reqs, idx, st, ierr)
+  print '(A,I0,1X,I0)', 'WAITANY ', ierr, idx
+  call MPI_TESTANY(3, reqs, idx, flag, st, ierr)
+  print '(A,I0,1X,I0,1X,L1)', 'TESTANY ', ierr, idx, flag
+  call MPI_TESTANY(3, reqs, idx, flag, st, ierr)
+  print '(A,I0,1X,L1)', 'TESTANY_NONE ', idx, flag
+  call MPI_IALLREDUCE(a, c, 10, MPI_INTEGER, MPI_SUM, MPI_COMM_WORLD, reqs(2), ierr)
+  call MPI_TESTALL(3, reqs, flag, MPI_STATUSES_IGNORE, ierr)
+  print '(A,I0,1X,L1,1X,L1)', 'TESTALL ', ierr, flag, reqs(2) == MPI_REQUEST_NULL
+  call MPI_IALLREDUCE(a, c, 10, MPI_INTEGER, MPI_SUM, MPI_COMM_WORLD, reqs(3), ierr)
+  call MPI_WAITSOME(3, reqs, nout, idxs, MPI_STATUSES_IGNORE, ierr)
+  print '(A,I0,1X,I0,1X,I0)', 'WAITSOME ', ierr, nout, idxs(1)
+  call MPI_IALLREDUCE(a, c, 10, MPI_INTEGER, MPI_SUM, MPI_COMM_WORLD, reqs(1), ierr)
+  call MPI_REQUEST_GET_STATUS(reqs(1), flag, st, ierr)
+  print '(A,I0,1X,L1,1X,L1)', 'GET_STATUS ', ierr, flag, reqs(1) /= MPI_REQUEST_NULL
+  call MPI_REQUEST_FREE(reqs(1), ierr)
+  call MPI_ERROR_CLASS(ierr, cls, i)
+  print '(A,I0)', 'REQUEST_FREE_CLASS ', cls
+  call MPI_TESTSOME(3, reqs, nout, idxs, MPI_STATUSES_IGNORE, ierr)
+  print '(A,I0,1X,I0,1X,I0)', 'TESTSOME ', ierr, nout, idxs(1)
+  call MPI_TESTSOME(3, reqs, nout, idxs, MPI_STATUSES_IGNORE, ierr)
+  print '(A,I0)', 'TESTSOME_NONE ', nout
 
   msg = 'x'
   call MPI_ERROR_STRING(MPI_ERR_OP, msg, rlen, ierr)

@@ -141,6 +141,15 @@ def test_fortran_program_without_gpu():
     assert as_int("IN_PLACE_CLASS") == [C.MPI_ERR_BUFFER]
     assert as_int("BAND_DOUBLE_CLASS") == [C.MPI_ERR_OP]
     assert as_int("COUNT0") == [0]
+    assert as_int("WAITANY") == [0, 1]
+    assert out["TESTANY"] == ["0", "3", "T"]
+    assert out["TESTANY_NONE"] == [str(-32766), "T"]
+    assert out["TESTALL"] == ["0", "T", "T"]
+    assert as_int("WAITSOME") == [0, 1, 3]
+    assert out["GET_STATUS"] == ["0", "T", "T"]
+    assert as_int("REQUEST_FREE_CLASS") == [C.MPI_ERR_OTHER]
+    assert as_int("TESTSOME") == [0, 1, 1]
+    assert as_int("TESTSOME_NONE") == [-32766]
     assert out["ERROR_STRING"] == ["0", "T", "T"]
     assert as_int("PACK_SIZE") == [12]
     assert out["WTIME"] == ["T"]
