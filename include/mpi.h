@@ -149,6 +149,15 @@ typedef int MPI_Comm;
 #define MPI_COMM_WORLD ((MPI_Comm)0x44000000)
 #define MPI_COMM_SELF  ((MPI_Comm)0x44000001)
 
+/* ---- MPI_Group (mpi.h:450-452, 2957-2960) -------------------------------- */
+typedef int MPI_Group;
+#define MPI_GROUP_NULL  ((MPI_Group)0x08000000)
+#define MPI_GROUP_EMPTY ((MPI_Group)0x48000000)
+#define MPI_IDENT       0
+#define MPI_CONGRUENT   1
+#define MPI_SIMILAR     2
+#define MPI_UNEQUAL     3
+
 /* ---- MPI_Op (mpi.h:410-426) --------------------------------------------- */
 typedef int MPI_Op;
 #define MPI_OP_NULL ((MPI_Op)0x18000000)
@@ -319,6 +328,13 @@ MPI_METHOD MPI_Win_flush_all(MPI_Win win);
 MPI_METHOD MPI_Win_flush_local(int rank, MPI_Win win);
 MPI_METHOD MPI_Win_flush_local_all(MPI_Win win);
 MPI_METHOD MPI_Win_sync(MPI_Win win);
+/* post-start-complete-wait synchronisation (api/mpi_win.cpp:28,979,1331,1487,1566,1769) */
+MPI_METHOD MPI_Win_post(MPI_Group group, int assert, MPI_Win win);
+MPI_METHOD MPI_Win_start(MPI_Group group, int assert, MPI_Win win);
+MPI_METHOD MPI_Win_complete(MPI_Win win);
+MPI_METHOD MPI_Win_wait(MPI_Win win);
+MPI_METHOD MPI_Win_test(MPI_Win win, int* flag);
+MPI_METHOD MPI_Win_get_group(MPI_Win win, MPI_Group* group);
 MPI_METHOD MPI_Win_set_errhandler(MPI_Win win, MPI_Errhandler errhandler);
 MPI_METHOD MPI_Win_get_errhandler(MPI_Win win, MPI_Errhandler* errhandler);
 MPI_METHOD MPI_Put(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
@@ -340,6 +356,22 @@ MPI_METHOD MPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Data
 MPI_METHOD MPI_Compare_and_swap(const void* origin_addr, const void* compare_addr,
                                 void* result_addr, MPI_Datatype datatype, int target_rank,
                                 MPI_Aint target_disp, MPI_Win win);
+
+/* ---- groups (api/mpi_group.cpp, api/mpi_comm.cpp:677) -------------------- */
+MPI_METHOD MPI_Comm_group(MPI_Comm comm, MPI_Group* group);
+MPI_METHOD MPI_Group_size(MPI_Group group, int* size);
+MPI_METHOD MPI_Group_rank(MPI_Group group, int* rank);
+MPI_METHOD MPI_Group_free(MPI_Group* group);
+MPI_METHOD MPI_Group_incl(MPI_Group group, int n, const int ranks[], MPI_Group* newgroup);
+MPI_METHOD MPI_Group_excl(MPI_Group group, int n, const int ranks[], MPI_Group* newgroup);
+MPI_METHOD MPI_Group_range_incl(MPI_Group group, int n, int ranges[][3], MPI_Group* newgroup);
+MPI_METHOD MPI_Group_range_excl(MPI_Group group, int n, int ranges[][3], MPI_Group* newgroup);
+MPI_METHOD MPI_Group_union(MPI_Group group1, MPI_Group group2, MPI_Group* newgroup);
+MPI_METHOD MPI_Group_intersection(MPI_Group group1, MPI_Group group2, MPI_Group* newgroup);
+MPI_METHOD MPI_Group_difference(MPI_Group group1, MPI_Group group2, MPI_Group* newgroup);
+MPI_METHOD MPI_Group_translate_ranks(MPI_Group group1, int n, const int ranks1[], MPI_Group group2,
+                                     int ranks2[]);
+MPI_METHOD MPI_Group_compare(MPI_Group group1, MPI_Group group2, int* result);
 
 /* ---- derived datatypes (mpi.h:1340-1822) and pack/unpack (mpi.h:1823-1887)
  * Constructors, queries and MPI_Pack/MPI_Unpack; the bytes are moved by the
@@ -498,6 +530,26 @@ MPI_METHOD PMPI_Get_accumulate(const void* origin_addr, int origin_count,
                                MPI_Datatype target_datatype, MPI_Op op, MPI_Win win);
 MPI_METHOD PMPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Datatype datatype,
                              int target_rank, MPI_Aint target_disp, MPI_Op op, MPI_Win win);
+MPI_METHOD PMPI_Comm_group(MPI_Comm comm, MPI_Group* group);
+MPI_METHOD PMPI_Group_size(MPI_Group group, int* size);
+MPI_METHOD PMPI_Group_rank(MPI_Group group, int* rank);
+MPI_METHOD PMPI_Group_free(MPI_Group* group);
+MPI_METHOD PMPI_Group_incl(MPI_Group group, int n, const int ranks[], MPI_Group* newgroup);
+MPI_METHOD PMPI_Group_excl(MPI_Group group, int n, const int ranks[], MPI_Group* newgroup);
+MPI_METHOD PMPI_Group_range_incl(MPI_Group group, int n, int ranges[][3], MPI_Group* newgroup);
+MPI_METHOD PMPI_Group_range_excl(MPI_Group group, int n, int ranges[][3], MPI_Group* newgroup);
+MPI_METHOD PMPI_Group_union(MPI_Group group1, MPI_Group group2, MPI_Group* newgroup);
+MPI_METHOD PMPI_Group_intersection(MPI_Group group1, MPI_Group group2, MPI_Group* newgroup);
+MPI_METHOD PMPI_Group_difference(MPI_Group group1, MPI_Group group2, MPI_Group* newgroup);
+MPI_METHOD PMPI_Group_translate_ranks(MPI_Group group1, int n, const int ranks1[], MPI_Group group2,
+                                      int ranks2[]);
+MPI_METHOD PMPI_Group_compare(MPI_Group group1, MPI_Group group2, int* result);
+MPI_METHOD PMPI_Win_post(MPI_Group group, int assert, MPI_Win win);
+MPI_METHOD PMPI_Win_start(MPI_Group group, int assert, MPI_Win win);
+MPI_METHOD PMPI_Win_complete(MPI_Win win);
+MPI_METHOD PMPI_Win_wait(MPI_Win win);
+MPI_METHOD PMPI_Win_test(MPI_Win win, int* flag);
+MPI_METHOD PMPI_Win_get_group(MPI_Win win, MPI_Group* group);
 MPI_METHOD PMPI_Testall(int count, MPI_Request array_of_requests[], int* flag,
                         MPI_Status array_of_statuses[]);
 MPI_METHOD PMPI_Testany(int count, MPI_Request array_of_requests[], int* index, int* flag,

@@ -1040,6 +1040,12 @@ MSX_EXPORT int MPI_Request_get_status(MPI_Request request, int* flag, MPI_Status
 #define MSX_ALIAS(name) extern "C" __attribute__((visibility("default"), alias(#name)))
 MSX_ALIAS(MPI_Reduce_local) int PMPI_Reduce_local(const void*, void*, int, MPI_Datatype, MPI_Op);
 MSX_ALIAS(MPI_Testall) int PMPI_Testall(int, MPI_Request[], int*, MPI_Status[]);
+MSX_ALIAS(MPI_Win_post) int PMPI_Win_post(MPI_Group, int, MPI_Win);
+MSX_ALIAS(MPI_Win_start) int PMPI_Win_start(MPI_Group, int, MPI_Win);
+MSX_ALIAS(MPI_Win_complete) int PMPI_Win_complete(MPI_Win);
+MSX_ALIAS(MPI_Win_wait) int PMPI_Win_wait(MPI_Win);
+MSX_ALIAS(MPI_Win_test) int PMPI_Win_test(MPI_Win, int*);
+MSX_ALIAS(MPI_Win_get_group) int PMPI_Win_get_group(MPI_Win, MPI_Group*);
 MSX_ALIAS(MPI_Testany) int PMPI_Testany(int, MPI_Request[], int*, int*, MPI_Status*);
 MSX_ALIAS(MPI_Testsome) int PMPI_Testsome(int, MPI_Request[], int*, int[], MPI_Status[]);
 MSX_ALIAS(MPI_Waitany) int PMPI_Waitany(int, MPI_Request[], int*, MPI_Status*);
@@ -1378,6 +1384,10 @@ MSX_EXPORT int MPI_Win_free(MPI_Win* win)
     if (!w->q.empty()) { set_error("MPI_Win_free with operations pending (no closing fence)"); return err_win(w, "MPI_Win_free", MPI_ERR_RMA_SYNC); }
     for (int m : w->lock_mode)
         if (m) { set_error("MPI_Win_free inside a passive-target epoch"); return err_win(w, "MPI_Win_free", MPI_ERR_RMA_SYNC); }
+    if (w->access_epoch || w->exposure_epoch) {
+        set_error("MPI_Win_free inside a post-start-complete-wait epoch");
+        return err_win(w, "MPI_Win_free", MPI_ERR_RMA_SYNC);
+    }
     rc = coll_barrier(w->comm);       // every rank is done with the window
     if (rc != MPI_SUCCESS) return err_win(w, "MPI_Win_free", rc);
     engine_rma_free(w);               // no request can be in flight after the barrier
@@ -1469,6 +1479,150 @@ MSX_EXPORT int MPI_Win_unlock(int rank, MPI_Win win)
     rc = v_lock_rank(w, rank);
     if (rc == MPI_SUCCESS) rc = win_unlock(w, rank);
     return err_win(w, "MPI_Win_unlock", rc);
+}
+
+// ---- post-start-complete-wait (api/mpi_win.cpp:28-70,979-1030,1331-1381,
+// 1487-1537,1566-1613,1769-1808; mpid/win.cpp:2001-2012,3689-4088) -------------
+namespace {
+// The window ranks of a group's members (MpiaGroupValidateHandle, then
+// MPIR_Group_translate_ranks into the window's communicator).  A member outside
+// the window's communicator is an invalid group here (the reference would
+// address rank MPI_UNDEFINED).
+int group_window_ranks(RmaWin* w, MPI_Group g, std::vector<int>* ranks)
+{
+    std::vector<int> lp;
+    int rc = group_members(g, &lp);
+    if (rc != MPI_SUCCESS) return rc;
+    ranks->clear();
+    for (int id : lp) {
+        const auto& cl = w->comm->lpid;
+        const auto it = std::find(cl.begin(), cl.end(), id);
+        if (it == cl.end()) {
+            set_error("group member (process %d) is not in the window's communicator", id);
+            return MPI_ERR_GROUP;
+        }
+        ranks->push_back((int)(it - cl.begin()));
+    }
+    return MPI_SUCCESS;
+}
+void pscw_sizes(RmaWin* w)
+{
+    const size_t p = (size_t)w->comm->size;
+    if (w->starts.size() != p) w->starts.assign(p, 0);
+    if (w->posts.size() != p) w->posts.assign(p, 0);
+}
+}  // namespace
+
+// Exposure epoch: every origin of `group` may access this window until MPI_Win_wait
+MSX_EXPORT int MPI_Win_post(MPI_Group group, int assert_, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_post");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_post", rc);
+    std::vector<int> origins;
+    rc = group_window_ranks(w, group, &origins);
+    if (rc == MPI_SUCCESS && w->exposure_epoch) {
+        set_error("MPI_Win_post inside an exposure epoch (**rmasync)");
+        rc = MPI_ERR_RMA_SYNC;
+    }
+    (void)assert_;                    // MPI_MODE_NOCHECK / NOSTORE / NOPUT: hints here
+    if (rc == MPI_SUCCESS) {
+        pscw_sizes(w);
+        w->exposure_origins = origins;
+        w->exposure_epoch = true;
+        rc = engine_rma_post(w);
+    }
+    return err_win(w, "MPI_Win_post", rc);
+}
+
+// Access epoch: operations to `group`'s members are queued until
+// MPI_Win_complete, which waits for their posts (MPID_Win_start only records
+// the group, win.cpp:3775-3801)
+MSX_EXPORT int MPI_Win_start(MPI_Group group, int assert_, MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_start");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_start", rc);
+    std::vector<int> targets;
+    rc = group_window_ranks(w, group, &targets);
+    if (rc == MPI_SUCCESS && w->access_epoch) {
+        set_error("MPI_Win_start inside an access epoch (**rmasync)");
+        rc = MPI_ERR_RMA_SYNC;
+    }
+    if (rc == MPI_SUCCESS) {
+        pscw_sizes(w);
+        w->access_targets = targets;
+        w->access_assert = assert_;
+        w->access_epoch = true;
+    }
+    return err_win(w, "MPI_Win_start", rc);
+}
+
+// Every operation of the access epoch is applied at its target before the
+// target's MPI_Win_wait can return.  Without a matching MPI_Win_start the
+// reference dereferences a null group; here it is MPI_ERR_RMA_SYNC.
+MSX_EXPORT int MPI_Win_complete(MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_complete");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_complete", rc);
+    if (!w->access_epoch) {
+        set_error("MPI_Win_complete without MPI_Win_start (**rmasync)");
+        return err_win(w, "MPI_Win_complete", MPI_ERR_RMA_SYNC);
+    }
+    rc = engine_rma_complete(w);
+    w->access_epoch = false;
+    w->access_targets.clear();
+    return err_win(w, "MPI_Win_complete", rc);
+}
+
+// MPID_Win_wait (win.cpp:4077-4088): returns once every origin of the posted
+// group completed; with no exposure epoch open there is nothing to wait for
+MSX_EXPORT int MPI_Win_wait(MPI_Win win)
+{
+    MSX_REQUIRE_INIT("MPI_Win_wait");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_wait", rc);
+    if (!w->exposure_epoch) return MPI_SUCCESS;
+    int flag = 0;
+    rc = engine_rma_wait(w, true, &flag);
+    if (rc == MPI_SUCCESS) {
+        w->exposure_epoch = false;
+        w->exposure_origins.clear();
+    }
+    return err_win(w, "MPI_Win_wait", rc);
+}
+
+// MPID_Win_test (win.cpp:2001-2012): the non-blocking MPI_Win_wait
+MSX_EXPORT int MPI_Win_test(MPI_Win win, int* flag)
+{
+    MSX_REQUIRE_INIT("MPI_Win_test");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_test", rc);
+    if (!flag) { set_error("null flag"); return err_win(w, "MPI_Win_test", MPI_ERR_ARG); }
+    if (!w->exposure_epoch) { *flag = 1; return MPI_SUCCESS; }
+    rc = engine_rma_wait(w, false, flag);
+    if (rc == MPI_SUCCESS && *flag) {
+        w->exposure_epoch = false;
+        w->exposure_origins.clear();
+    }
+    return err_win(w, "MPI_Win_test", rc);
+}
+
+// api/mpi_win.cpp:979-1030: the group of the window's communicator
+MSX_EXPORT int MPI_Win_get_group(MPI_Win win, MPI_Group* group)
+{
+    MSX_REQUIRE_INIT("MPI_Win_get_group");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Win_get_group", rc);
+    if (!group) { set_error("null group"); return err_win(w, "MPI_Win_get_group", MPI_ERR_ARG); }
+    return err_win(w, "MPI_Win_get_group", group_create(w->comm->lpid, group));
 }
 
 // MPID_Win_lock_all: a shared lock on every rank (mpid/win.cpp:4133-4150)

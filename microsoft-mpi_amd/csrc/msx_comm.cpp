@@ -99,6 +99,9 @@ int world_init()
     (void)ensure_device();
     g_world.rank = rank;
     g_world.size = size;
+    g_world.lpid.resize((size_t)size);
+    for (int r = 0; r < size; ++r) g_world.lpid[(size_t)r] = r;
+    g_self.lpid.assign(1, rank);
     if (size > 1) {
         int rc = transport_create(rank, size, &g_world.tp);
         if (rc != MPI_SUCCESS) return rc;

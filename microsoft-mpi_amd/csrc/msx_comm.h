@@ -19,12 +19,21 @@ struct Comm {
     int size = 1;
     MPI_Errhandler errhandler = MPI_ERRORS_ARE_FATAL;
     Transport* tp = nullptr;   // null when size == 1
+    // process id (MPI_COMM_WORLD rank) of every member, by rank in this
+    // communicator: the lrank_to_lpid map of the comm's group (mpid/group.cpp)
+    std::vector<int> lpid;
 };
 
 // MPI_COMM_WORLD, MPI_COMM_SELF or a derived communicator; nullptr otherwise.
 Comm* lookup_comm(MPI_Comm c);
 MPI_Comm comm_register(Comm* c);      // assigns c->handle
 void comm_unregister(Comm* c);
+
+// Groups (msx_group.cpp): ordered lists of process ids.  MpiaGroupValidateHandle:
+// MPI_SUCCESS and *lpid = the members, or MPI_ERR_GROUP.
+int group_members(MPI_Group g, std::vector<int>* lpid);
+// A new group handle for the members (MPI_GROUP_EMPTY when empty).
+int group_create(const std::vector<int>& lpid, MPI_Group* out);
 
 // Resolved op (builtin kernel or user function), MPID_Op (include/op.h:82-134).
 struct OpRef {

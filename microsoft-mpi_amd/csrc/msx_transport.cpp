@@ -477,7 +477,8 @@ static int listen_ephemeral(int* port)
     return fd;
 }
 
-int transport_split(Transport* parent, int color, int key, int* new_rank, int* new_size, Transport** out)
+int transport_split(Transport* parent, int color, int key, int* new_rank, int* new_size, Transport** out,
+                    std::vector<int>* members_out)
 {
     *out = nullptr;
     *new_rank = -1;
@@ -497,6 +498,10 @@ int transport_split(Transport* parent, int color, int key, int* new_rank, int* n
     for (size_t i = 0; i < members.size(); ++i)
         if (members[i].second == parent->rank) *new_rank = (int)i;
     *new_size = (int)members.size();
+    if (members_out) {
+        members_out->clear();
+        for (auto& m : members) members_out->push_back(m.second);
+    }
     // the new rank 0 of every group of >= 2 opens the group's hub
     int32_t port = 0;
     int lfd = -1;
@@ -2510,6 +2515,8 @@ struct PassiveState {
     std::atomic<uint32_t>* door = nullptr;    // per target: doorbell of its service thread
     std::atomic<int32_t>* lock = nullptr;     // per target: 0 free, > 0 readers, -1 writer
     PassiveSlot* slots = nullptr;             // [target * p + origin]
+    std::atomic<uint32_t>* post = nullptr;    // [target * p + origin]: exposure epochs posted
+    std::atomic<uint32_t>* cmpl = nullptr;    // [target * p + origin]: access epochs completed
     std::thread th;
     std::atomic<bool> stop{false};
     std::mutex apply_mu;                      // service thread vs. self-target applies
@@ -2727,7 +2734,8 @@ int passive_init(RmaWin* w)
     int rc = get_windows(c->tp, &ps->win);
     const size_t p = (size_t)ps->p;
     const size_t hdr = ((p * sizeof(std::atomic<uint32_t>) + p * sizeof(std::atomic<int32_t>)) + 63) & ~(size_t)63;
-    ps->shm_bytes = hdr + p * p * sizeof(PassiveSlot);
+    const size_t pscw = (2 * p * p * sizeof(std::atomic<uint32_t>) + 63) & ~(size_t)63;
+    ps->shm_bytes = hdr + p * p * sizeof(PassiveSlot) + pscw;
     if (rc == MPI_SUCCESS) rc = shm_collective(c->tp, ps->shm_bytes, &ps->shm);
     if (rc == MPI_SUCCESS && hipStreamCreateWithFlags(&ps->os, hipStreamNonBlocking) != hipSuccess) {
         set_error("passive target: stream creation failed");
@@ -2742,6 +2750,8 @@ int passive_init(RmaWin* w)
     ps->door = reinterpret_cast<std::atomic<uint32_t>*>(base);
     ps->lock = reinterpret_cast<std::atomic<int32_t>*>(base + p * sizeof(std::atomic<uint32_t>));
     ps->slots = reinterpret_cast<PassiveSlot*>(base + hdr);
+    ps->post = reinterpret_cast<std::atomic<uint32_t>*>(base + hdr + p * p * sizeof(PassiveSlot));
+    ps->cmpl = ps->post + p * p;
     ps->th = std::thread(passive_serve, ps);
     w->passive = ps;
     return MPI_SUCCESS;
@@ -2813,6 +2823,78 @@ int engine_rma_flush(RmaWin* w, int target)
     w->ql.swap(keep_l);
     if (w->q.empty()) w->blob.clear();
     return rc;
+}
+
+namespace {
+// Block until *word >= want (shared memory, another process bumps it).
+int wait_counter(std::atomic<uint32_t>* word, uint32_t want, const char* what, int peer)
+{
+    const double t_end = now_s() + 600.0;
+    for (int spin = 0;; ++spin) {
+        const uint32_t v = word->load(std::memory_order_acquire);
+        if ((int32_t)(v - want) >= 0) return MPI_SUCCESS;
+        if (now_s() > t_end) {
+            set_error("%s: rank %d did not synchronise within 600 s", what, peer);
+            return MPI_ERR_OTHER;
+        }
+        if (spin < 2000) sched_yield();
+        else futex_wait_ms(word, v, 10);
+    }
+}
+}  // namespace
+
+int engine_rma_post(RmaWin* w)
+{
+    PassiveState* ps = w->passive;
+    for (int o : w->exposure_origins) {
+        w->posts[(size_t)o] += 1;
+        if (!ps) continue;                         // one rank: nothing to tell
+        std::atomic<uint32_t>& word = ps->post[(size_t)ps->me * ps->p + o];
+        word.fetch_add(1, std::memory_order_acq_rel);
+        futex_wake_all(&word);
+    }
+    return MPI_SUCCESS;
+}
+
+int engine_rma_complete(RmaWin* w)
+{
+    PassiveState* ps = w->passive;
+    int rc = MPI_SUCCESS;
+    for (int t : w->access_targets) {
+        w->starts[(size_t)t] += 1;
+        if (!ps) continue;                         // one rank: every operation was applied at its call
+        // MPID_Win_complete (win.cpp:3859-3874): the target's post first
+        if (t != ps->me && !(w->access_assert & MPI_MODE_NOCHECK)) {
+            const int r2 = wait_counter(&ps->post[(size_t)t * ps->p + ps->me], w->starts[(size_t)t],
+                                        "MPI_Win_complete", t);
+            if (rc == MPI_SUCCESS) rc = r2;
+            if (r2 != MPI_SUCCESS) continue;
+        }
+        const int r3 = engine_rma_flush(w, t);     // applied at the target before it is counted
+        if (rc == MPI_SUCCESS) rc = r3;
+        std::atomic<uint32_t>& word = ps->cmpl[(size_t)t * ps->p + ps->me];
+        word.fetch_add(1, std::memory_order_acq_rel);
+        futex_wake_all(&word);
+    }
+    return rc;
+}
+
+int engine_rma_wait(RmaWin* w, bool block, int* flag)
+{
+    PassiveState* ps = w->passive;
+    *flag = 1;
+    if (!ps) return MPI_SUCCESS;
+    for (int o : w->exposure_origins) {
+        std::atomic<uint32_t>* word = &ps->cmpl[(size_t)ps->me * ps->p + o];
+        const uint32_t want = w->posts[(size_t)o];
+        if (!block) {
+            if ((int32_t)(word->load(std::memory_order_acquire) - want) < 0) { *flag = 0; return MPI_SUCCESS; }
+            continue;
+        }
+        const int rc = wait_counter(word, want, "MPI_Win_wait", o);
+        if (rc != MPI_SUCCESS) return rc;
+    }
+    return MPI_SUCCESS;
 }
 
 void engine_rma_self_guard(RmaWin* w, bool enter)
@@ -2899,8 +2981,9 @@ int engine_comm_split(Comm* parent, int color, int key, Comm** out)
     return worker().run([parent, color, key, out]() -> int {
         int nr = 0, ns = 1;
         Transport* t = nullptr;
+        std::vector<int> members(1, 0);
         if (parent->tp) {
-            const int rc = transport_split(parent->tp, color, key, &nr, &ns, &t);
+            const int rc = transport_split(parent->tp, color, key, &nr, &ns, &t, &members);
             if (rc != MPI_SUCCESS) return rc;
         } else if (color == MPI_UNDEFINED) {
             ns = 0;
@@ -2909,6 +2992,8 @@ int engine_comm_split(Comm* parent, int color, int key, Comm** out)
         Comm* c = new Comm();
         c->rank = nr;
         c->size = ns;
+        for (int m : members)                               // process ids of the members
+            c->lpid.push_back(m >= 0 && (size_t)m < parent->lpid.size() ? parent->lpid[(size_t)m] : -1);
         c->errhandler = parent->errhandler;                 // inherited from the parent
         c->tp = t;
         *out = c;

@@ -59,7 +59,8 @@ int transport_create(int rank, int size, Transport** out);
 // MPI_Comm_split over `parent` (collective): this rank's place in its color's
 // group and, for groups of two or more, the group's own transport (hub,
 // shared-memory barrier, engine windows).  color MPI_UNDEFINED: no group.
-int transport_split(Transport* parent, int color, int key, int* new_rank, int* new_size, Transport** out);
+int transport_split(Transport* parent, int color, int key, int* new_rank, int* new_size, Transport** out,
+                    std::vector<int>* members = nullptr);   // parent ranks, by new rank
 // window-allreduce phase timers (seconds): stage+scatter, collect wait+barrier A,
 // reduce+push, barrier B, last collect, chunks, calls; returns 7
 int engine_stats(double* out, int n, int reset);
@@ -171,6 +172,16 @@ struct RmaWin {
     bool lock_all = false;
     PassiveState* passive = nullptr;
     void* owned = nullptr;       // MPI_Win_allocate: memory freed with the window
+    // post-start-complete-wait (generalized active target): window ranks of the
+    // open access epoch's targets / exposure epoch's origins, and per rank the
+    // number of epochs opened so far (matched against the peers' counters)
+    bool access_epoch = false;
+    int access_assert = 0;
+    std::vector<int> access_targets;
+    std::vector<uint32_t> starts;     // per target: access epochs opened to it
+    bool exposure_epoch = false;
+    std::vector<int> exposure_origins;
+    std::vector<uint32_t> posts;      // per origin: exposure epochs opened to it
 };
 // Finish an operation's origin side: unpack a derived result, free temporaries.
 int rma_local_complete(RmaLocal& l);
@@ -196,6 +207,15 @@ int engine_rma_unlock_target(RmaWin* w, int target);       // release
 int engine_rma_flush(RmaWin* w, int target);               // complete queued ops to target
 // serialises a self-target apply with the window's service thread
 void engine_rma_self_guard(RmaWin* w, bool enter);
+// PSCW (mpid/win.cpp:3689-4088).  Post: tell each origin of the group that the
+// window is exposed to it (a counter per (target, origin) in the window's
+// shared memory).  Complete: for each target of the start group, wait for its
+// post (unless MPI_MODE_NOCHECK), ship the queued operations (applied by the
+// target's service thread, as a flush), then count this origin's epoch done at
+// the target.  Wait / test: every origin of the posted group counted done.
+int engine_rma_post(RmaWin* w);
+int engine_rma_complete(RmaWin* w);
+int engine_rma_wait(RmaWin* w, bool block, int* flag);
 
 // Run `fn` on the collective worker thread, after every collective issued
 // before it (MPI issue order); re-entrant calls from the worker run inline.

@@ -281,6 +281,48 @@ def test_rma_window_validation(msxlib):
     assert L.MPI_Win_fence(0, bad) == C.MPI_ERR_WIN
 
 
+def test_pscw_synchronisation_state(msxlib):
+    """Post-start-complete-wait epoch rules on one rank (api/mpi_win.cpp:1331-1381,
+    1487-1537, 1566-1613, 1769-1808; no GPU needed, no transfers): a second post or
+    start inside an open epoch and complete without start are MPI_ERR_RMA_SYNC,
+    wait / test without an exposure epoch succeed at once, an invalid group is
+    MPI_ERR_GROUP, MPI_Win_get_group is the communicator's group, and a window
+    with an open epoch cannot be freed."""
+    L = msxlib
+    buf = np.zeros(64, np.int32)
+    win = ctypes.c_int()
+    assert L.MPI_Win_create(buf.ctypes.data, 256, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(win)) == 0
+    W = win.value
+    assert L.MPI_Win_set_errhandler(W, C.MPI_ERRORS_RETURN) == 0
+    wg, g2 = ctypes.c_int(), ctypes.c_int()
+    assert L.MPI_Comm_group(C.MPI_COMM_WORLD, ctypes.byref(wg)) == 0
+    assert L.MPI_Win_get_group(W, ctypes.byref(g2)) == 0
+    res = ctypes.c_int()
+    assert L.MPI_Group_compare(wg.value, g2.value, ctypes.byref(res)) == 0 and res.value == C.MPI_IDENT
+    flag = ctypes.c_int(-1)
+    assert L.MPI_Win_wait(W) == 0
+    assert L.MPI_Win_test(W, ctypes.byref(flag)) == 0 and flag.value == 1
+    assert L.MPI_Win_complete(W) == C.MPI_ERR_RMA_SYNC
+    assert L.MPI_Win_post(C.MPI_GROUP_NULL, 0, W) == C.MPI_ERR_GROUP
+    assert L.MPI_Win_start(0x48000077, 0, W) == C.MPI_ERR_GROUP
+    # exposure and access to self
+    assert L.MPI_Win_post(wg.value, C.MPI_MODE_NOPUT, W) == 0
+    assert L.MPI_Win_post(wg.value, 0, W) == C.MPI_ERR_RMA_SYNC
+    assert L.MPI_Win_start(wg.value, 0, W) == 0
+    assert L.MPI_Win_start(wg.value, 0, W) == C.MPI_ERR_RMA_SYNC
+    assert L.MPI_Win_free(ctypes.byref(win)) == C.MPI_ERR_RMA_SYNC
+    assert L.MPI_Put(buf.ctypes.data, 0, C.MPI_INT, 0, 0, 0, C.MPI_INT, W) == 0
+    assert L.MPI_Win_complete(W) == 0
+    assert L.MPI_Win_test(W, ctypes.byref(flag)) == 0 and flag.value == 1
+    assert L.MPI_Win_wait(W) == 0
+    # the empty group: an epoch with nobody in it
+    assert L.MPI_Win_post(C.MPI_GROUP_EMPTY, 0, W) == 0 and L.MPI_Win_wait(W) == 0
+    assert L.MPI_Win_start(C.MPI_GROUP_EMPTY, C.MPI_MODE_NOCHECK, W) == 0 and L.MPI_Win_complete(W) == 0
+    for g in (wg, g2):
+        assert L.MPI_Group_free(ctypes.byref(g)) == 0
+    assert L.MPI_Win_free(ctypes.byref(win)) == 0
+
+
 def _build_c_demo(tmp_path):
     exe = str(tmp_path / "reduce_local_demo")
     libdir = os.path.join(msx.REPO_ROOT, "microsoft-mpi_amd", "lib")

@@ -15,6 +15,7 @@
    on a GPU-less host instead of computing on the CPU.
 """
 import ctypes
+import json
 import os
 import socket
 import subprocess
@@ -484,3 +485,91 @@ def test_comm_split_dup_free_with_user_ops():
         assert int(got[r][6]) == C.MPI_ERR_ARG and int(got[r][7]) == C.MPI_ERR_COMM
     # the duplicate of WORLD reduces like WORLD: every rank gets the same value
     assert len({got[r][5] for r in range(5)}) == 1
+
+
+GROUP_WORKER = r'''
+import ctypes, json, os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
+import msx
+C = msx.C
+L = msx.init(errors_return=True)
+r = ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r))
+rank = r.value
+G = lambda: ctypes.c_int()
+def members(g):
+    n = ctypes.c_int(); assert L.MPI_Group_size(g, ctypes.byref(n)) == 0
+    a = (ctypes.c_int * max(n.value, 1))(*range(n.value))
+    w = G(); assert L.MPI_Comm_group(C.MPI_COMM_WORLD, ctypes.byref(w)) == 0
+    out = (ctypes.c_int * max(n.value, 1))()
+    assert L.MPI_Group_translate_ranks(g, n.value, a, w.value, out) == 0
+    return list(out)[:n.value]
+wg = G(); assert L.MPI_Comm_group(C.MPI_COMM_WORLD, ctypes.byref(wg)) == 0
+ia = (ctypes.c_int * 3)(4, 1, 3)
+inc = G(); assert L.MPI_Group_incl(wg.value, 3, ia, ctypes.byref(inc)) == 0
+exc = G(); assert L.MPI_Group_excl(wg.value, 3, ia, ctypes.byref(exc)) == 0
+rg = (ctypes.c_int * 6)(4, 0, -2, 1, 1, 1)          # ranges (4,0,-2) and (1,1,1): 4, 2, 0, 1
+rinc = G(); assert L.MPI_Group_range_incl(wg.value, 2, rg, ctypes.byref(rinc)) == 0
+rexc = G(); assert L.MPI_Group_range_excl(wg.value, 2, rg, ctypes.byref(rexc)) == 0
+un = G(); assert L.MPI_Group_union(inc.value, rinc.value, ctypes.byref(un)) == 0
+it = G(); assert L.MPI_Group_intersection(inc.value, rinc.value, ctypes.byref(it)) == 0
+df = G(); assert L.MPI_Group_difference(rinc.value, inc.value, ctypes.byref(df)) == 0
+gr = ctypes.c_int(); assert L.MPI_Group_rank(inc.value, ctypes.byref(gr)) == 0
+cmp = []
+for a, b in ((wg, wg), (inc, inc), (un, wg), (inc, rinc)):
+    c = ctypes.c_int(); assert L.MPI_Group_compare(a.value, b.value, ctypes.byref(c)) == 0; cmp.append(c.value)
+sim = (ctypes.c_int * 5)(4, 3, 2, 1, 0)
+rv = G(); assert L.MPI_Group_incl(wg.value, 5, sim, ctypes.byref(rv)) == 0
+c = ctypes.c_int(); assert L.MPI_Group_compare(rv.value, wg.value, ctypes.byref(c)) == 0; cmp.append(c.value)
+# a split communicator's group holds WORLD process ids: odd = {3, 1} by key -rank
+sub = ctypes.c_int()
+assert L.MPI_Comm_split(C.MPI_COMM_WORLD, rank % 2, -rank, ctypes.byref(sub)) == 0
+sg = G(); assert L.MPI_Comm_group(sub.value, ctypes.byref(sg)) == 0
+# translate ranks incl. MPI_PROC_NULL and a non-member
+tr_in = (ctypes.c_int * 3)(0, -1, 2)
+tr_out = (ctypes.c_int * 3)()
+assert L.MPI_Group_translate_ranks(inc.value, 3, tr_in, exc.value, tr_out) == 0
+errs = [L.MPI_Group_incl(wg.value, 2, (ctypes.c_int * 2)(1, 1), ctypes.byref(G())),     # duplicate
+        L.MPI_Group_incl(wg.value, 1, (ctypes.c_int * 1)(5), ctypes.byref(G())),        # out of range
+        L.MPI_Group_range_incl(wg.value, 1, (ctypes.c_int * 3)(0, 4, 0), ctypes.byref(G())),   # stride 0
+        L.MPI_Group_size(C.MPI_GROUP_NULL, ctypes.byref(ctypes.c_int())),
+        L.MPI_Group_size(0x48000099, ctypes.byref(ctypes.c_int()))]
+ex = ctypes.c_int(C.MPI_GROUP_EMPTY)
+assert L.MPI_Group_free(ctypes.byref(ex)) == 0 and ex.value == C.MPI_GROUP_NULL
+e0 = G(); assert L.MPI_Group_excl(wg.value, 0, None, ctypes.byref(e0)) == 0
+print("M", rank, json.dumps([members(g.value) for g in (inc, exc, rinc, rexc, un, it, df, sg)]), flush=True)
+print("G", rank, json.dumps([gr.value, cmp, list(tr_out), errs]), flush=True)
+for g in (inc, exc, rinc, rexc, un, it, df, rv, sg, wg):
+    assert L.MPI_Group_free(ctypes.byref(g)) == 0 and g.value == C.MPI_GROUP_NULL
+assert L.MPI_Finalize() == 0
+'''
+
+
+def test_groups_five_processes():
+    """MPI groups (api/mpi_group.cpp): incl / excl / range_incl / range_excl /
+    union / intersection / difference member order, translate_ranks with
+    MPI_PROC_NULL and non-members, compare (IDENT / SIMILAR / UNEQUAL), the
+    reference's rank and range checks, groups of split communicators.
+    Host-only calls: no GPU involved."""
+    port = _free_port()
+    outs = _spawn(GROUP_WORKER, 5, lambda r: {"MSX_SIZE": "5", "MSX_RANK": str(r),
+                                              "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1"})
+    U = -32766
+    for rc, o, e in outs:
+        assert rc == 0, e[-3000:]
+        f = [l for l in o.splitlines() if l.startswith("G ")][0].split(" ", 2)
+        rank = int(f[1])
+        gr, cmp, tr, errs = json.loads(f[2])
+        # incl(4,1,3): rank of world 4 -> 0, 1 -> 1, 3 -> 2, others undefined
+        assert gr == {4: 0, 1: 1, 3: 2}.get(rank, U), (rank, gr)
+        # compare: world/world IDENT, inc/inc IDENT, union(inc, rinc) = 4,1,3,2,0 vs world SIMILAR,
+        # inc vs rinc (sizes 3 / 4) UNEQUAL, reversed world SIMILAR
+        assert list(cmp) == [C.MPI_IDENT, C.MPI_IDENT, C.MPI_SIMILAR, C.MPI_UNEQUAL, C.MPI_SIMILAR]
+        # translate inc ranks (0 -> world 4, PROC_NULL, 2 -> world 3) into excl = {0, 2}
+        assert list(tr) == [U, -1, U]
+        assert list(errs) == [C.MPI_ERR_RANK, C.MPI_ERR_RANK, C.MPI_ERR_ARG, C.MPI_ERR_GROUP, C.MPI_ERR_GROUP]
+        m = [l for l in o.splitlines() if l.startswith("M ")][0].split(" ", 2)[2]
+        inc, exc, rinc, rexc, un, it, df, sg = json.loads(m)
+        assert inc == [4, 1, 3] and exc == [0, 2] and rinc == [4, 2, 0, 1] and rexc == [3]
+        assert un == [4, 1, 3, 2, 0] and it == [4, 1] and df == [2, 0]
+        assert sg == ([3, 1] if rank % 2 else [4, 2, 0])
