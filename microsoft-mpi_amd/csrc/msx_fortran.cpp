@@ -176,6 +176,64 @@ FAPI void mpi_comm_dup_(const MPI_Fint* comm, MPI_Fint* newcomm, MPI_Fint* ierr)
 FNAMES(comm_dup, COMM_DUP)
 FAPI void mpi_comm_free_(MPI_Fint* comm, MPI_Fint* ierr) { *ierr = MPI_Comm_free(comm); }
 FNAMES(comm_free, COMM_FREE)
+// groups (api/mpi_group.cpp): ranks are ranks, not Fortran indices
+FAPI void mpi_comm_group_(const MPI_Fint* comm, MPI_Fint* group, MPI_Fint* ierr) { *ierr = MPI_Comm_group(*comm, group); }
+FNAMES(comm_group, COMM_GROUP)
+FAPI void mpi_group_size_(const MPI_Fint* group, MPI_Fint* size, MPI_Fint* ierr) { *ierr = MPI_Group_size(*group, size); }
+FNAMES(group_size, GROUP_SIZE)
+FAPI void mpi_group_rank_(const MPI_Fint* group, MPI_Fint* rank, MPI_Fint* ierr) { *ierr = MPI_Group_rank(*group, rank); }
+FNAMES(group_rank, GROUP_RANK)
+FAPI void mpi_group_incl_(const MPI_Fint* group, const MPI_Fint* n, const MPI_Fint* ranks, MPI_Fint* out, MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_incl(*group, *n, ranks, out);
+}
+FNAMES(group_incl, GROUP_INCL)
+FAPI void mpi_group_excl_(const MPI_Fint* group, const MPI_Fint* n, const MPI_Fint* ranks, MPI_Fint* out, MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_excl(*group, *n, ranks, out);
+}
+FNAMES(group_excl, GROUP_EXCL)
+// ranges: INTEGER RANGES(3, N), column-major = n consecutive (first, last, stride) triples
+FAPI void mpi_group_range_incl_(const MPI_Fint* group, const MPI_Fint* n, MPI_Fint* ranges, MPI_Fint* out,
+                                MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_range_incl(*group, *n, reinterpret_cast<int (*)[3]>(ranges), out);
+}
+FNAMES(group_range_incl, GROUP_RANGE_INCL)
+FAPI void mpi_group_range_excl_(const MPI_Fint* group, const MPI_Fint* n, MPI_Fint* ranges, MPI_Fint* out,
+                                MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_range_excl(*group, *n, reinterpret_cast<int (*)[3]>(ranges), out);
+}
+FNAMES(group_range_excl, GROUP_RANGE_EXCL)
+FAPI void mpi_group_union_(const MPI_Fint* a, const MPI_Fint* b, MPI_Fint* out, MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_union(*a, *b, out);
+}
+FNAMES(group_union, GROUP_UNION)
+FAPI void mpi_group_intersection_(const MPI_Fint* a, const MPI_Fint* b, MPI_Fint* out, MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_intersection(*a, *b, out);
+}
+FNAMES(group_intersection, GROUP_INTERSECTION)
+FAPI void mpi_group_difference_(const MPI_Fint* a, const MPI_Fint* b, MPI_Fint* out, MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_difference(*a, *b, out);
+}
+FNAMES(group_difference, GROUP_DIFFERENCE)
+FAPI void mpi_group_translate_ranks_(const MPI_Fint* a, const MPI_Fint* n, const MPI_Fint* ranks, const MPI_Fint* b,
+                                     MPI_Fint* out, MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_translate_ranks(*a, *n, ranks, *b, out);
+}
+FNAMES(group_translate_ranks, GROUP_TRANSLATE_RANKS)
+FAPI void mpi_group_compare_(const MPI_Fint* a, const MPI_Fint* b, MPI_Fint* result, MPI_Fint* ierr)
+{
+    *ierr = MPI_Group_compare(*a, *b, result);
+}
+FNAMES(group_compare, GROUP_COMPARE)
+FAPI void mpi_group_free_(MPI_Fint* group, MPI_Fint* ierr) { *ierr = MPI_Group_free(group); }
+FNAMES(group_free, GROUP_FREE)
 FAPI void mpi_comm_set_errhandler_(const MPI_Fint* comm, const MPI_Fint* eh, MPI_Fint* ierr)
 {
     *ierr = MPI_Comm_set_errhandler(*comm, *eh);
@@ -607,6 +665,32 @@ FAPI void mpi_win_flush_local_all_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr 
 FNAMES(win_flush_local_all, WIN_FLUSH_LOCAL_ALL)
 FAPI void mpi_win_sync_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_sync(*win); }
 FNAMES(win_sync, WIN_SYNC)
+FAPI void mpi_win_post_(const MPI_Fint* group, const MPI_Fint* assert_, const MPI_Fint* win, MPI_Fint* ierr)
+{
+    *ierr = MPI_Win_post(*group, *assert_, *win);
+}
+FNAMES(win_post, WIN_POST)
+FAPI void mpi_win_start_(const MPI_Fint* group, const MPI_Fint* assert_, const MPI_Fint* win, MPI_Fint* ierr)
+{
+    *ierr = MPI_Win_start(*group, *assert_, *win);
+}
+FNAMES(win_start, WIN_START)
+FAPI void mpi_win_complete_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_complete(*win); }
+FNAMES(win_complete, WIN_COMPLETE)
+FAPI void mpi_win_wait_(const MPI_Fint* win, MPI_Fint* ierr) { *ierr = MPI_Win_wait(*win); }
+FNAMES(win_wait, WIN_WAIT)
+FAPI void mpi_win_test_(const MPI_Fint* win, MPI_Fint* flag, MPI_Fint* ierr)
+{
+    int f = 0;
+    *ierr = MPI_Win_test(*win, &f);
+    *flag = to_flog(f);
+}
+FNAMES(win_test, WIN_TEST)
+FAPI void mpi_win_get_group_(const MPI_Fint* win, MPI_Fint* group, MPI_Fint* ierr)
+{
+    *ierr = MPI_Win_get_group(*win, group);
+}
+FNAMES(win_get_group, WIN_GET_GROUP)
 FAPI void mpi_win_set_errhandler_(const MPI_Fint* win, const MPI_Fint* eh, MPI_Fint* ierr)
 {
     *ierr = MPI_Win_set_errhandler(*win, *eh);

@@ -25,6 +25,8 @@ program fcpu
   integer a(10), b(10), c(10)
   integer reqs(3), idx, nout, idxs(3), st(MPI_STATUS_SIZE)
   logical flag, comm
+  integer wg, g1, g2, g3, ranges(3, 2), tin(2), tout(2), gres, win
+  integer(kind=MPI_ADDRESS_KIND) wsize
   double precision t
   character(len=600) msg
   integer seen_len, seen_type
@@ -143,6 +145,61 @@ program fcpu
   print '(A,I0,1X,I0,1X,I0)', 'TESTSOME ', ierr, nout, idxs(1)
   call MPI_TESTSOME(3, reqs, nout, idxs, MPI_STATUSES_IGNORE, ierr)
   print '(A,I0)', 'TESTSOME_NONE ', nout
+
+  ! groups (one process): range (0, 0, 1) twice is a duplicate (MPI_ERR_ARG)
+  call MPI_COMM_GROUP(MPI_COMM_WORLD, wg, ierr)
+  call MPI_GROUP_SIZE(wg, sz, ierr)
+  call MPI_GROUP_RANK(wg, i, ierr)
+  print '(A,I0,1X,I0,1X,I0)', 'GROUP ', ierr, sz, i
+  ranges(:, 1) = (/ 0, 0, 1 /)
+  call MPI_GROUP_RANGE_INCL(wg, 1, ranges, g1, ierr)
+  call MPI_GROUP_COMPARE(g1, wg, gres, ierr)
+  print '(A,I0,1X,L1)', 'RANGE_INCL ', ierr, gres == MPI_IDENT
+  ranges(:, 2) = (/ 0, 0, 1 /)
+  call MPI_GROUP_RANGE_INCL(wg, 2, ranges, g3, ierr)
+  call MPI_ERROR_CLASS(ierr, cls, i)
+  print '(A,I0)', 'RANGE_DUP_CLASS ', cls
+  call MPI_GROUP_EXCL(wg, 1, (/ 0 /), g2, ierr)
+  call MPI_GROUP_SIZE(g2, sz, ierr)
+  call MPI_GROUP_RANK(g2, i, ierr)
+  print '(A,I0,1X,I0,1X,I0)', 'EXCL ', ierr, sz, i
+  tin = (/ 0, MPI_PROC_NULL /)
+  call MPI_GROUP_TRANSLATE_RANKS(wg, 2, tin, g2, tout, ierr)
+  print '(A,I0,1X,I0,1X,I0)', 'TRANSLATE ', ierr, tout(1), tout(2)
+  call MPI_GROUP_UNION(g2, wg, g3, ierr)
+  call MPI_GROUP_COMPARE(g3, wg, gres, ierr)
+  print '(A,L1)', 'UNION_IDENT ', gres == MPI_IDENT
+  call MPI_GROUP_FREE(g3, ierr)
+  call MPI_GROUP_INTERSECTION(g2, wg, g3, ierr)
+  call MPI_GROUP_COMPARE(g3, MPI_GROUP_EMPTY, gres, ierr)
+  print '(A,L1)', 'INTERSECTION_EMPTY ', gres == MPI_IDENT
+  call MPI_GROUP_FREE(g3, ierr)
+  call MPI_GROUP_DIFFERENCE(wg, g1, g3, ierr)
+  call MPI_GROUP_SIZE(g3, sz, ierr)
+  print '(A,I0)', 'DIFFERENCE ', sz
+  call MPI_GROUP_FREE(g3, ierr)
+
+  ! post-start-complete-wait on a one-rank window (no transfers)
+  wsize = 40
+  call MPI_WIN_CREATE(a, wsize, 4, MPI_INFO_NULL, MPI_COMM_WORLD, win, ierr)
+  call MPI_WIN_SET_ERRHANDLER(win, MPI_ERRORS_RETURN, ierr)
+  call MPI_WIN_GET_GROUP(win, g3, ierr)
+  call MPI_GROUP_COMPARE(g3, wg, gres, ierr)
+  call MPI_WIN_POST(wg, 0, win, ierr)
+  call MPI_WIN_START(wg, MPI_MODE_NOCHECK, win, ierr)
+  call MPI_WIN_COMPLETE(win, ierr)
+  call MPI_WIN_TEST(win, flag, ierr)
+  print '(A,I0,1X,L1,1X,L1)', 'PSCW ', ierr, flag, gres == MPI_IDENT
+  call MPI_WIN_COMPLETE(win, ierr)
+  call MPI_ERROR_CLASS(ierr, cls, i)
+  print '(A,I0)', 'COMPLETE_CLASS ', cls
+  call MPI_WIN_WAIT(win, ierr)
+  call MPI_WIN_FREE(win, ierr)
+  call MPI_GROUP_FREE(g1, ierr)
+  call MPI_GROUP_FREE(g2, ierr)
+  call MPI_GROUP_FREE(g3, ierr)
+  call MPI_GROUP_FREE(wg, ierr)
+  print '(A,I0,1X,L1)', 'GROUP_FREE ', ierr, wg == MPI_GROUP_NULL
 
   msg = 'x'
   call MPI_ERROR_STRING(MPI_ERR_OP, msg, rlen, ierr)

@@ -30,7 +30,12 @@ ENTRIES = [
     "op_create", "op_commutative", "op_free",
     "reduce_local", "reduce", "ireduce", "allreduce", "iallreduce", "reduce_scatter", "ireduce_scatter",
     "reduce_scatter_block", "ireduce_scatter_block", "scan", "iscan", "exscan", "iexscan",
-    "wait", "test", "waitall",
+    "wait", "test", "waitall", "waitany", "waitsome", "testall", "testany", "testsome", "request_free",
+    "request_get_status",
+    "comm_group", "group_size", "group_rank", "group_incl", "group_excl", "group_range_incl",
+    "group_range_excl", "group_union", "group_intersection", "group_difference", "group_translate_ranks",
+    "group_compare", "group_free",
+    "win_post", "win_start", "win_complete", "win_wait", "win_test", "win_get_group",
     "type_size", "type_size_x", "type_contiguous", "type_vector", "type_hvector", "type_create_hvector",
     "type_indexed", "type_hindexed", "type_create_hindexed", "type_create_indexed_block",
     "type_create_hindexed_block", "type_struct", "type_create_struct", "type_create_subarray",
@@ -150,6 +155,18 @@ def test_fortran_program_without_gpu():
     assert as_int("REQUEST_FREE_CLASS") == [C.MPI_ERR_OTHER]
     assert as_int("TESTSOME") == [0, 1, 1]
     assert as_int("TESTSOME_NONE") == [-32766]
+    assert as_int("GROUP") == [0, 1, 0]
+    assert out["RANGE_INCL"] == ["0", "T"]
+    assert as_int("RANGE_DUP_CLASS") == [C.MPI_ERR_ARG]     # **rangedup, mpid/group.cpp:372-390
+    assert as_int("EXCL") == [0, 0, -32766]
+    # group2 is empty: even MPI_PROC_NULL stays MPI_UNDEFINED (api/mpi_group.cpp:1351-1368)
+    assert as_int("TRANSLATE") == [0, -32766, -32766]
+    assert out["UNION_IDENT"] == ["T"]
+    assert out["INTERSECTION_EMPTY"] == ["T"]
+    assert as_int("DIFFERENCE") == [0]
+    assert out["PSCW"] == ["0", "T", "T"]
+    assert as_int("COMPLETE_CLASS") == [C.MPI_ERR_RMA_SYNC]
+    assert out["GROUP_FREE"] == ["0", "T"]
     assert out["ERROR_STRING"] == ["0", "T", "T"]
     assert as_int("PACK_SIZE") == [12]
     assert out["WTIME"] == ["T"]
