@@ -362,6 +362,36 @@ def main(out_path, scale):
         res["rma_accumulate_sum_f32_fence"] = {
             "bytes_per_rank": n * 4, "seconds": round(t, 5), "GB_s_per_rank": round(n * 4 / t / 1e9, 2),
             "correct": bool(torch.all(base == 1.0 + (reps + 1) * (src_rank + 1)).item())}
+        done = 1.0 + (reps + 1) * (src_rank + 1)
+
+        # the same accumulate in a passive-target epoch (lock / unlock: the
+        # target's service thread applies it) and in a post-start-complete-wait
+        # epoch with the ring's neighbours
+        def passive():
+            return (L.MPI_Win_lock(C.MPI_LOCK_SHARED, tgt, 0, win) or
+                    L.MPI_Accumulate(contrib.data_ptr(), n, C.MPI_FLOAT, tgt, 0, n, C.MPI_FLOAT, C.MPI_SUM, win) or
+                    L.MPI_Win_unlock(tgt, win))
+        wg = ctypes.c_int()
+        L.MPI_Comm_group(C.MPI_COMM_WORLD, ctypes.byref(wg))
+        gprev, gnext = ctypes.c_int(), ctypes.c_int()
+        L.MPI_Group_incl(wg.value, 1, (ctypes.c_int * 1)(src_rank), ctypes.byref(gprev))
+        L.MPI_Group_incl(wg.value, 1, (ctypes.c_int * 1)(tgt), ctypes.byref(gnext))
+
+        def pscw():
+            return (L.MPI_Win_post(gprev.value, 0, win) or L.MPI_Win_start(gnext.value, 0, win) or
+                    L.MPI_Accumulate(contrib.data_ptr(), n, C.MPI_FLOAT, tgt, 0, n, C.MPI_FLOAT, C.MPI_SUM, win) or
+                    L.MPI_Win_complete(win) or L.MPI_Win_wait(win))
+        for key, fn in (("rma_accumulate_sum_f32_lock", passive), ("rma_accumulate_sum_f32_pscw", pscw)):
+            t, rc = timed(fn)
+            if rc:
+                res[key] = {"error": f"rc={rc} {msx.last_error()}"}
+                break
+            barrier()
+            done += (3 + 1) * (src_rank + 1)
+            res[key] = {"bytes_per_rank": n * 4, "seconds": round(t, 5), "GB_s_per_rank": round(n * 4 / t / 1e9, 2),
+                        "correct": bool(torch.all(base == done).item())}
+        for g in (gprev, gnext, wg):
+            L.MPI_Group_free(ctypes.byref(g))
         L.MPI_Win_free(ctypes.byref(win))
     barrier()
     L.msx_engine_transport.restype = ctypes.c_char_p

@@ -1096,8 +1096,24 @@ size_t chunk_bytes()
 // flag k of window r (8 bytes) = the last call sequence rank k posted to r.
 constexpr size_t kFlagBytes = 64 << 10;
 // Passive-target RMA area behind the flags: p payload slots (written by each
-// origin) then p fetch slots (written by each target), kRmaBytes / (2p) each.
-constexpr size_t kRmaBytes = (size_t)64 << 20;
+// origin) then p fetch slots (written by each target), rma_bytes() / (2p) each.
+// Every slot-sized piece of a lock / PSCW operation costs one host handshake
+// with the target's service thread (~50 us), so the area is sized for large
+// pieces (MSX_RMA_BYTES, default 512 MiB), bounded so the window stays below
+// the 2 GiB IPC limit.  256 MiB lock / PSCW accumulates, 2 ranks on one MI355X
+// (profiles/r02/rma_area_*.json): 1.27 ms with 64 MiB, 0.66 ms with 256 MiB,
+// 0.53 ms with 512 MiB (= the fence epoch's 0.54 ms).
+size_t rma_bytes()
+{
+    static size_t v = [] {
+        size_t b = (size_t)512 << 20;
+        if (const char* e = getenv("MSX_RMA_BYTES")) b = (size_t)atoll(e);
+        const size_t cap = ((size_t)2 << 30) - 2 * chunk_bytes() - kFlagBytes - ((size_t)1 << 20);
+        b = std::min(b, cap);
+        return std::max(b, (size_t)4 << 20) & ~(size_t)4095;
+    }();
+    return v;
+}
 
 // Sub-slots are Q bytes long but S = Q + skew apart: the p-source tree reads
 // every sub-slot at the same offset, and sources a power of two apart lose
@@ -1124,7 +1140,7 @@ struct Windows {
     char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * S; }
     char* out(int r) const { return base[(size_t)r] + C; }
     unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + 2 * C); }
-    size_t rma_slot() const { return (kRmaBytes / (2 * base.size())) & ~(size_t)255; }
+    size_t rma_slot() const { return (rma_bytes() / (2 * base.size())) & ~(size_t)255; }
     // rank r's window: payload slot written by origin o / fetch slot written by target t
     char* rma_in(int r, int o) const { return base[(size_t)r] + 2 * C + kFlagBytes + (size_t)o * rma_slot(); }
     char* rma_fetch(int r, int t) const
@@ -1186,7 +1202,7 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
     w->C = chunk_bytes();
     w->Q = sub_len(w->C, tp->size);
     w->S = w->Q + sub_skew(w->C / (size_t)tp->size);
-    int rc = tp->window(2 * w->C + kFlagBytes + kRmaBytes, w->base);
+    int rc = tp->window(2 * w->C + kFlagBytes + rma_bytes(), w->base);
     if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
         // the last recursive-doubling call left without its closing barrier:
         // peers may still be reading their IN areas

@@ -185,7 +185,8 @@ def test_post_start_complete_wait(p, hostwin):
         env = dict(os.environ)
         env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
-                    "MSX_BOOTSTRAP_TIMEOUT": "180", "HOSTWIN": "1" if hostwin else "0"})
+                    "MSX_BOOTSTRAP_TIMEOUT": "180", "HOSTWIN": "1" if hostwin else "0",
+                    "MSX_RMA_BYTES": "16777216"})   # 16 MiB RMA area: section 5 spans several staging slots
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
