@@ -25,8 +25,8 @@ extern "C" {
 /* mpi.h:515 */
 #define MPI_METHOD int MPIAPI
 
-#define MPI_VERSION    2
-#define MPI_SUBVERSION 2
+#define MPI_VERSION    2      /* mpi.h:4070-4071: MS-MPI reports 2.0 */
+#define MPI_SUBVERSION 0
 
 /* ---- error classes (mpi.h:192-250) -------------------------------------- */
 #define MPI_SUCCESS          0
@@ -63,6 +63,7 @@ extern "C" {
 #define MPI_ERR_LASTCODE    0x3fffffff
 
 #define MPI_MAX_ERROR_STRING 512
+#define MPI_MAX_PROCESSOR_NAME 128
 
 /* ---- basic integer types (mpi.h:258-270, Win64 / LLP64) ------------------ */
 typedef int64_t MPI_Aint;
@@ -219,6 +220,11 @@ MPI_METHOD MPI_Initialized(int* flag);
 MPI_METHOD MPI_Finalized(int* flag);
 MPI_METHOD MPI_Abort(MPI_Comm comm, int errorcode);
 double MPIAPI MPI_Wtime(void);
+double MPIAPI MPI_Wtick(void);
+MPI_METHOD MPI_Query_thread(int* provided);
+MPI_METHOD MPI_Is_thread_main(int* flag);
+MPI_METHOD MPI_Get_version(int* version, int* subversion);
+MPI_METHOD MPI_Get_processor_name(char* name, int* resultlen);
 MPI_METHOD MPI_Comm_rank(MPI_Comm comm, int* rank);
 MPI_METHOD MPI_Comm_size(MPI_Comm comm, int* size);
 MPI_METHOD MPI_Barrier(MPI_Comm comm);
@@ -359,6 +365,9 @@ MPI_METHOD MPI_Compare_and_swap(const void* origin_addr, const void* compare_add
 
 /* ---- groups (api/mpi_group.cpp, api/mpi_comm.cpp:677) -------------------- */
 MPI_METHOD MPI_Comm_group(MPI_Comm comm, MPI_Group* group);
+MPI_METHOD MPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm* newcomm);
+MPI_METHOD MPI_Comm_compare(MPI_Comm comm1, MPI_Comm comm2, int* result);
+MPI_METHOD MPI_Comm_test_inter(MPI_Comm comm, int* flag);
 MPI_METHOD MPI_Group_size(MPI_Group group, int* size);
 MPI_METHOD MPI_Group_rank(MPI_Group group, int* rank);
 MPI_METHOD MPI_Group_free(MPI_Group* group);
@@ -531,6 +540,8 @@ MPI_METHOD PMPI_Get_accumulate(const void* origin_addr, int origin_count,
 MPI_METHOD PMPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Datatype datatype,
                              int target_rank, MPI_Aint target_disp, MPI_Op op, MPI_Win win);
 MPI_METHOD PMPI_Comm_group(MPI_Comm comm, MPI_Group* group);
+MPI_METHOD PMPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm* newcomm);
+MPI_METHOD PMPI_Comm_compare(MPI_Comm comm1, MPI_Comm comm2, int* result);
 MPI_METHOD PMPI_Group_size(MPI_Group group, int* size);
 MPI_METHOD PMPI_Group_rank(MPI_Group group, int* rank);
 MPI_METHOD PMPI_Group_free(MPI_Group* group);

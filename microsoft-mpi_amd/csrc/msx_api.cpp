@@ -18,6 +18,8 @@
 #include <map>
 #include <chrono>
 #include <mutex>
+#include <thread>
+#include <unistd.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -241,6 +243,11 @@ int api_comm_valid(MPI_Comm comm)
 // ===========================================================================
 // environment
 // ===========================================================================
+namespace {
+int g_thread_level = MPI_THREAD_SINGLE;     // Mpi.ThreadLevel
+std::thread::id g_main_thread;              // the thread that initialised MPI
+}
+
 MSX_EXPORT int MPI_Init(int* argc, char*** argv)
 {
     (void)argc; (void)argv;
@@ -253,6 +260,8 @@ MSX_EXPORT int MPI_Init(int* argc, char*** argv)
         fprintf(stderr, "Fatal error in MPI_Init: %s\n", last_error());
         exit(rc);
     }
+    g_thread_level = MPI_THREAD_SINGLE;       // mpi_env.cpp:167
+    g_main_thread = std::this_thread::get_id();
     return MPI_SUCCESS;
 }
 
@@ -261,7 +270,9 @@ MSX_EXPORT int MPI_Init_thread(int* argc, char*** argv, int required, int* provi
     int rc = MPI_Init(argc, argv);
     // Kernels are reentrant; the host staging path and bootstrap are locked
     // (mid/env.cpp:1071-1078 grants up to MULTIPLE).
-    if (provided) *provided = required > MPI_THREAD_MULTIPLE ? MPI_THREAD_MULTIPLE : required;
+    const int level = required > MPI_THREAD_MULTIPLE ? MPI_THREAD_MULTIPLE : required;
+    if (rc == MPI_SUCCESS) g_thread_level = level;
+    if (provided) *provided = level;
     return rc;
 }
 
@@ -297,6 +308,60 @@ MSX_EXPORT double MPI_Wtime(void)
 {
     using namespace std::chrono;
     return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+// the resolution of MPI_Wtime's clock (mpi_env.cpp:767)
+MSX_EXPORT double MPI_Wtick(void)
+{
+    using namespace std::chrono;
+    return duration<double>(steady_clock::duration(1)).count();
+}
+
+// mpi_env.cpp:575-610: the level MPI_Init / MPI_Init_thread provided
+MSX_EXPORT int MPI_Query_thread(int* provided)
+{
+    MSX_REQUIRE_INIT("MPI_Query_thread");
+    if (!provided) { set_error("**nullptr provided"); return err_return(nullptr, "MPI_Query_thread", MPI_ERR_ARG); }
+    *provided = g_thread_level;
+    return MPI_SUCCESS;
+}
+
+// mpi_env.cpp:463-500: is the caller the thread that initialised MPI
+MSX_EXPORT int MPI_Is_thread_main(int* flag)
+{
+    MSX_REQUIRE_INIT("MPI_Is_thread_main");
+    if (!flag) { set_error("**nullptr flag"); return err_return(nullptr, "MPI_Is_thread_main", MPI_ERR_ARG); }
+    *flag = std::this_thread::get_id() == g_main_thread ? 1 : 0;
+    return MPI_SUCCESS;
+}
+
+// mpi_env.cpp:630-680; callable before MPI_Init
+MSX_EXPORT int MPI_Get_version(int* version, int* subversion)
+{
+    if (!version || !subversion) {
+        set_error("**nullptr %s", version ? "subversion" : "version");
+        return is_initialized() ? err_return(nullptr, "MPI_Get_version", MPI_ERR_ARG) : MPI_ERR_ARG;
+    }
+    *version = MPI_VERSION;
+    *subversion = MPI_SUBVERSION;
+    return MPI_SUCCESS;
+}
+
+// mpi_env.cpp:1095-1140 (MPID_Get_processor_name: the host name)
+MSX_EXPORT int MPI_Get_processor_name(char* name, int* resultlen)
+{
+    MSX_REQUIRE_INIT("MPI_Get_processor_name");
+    if (!name || !resultlen) {
+        set_error("**nullptr %s", name ? "resultlen" : "name");
+        return err_return(nullptr, "MPI_Get_processor_name", MPI_ERR_ARG);
+    }
+    char host[MPI_MAX_PROCESSOR_NAME] = {0};
+    if (gethostname(host, sizeof(host) - 1) != 0) snprintf(host, sizeof(host), "localhost");
+    const size_t n = strnlen(host, MPI_MAX_PROCESSOR_NAME - 1);
+    memcpy(name, host, n);
+    name[n] = 0;
+    *resultlen = (int)n;
+    return MPI_SUCCESS;
 }
 
 MSX_EXPORT int MPI_Comm_rank(MPI_Comm comm, int* rank)
@@ -352,6 +417,74 @@ MSX_EXPORT int MPI_Comm_dup(MPI_Comm comm, MPI_Comm* newcomm)
     if (rc == MPI_SUCCESS) rc = engine_comm_split(c, 0, c->rank, &n);   // same group, same order
     if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_dup", rc);
     *newcomm = comm_register(n);
+    return MPI_SUCCESS;
+}
+
+// api/mpi_comm.cpp:184-248, MPIR_Comm_create_intra (mpid/comm.cpp:1027-1128):
+// collective over `comm`; members get a communicator ranked in group order,
+// the others MPI_COMM_NULL.  A group member outside `comm` is MPI_ERR_GROUP
+// (**groupnotincomm, comm.cpp:977) on the members, after the collective step
+// every process takes (here the split, there the context id).
+MSX_EXPORT int MPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm* newcomm)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_create");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_create", rc);
+    std::vector<int> members;
+    rc = group_members(group, &members);
+    if (rc == MPI_SUCCESS && !newcomm) { set_error("null newcomm"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_create", rc);
+    const int me = c->lpid.empty() ? c->rank : c->lpid[(size_t)c->rank];
+    int grank = MPI_UNDEFINED;
+    bool valid = true;
+    for (size_t i = 0; i < members.size(); ++i) {
+        if (members[i] == me) grank = (int)i;
+        if (std::find(c->lpid.begin(), c->lpid.end(), members[i]) == c->lpid.end()) valid = false;
+    }
+    Comm* n = nullptr;
+    rc = engine_comm_split(c, grank != MPI_UNDEFINED && valid ? 0 : MPI_UNDEFINED, grank, &n);
+    if (rc == MPI_SUCCESS && grank != MPI_UNDEFINED && !valid) {
+        set_error("**groupnotincomm: a group member is not in the communicator");
+        rc = MPI_ERR_GROUP;
+    }
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_create", rc);
+    *newcomm = n ? comm_register(n) : MPI_COMM_NULL;
+    return MPI_SUCCESS;
+}
+
+// api/mpi_comm.cpp:51-157 (intracommunicators): IDENT for the same handle,
+// else the groups' relation with IDENT promoted to CONGRUENT
+MSX_EXPORT int MPI_Comm_compare(MPI_Comm comm1, MPI_Comm comm2, int* result)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_compare");
+    Comm *c1, *c2 = nullptr;
+    int rc = v_comm(comm1, &c1);
+    if (rc == MPI_SUCCESS) rc = v_comm(comm2, &c2);
+    if (rc == MPI_SUCCESS && !result) { set_error("**nullptr result"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_compare", rc);
+    if (comm1 == comm2) {
+        *result = MPI_IDENT;
+    } else if (c1->lpid == c2->lpid) {
+        *result = MPI_CONGRUENT;
+    } else {
+        std::vector<int> a = c1->lpid, b = c2->lpid;
+        std::sort(a.begin(), a.end());
+        std::sort(b.begin(), b.end());
+        *result = a == b ? MPI_SIMILAR : MPI_UNEQUAL;
+    }
+    return MPI_SUCCESS;
+}
+
+// api/mpi_comm.cpp:1386-1420: every communicator here is an intracommunicator
+MSX_EXPORT int MPI_Comm_test_inter(MPI_Comm comm, int* flag)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_test_inter");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !flag) { set_error("**nullptr flag"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_test_inter", rc);
+    *flag = 0;
     return MPI_SUCCESS;
 }
 
@@ -1041,6 +1174,8 @@ MSX_EXPORT int MPI_Request_get_status(MPI_Request request, int* flag, MPI_Status
 MSX_ALIAS(MPI_Reduce_local) int PMPI_Reduce_local(const void*, void*, int, MPI_Datatype, MPI_Op);
 MSX_ALIAS(MPI_Testall) int PMPI_Testall(int, MPI_Request[], int*, MPI_Status[]);
 MSX_ALIAS(MPI_Win_post) int PMPI_Win_post(MPI_Group, int, MPI_Win);
+MSX_ALIAS(MPI_Comm_create) int PMPI_Comm_create(MPI_Comm, MPI_Group, MPI_Comm*);
+MSX_ALIAS(MPI_Comm_compare) int PMPI_Comm_compare(MPI_Comm, MPI_Comm, int*);
 MSX_ALIAS(MPI_Win_start) int PMPI_Win_start(MPI_Group, int, MPI_Win);
 MSX_ALIAS(MPI_Win_complete) int PMPI_Win_complete(MPI_Win);
 MSX_ALIAS(MPI_Win_wait) int PMPI_Win_wait(MPI_Win);

@@ -160,6 +160,35 @@ FAPI void mpi_abort_(const MPI_Fint* comm, const MPI_Fint* code, MPI_Fint* ierr)
 FNAMES(abort, ABORT)
 FAPI double mpi_wtime_() { return MPI_Wtime(); }
 FNAMES(wtime, WTIME)
+FAPI double mpi_wtick_() { return MPI_Wtick(); }
+FNAMES(wtick, WTICK)
+FAPI void mpi_query_thread_(MPI_Fint* provided, MPI_Fint* ierr) { *ierr = MPI_Query_thread(provided); }
+FNAMES(query_thread, QUERY_THREAD)
+FAPI void mpi_is_thread_main_(MPI_Fint* flag, MPI_Fint* ierr)
+{
+    int f = 0;
+    *ierr = MPI_Is_thread_main(&f);
+    *flag = to_flog(f);
+}
+FNAMES(is_thread_main, IS_THREAD_MAIN)
+FAPI void mpi_get_version_(MPI_Fint* version, MPI_Fint* subversion, MPI_Fint* ierr)
+{
+    *ierr = MPI_Get_version(version, subversion);
+}
+FNAMES(get_version, GET_VERSION)
+// CHARACTER*(*) name, blank-padded like mpi_error_string_
+FAPI void mpi_get_processor_name_(char* name, MPI_Fint* resultlen, MPI_Fint* ierr, size_t len)
+{
+    char tmp[MPI_MAX_PROCESSOR_NAME] = {0};
+    int n = 0;
+    *ierr = MPI_Get_processor_name(tmp, &n);
+    size_t k = strnlen(tmp, sizeof(tmp));
+    if (k > len) k = len;
+    memcpy(name, tmp, k);
+    if (len > k) memset(name + k, ' ', len - k);
+    *resultlen = n;
+}
+FNAMES(get_processor_name, GET_PROCESSOR_NAME)
 FAPI void mpi_comm_rank_(const MPI_Fint* comm, MPI_Fint* rank, MPI_Fint* ierr) { *ierr = MPI_Comm_rank(*comm, rank); }
 FNAMES(comm_rank, COMM_RANK)
 FAPI void mpi_comm_size_(const MPI_Fint* comm, MPI_Fint* size, MPI_Fint* ierr) { *ierr = MPI_Comm_size(*comm, size); }
@@ -179,6 +208,23 @@ FNAMES(comm_free, COMM_FREE)
 // groups (api/mpi_group.cpp): ranks are ranks, not Fortran indices
 FAPI void mpi_comm_group_(const MPI_Fint* comm, MPI_Fint* group, MPI_Fint* ierr) { *ierr = MPI_Comm_group(*comm, group); }
 FNAMES(comm_group, COMM_GROUP)
+FAPI void mpi_comm_create_(const MPI_Fint* comm, const MPI_Fint* group, MPI_Fint* newcomm, MPI_Fint* ierr)
+{
+    *ierr = MPI_Comm_create(*comm, *group, newcomm);
+}
+FNAMES(comm_create, COMM_CREATE)
+FAPI void mpi_comm_compare_(const MPI_Fint* a, const MPI_Fint* b, MPI_Fint* result, MPI_Fint* ierr)
+{
+    *ierr = MPI_Comm_compare(*a, *b, result);
+}
+FNAMES(comm_compare, COMM_COMPARE)
+FAPI void mpi_comm_test_inter_(const MPI_Fint* comm, MPI_Fint* flag, MPI_Fint* ierr)
+{
+    int f = 0;
+    *ierr = MPI_Comm_test_inter(*comm, &f);
+    *flag = to_flog(f);
+}
+FNAMES(comm_test_inter, COMM_TEST_INTER)
 FAPI void mpi_group_size_(const MPI_Fint* group, MPI_Fint* size, MPI_Fint* ierr) { *ierr = MPI_Group_size(*group, size); }
 FNAMES(group_size, GROUP_SIZE)
 FAPI void mpi_group_rank_(const MPI_Fint* group, MPI_Fint* rank, MPI_Fint* ierr) { *ierr = MPI_Group_rank(*group, rank); }

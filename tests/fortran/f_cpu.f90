@@ -27,6 +27,8 @@ program fcpu
   logical flag, comm
   integer wg, g1, g2, g3, ranges(3, 2), tin(2), tout(2), gres, win
   integer(kind=MPI_ADDRESS_KIND) wsize
+  integer ver, subver, newc
+  character(len=MPI_MAX_PROCESSOR_NAME) pname
   double precision t
   character(len=600) msg
   integer seen_len, seen_type
@@ -178,6 +180,20 @@ program fcpu
   call MPI_GROUP_SIZE(g3, sz, ierr)
   print '(A,I0)', 'DIFFERENCE ', sz
   call MPI_GROUP_FREE(g3, ierr)
+
+  ! environment queries, communicator relations
+  call MPI_GET_VERSION(ver, subver, ierr)
+  call MPI_QUERY_THREAD(i, ierr)
+  call MPI_IS_THREAD_MAIN(flag, ierr)
+  print '(A,I0,1X,I0,1X,I0,1X,L1)', 'VERSION ', ver, subver, i, flag
+  call MPI_GET_PROCESSOR_NAME(pname, rlen, ierr)
+  print '(A,I0,1X,L1,1X,L1)', 'PROCNAME ', ierr, rlen > 0, len_trim(pname) == rlen
+  print '(A,L1)', 'WTICK ', MPI_WTICK() > 0.0d0
+  call MPI_COMM_CREATE(MPI_COMM_WORLD, wg, newc, ierr)
+  call MPI_COMM_COMPARE(MPI_COMM_WORLD, newc, gres, ierr)
+  call MPI_COMM_TEST_INTER(newc, flag, ierr)
+  print '(A,I0,1X,L1,1X,L1)', 'COMM_CREATE ', ierr, gres == MPI_CONGRUENT, flag
+  call MPI_COMM_FREE(newc, ierr)
 
   ! post-start-complete-wait on a one-rank window (no transfers)
   wsize = 40

@@ -323,6 +323,54 @@ def test_pscw_synchronisation_state(msxlib):
     assert L.MPI_Win_free(ctypes.byref(win)) == 0
 
 
+def test_environment_queries_and_communicator_relations(msxlib):
+    """MPI_Get_version (2.0, mpi.h:4070), MPI_Query_thread / MPI_Is_thread_main /
+    MPI_Get_processor_name / MPI_Wtick (api/mpi_env.cpp), MPI_Comm_compare
+    (api/mpi_comm.cpp:51-157), MPI_Comm_test_inter and MPI_Comm_create
+    (api/mpi_comm.cpp:184-248) on one rank; no GPU needed."""
+    L = msxlib
+    v, sv = ctypes.c_int(), ctypes.c_int()
+    assert L.MPI_Get_version(ctypes.byref(v), ctypes.byref(sv)) == 0 and (v.value, sv.value) == (2, 0)
+    assert L.MPI_Get_version(None, ctypes.byref(sv)) == C.MPI_ERR_ARG
+    lvl, flag = ctypes.c_int(-1), ctypes.c_int(-1)
+    assert L.MPI_Query_thread(ctypes.byref(lvl)) == 0 and lvl.value in (C.MPI_THREAD_SINGLE, C.MPI_THREAD_MULTIPLE)
+    assert L.MPI_Is_thread_main(ctypes.byref(flag)) == 0 and flag.value == 1
+    import threading
+    other = []
+    th = threading.Thread(target=lambda: other.append((L.MPI_Is_thread_main(ctypes.byref(flag)), flag.value)))
+    th.start(); th.join()
+    assert other == [(0, 0)]
+    name, n = ctypes.create_string_buffer(C.MPI_MAX_PROCESSOR_NAME), ctypes.c_int()
+    assert L.MPI_Get_processor_name(name, ctypes.byref(n)) == 0
+    import socket
+    assert name.value.decode() == socket.gethostname()[:127] and n.value == len(name.value)
+    L.MPI_Wtick.restype = ctypes.c_double
+    assert 0 < L.MPI_Wtick() <= 1e-6
+    res = ctypes.c_int(-1)
+    W, S = C.MPI_COMM_WORLD, C.MPI_COMM_SELF
+    assert L.MPI_Comm_compare(W, W, ctypes.byref(res)) == 0 and res.value == C.MPI_IDENT
+    d = ctypes.c_int()
+    assert L.MPI_Comm_dup(W, ctypes.byref(d)) == 0
+    assert L.MPI_Comm_compare(W, d.value, ctypes.byref(res)) == 0 and res.value == C.MPI_CONGRUENT
+    assert L.MPI_Comm_compare(W, S, ctypes.byref(res)) == 0 and res.value == C.MPI_CONGRUENT
+    assert L.MPI_Comm_compare(W, C.MPI_COMM_NULL, ctypes.byref(res)) == C.MPI_ERR_COMM
+    assert L.MPI_Comm_compare(W, W, None) == C.MPI_ERR_ARG
+    assert L.MPI_Comm_test_inter(W, ctypes.byref(flag)) == 0 and flag.value == 0
+    wg, nc = ctypes.c_int(), ctypes.c_int()
+    assert L.MPI_Comm_group(W, ctypes.byref(wg)) == 0
+    assert L.MPI_Comm_create(d.value, wg.value, ctypes.byref(nc)) == 0 and nc.value != C.MPI_COMM_NULL
+    sz, rk = ctypes.c_int(), ctypes.c_int()
+    L.MPI_Comm_size(nc.value, ctypes.byref(sz)); L.MPI_Comm_rank(nc.value, ctypes.byref(rk))
+    assert (sz.value, rk.value) == (1, 0)
+    assert L.MPI_Comm_compare(nc.value, W, ctypes.byref(res)) == 0 and res.value == C.MPI_CONGRUENT
+    assert L.MPI_Comm_free(ctypes.byref(nc)) == 0
+    assert L.MPI_Comm_create(W, C.MPI_GROUP_EMPTY, ctypes.byref(nc)) == 0 and nc.value == C.MPI_COMM_NULL
+    assert L.MPI_Comm_create(W, C.MPI_GROUP_NULL, ctypes.byref(nc)) == C.MPI_ERR_GROUP
+    assert L.MPI_Comm_create(C.MPI_COMM_NULL, wg.value, ctypes.byref(nc)) == C.MPI_ERR_COMM
+    assert L.MPI_Group_free(ctypes.byref(wg)) == 0
+    assert L.MPI_Comm_free(ctypes.byref(d)) == 0
+
+
 def _build_c_demo(tmp_path):
     exe = str(tmp_path / "reduce_local_demo")
     libdir = os.path.join(msx.REPO_ROOT, "microsoft-mpi_amd", "lib")

@@ -538,7 +538,24 @@ ex = ctypes.c_int(C.MPI_GROUP_EMPTY)
 assert L.MPI_Group_free(ctypes.byref(ex)) == 0 and ex.value == C.MPI_GROUP_NULL
 e0 = G(); assert L.MPI_Group_excl(wg.value, 0, None, ctypes.byref(e0)) == 0
 print("M", rank, json.dumps([members(g.value) for g in (inc, exc, rinc, rexc, un, it, df, sg)]), flush=True)
-print("G", rank, json.dumps([gr.value, cmp, list(tr_out), errs]), flush=True)
+# MPI_Comm_create: members of incl(4, 1, 3) get a communicator ranked in group
+# order, the others MPI_COMM_NULL; a group reaching outside the communicator
+# (WORLD's group on the parity sub-communicator) is MPI_ERR_GROUP on its members
+cc = ctypes.c_int()
+assert L.MPI_Comm_create(C.MPI_COMM_WORLD, inc.value, ctypes.byref(cc)) == 0
+created = None
+if cc.value != C.MPI_COMM_NULL:
+    cr, cs, cg = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    L.MPI_Comm_rank(cc.value, ctypes.byref(cr)); L.MPI_Comm_size(cc.value, ctypes.byref(cs))
+    assert L.MPI_Comm_group(cc.value, ctypes.byref(cg)) == 0
+    rel = ctypes.c_int()
+    assert L.MPI_Comm_compare(cc.value, C.MPI_COMM_WORLD, ctypes.byref(rel)) == 0
+    created = [cr.value, cs.value, members(cg.value), rel.value]
+    assert L.MPI_Group_free(ctypes.byref(cg)) == 0
+    assert L.MPI_Comm_free(ctypes.byref(cc)) == 0
+bad = ctypes.c_int()
+create_err = L.MPI_Comm_create(sub.value, wg.value, ctypes.byref(bad))
+print("G", rank, json.dumps([gr.value, cmp, list(tr_out), errs, created, create_err]), flush=True)
 for g in (inc, exc, rinc, rexc, un, it, df, rv, sg, wg):
     assert L.MPI_Group_free(ctypes.byref(g)) == 0 and g.value == C.MPI_GROUP_NULL
 assert L.MPI_Finalize() == 0
@@ -559,7 +576,10 @@ def test_groups_five_processes():
         assert rc == 0, e[-3000:]
         f = [l for l in o.splitlines() if l.startswith("G ")][0].split(" ", 2)
         rank = int(f[1])
-        gr, cmp, tr, errs = json.loads(f[2])
+        gr, cmp, tr, errs, created, create_err = json.loads(f[2])
+        assert created == ({4: [0, 3, [4, 1, 3], C.MPI_UNEQUAL], 1: [1, 3, [4, 1, 3], C.MPI_UNEQUAL],
+                            3: [2, 3, [4, 1, 3], C.MPI_UNEQUAL]}.get(rank)), (rank, created)
+        assert create_err == C.MPI_ERR_GROUP
         # incl(4,1,3): rank of world 4 -> 0, 1 -> 1, 3 -> 2, others undefined
         assert gr == {4: 0, 1: 1, 3: 2}.get(rank, U), (rank, gr)
         # compare: world/world IDENT, inc/inc IDENT, union(inc, rinc) = 4,1,3,2,0 vs world SIMILAR,

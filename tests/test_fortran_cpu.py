@@ -35,6 +35,8 @@ ENTRIES = [
     "comm_group", "group_size", "group_rank", "group_incl", "group_excl", "group_range_incl",
     "group_range_excl", "group_union", "group_intersection", "group_difference", "group_translate_ranks",
     "group_compare", "group_free",
+    "wtick", "query_thread", "is_thread_main", "get_version", "get_processor_name", "comm_create",
+    "comm_compare", "comm_test_inter",
     "win_post", "win_start", "win_complete", "win_wait", "win_test", "win_get_group",
     "type_size", "type_size_x", "type_contiguous", "type_vector", "type_hvector", "type_create_hvector",
     "type_indexed", "type_hindexed", "type_create_hindexed", "type_create_indexed_block",
@@ -164,6 +166,10 @@ def test_fortran_program_without_gpu():
     assert out["UNION_IDENT"] == ["T"]
     assert out["INTERSECTION_EMPTY"] == ["T"]
     assert as_int("DIFFERENCE") == [0]
+    assert out["VERSION"] == ["2", "0", str(C.MPI_THREAD_SINGLE), "T"]
+    assert out["PROCNAME"] == ["0", "T", "T"]
+    assert out["WTICK"] == ["T"]
+    assert out["COMM_CREATE"] == ["0", "T", "F"]
     assert out["PSCW"] == ["0", "T", "T"]
     assert as_int("COMPLETE_CLASS") == [C.MPI_ERR_RMA_SYNC]
     assert out["GROUP_FREE"] == ["0", "T"]
