@@ -1,4 +1,5 @@
-"""GPU: reductions on derived communicators (MPI_Comm_split / MPI_Comm_dup),
+"""GPU: reductions on derived communicators (MPI_Comm_split / MPI_Comm_dup /
+MPI_Comm_create),
 4 and 5 ranks sharing one GPU.  Each group runs the engine on its own
 transport (hub, shared-memory barrier, IPC windows, arrival flags), so
 collectives on WORLD and on the groups interleave freely.  Integer data:
@@ -80,6 +81,31 @@ res = dev(np.zeros(n, np.int32))
 ok(L.MPI_Iallreduce(send.data_ptr(), res.data_ptr(), n, C.MPI_INT, C.MPI_SUM, S, ctypes.byref(req)), "sub iallreduce")
 ok(L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)), "wait")
 if not np.array_equal(host(res), tot): fails.append("sub iallreduce")
+
+# MPI_Comm_create from a group in reversed world order without world rank 1:
+# the new ranks follow the group, so a scan accumulates in that order
+wg, rg, cc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+L.MPI_Comm_group(C.MPI_COMM_WORLD, ctypes.byref(wg))
+order = [r for r in reversed(range(p)) if r != 1 or p == 1]
+ok(L.MPI_Group_incl(wg.value, len(order), (ctypes.c_int * len(order))(*order), ctypes.byref(rg)), "incl")
+ok(L.MPI_Comm_create(C.MPI_COMM_WORLD, rg.value, ctypes.byref(cc)), "comm_create")
+if rank in order:
+    k = order.index(rank)
+    cr = ctypes.c_int(); L.MPI_Comm_rank(cc.value, ctypes.byref(cr))
+    if cr.value != k: fails.append(f"created rank {cr.value} != {k}")
+    n = 1 << 16
+    x = lambda r: ((np.arange(n, dtype=np.int64) * 5 + r * 17) % 1009).astype(np.int32)
+    send = dev(x(rank)); out = dev(np.zeros(n, np.int32))
+    ok(L.MPI_Scan(send.data_ptr(), out.data_ptr(), n, C.MPI_INT, C.MPI_SUM, cc.value), "scan created")
+    if not np.array_equal(host(out), sum(x(r).astype(np.int64) for r in order[:k + 1]).astype(np.int32)):
+        fails.append("scan on the created communicator")
+    ok(L.MPI_Allreduce(send.data_ptr(), out.data_ptr(), n, C.MPI_INT, C.MPI_SUM, cc.value), "allreduce created")
+    if not np.array_equal(host(out), sum(x(r).astype(np.int64) for r in order).astype(np.int32)):
+        fails.append("allreduce on the created communicator")
+    ok(L.MPI_Comm_free(ctypes.byref(cc)), "free created")
+elif cc.value != C.MPI_COMM_NULL:
+    fails.append("non-member got a communicator")
+L.MPI_Group_free(ctypes.byref(rg)); L.MPI_Group_free(ctypes.byref(wg))
 
 ok(L.MPI_Comm_free(ctypes.byref(sub)), "free sub")
 ok(L.MPI_Comm_free(ctypes.byref(dup)), "free dup")
