@@ -7,6 +7,17 @@
 
 namespace msx {
 
+// Completion counters of the engine's flag-posting kernels: a transport owns
+// kCountBlocks blocks of kCountWords zeroed words (push_counter()): block 0
+// word 0 counts k_push_post / the fused push; block 1 is k_push_wait's bulk
+// push, block 2 the two-step tree's result count.  Inside a block, word 0 is
+// the top level, word 1 a launch count, and kCountSubs sub-counters sit 16
+// words (64 B) apart from kCountSubBase (see count_done).
+constexpr unsigned kCountSubs = 32;
+constexpr unsigned kCountSubBase = 64;
+constexpr unsigned kCountWords = 1024;
+constexpr unsigned kCountBlocks = 4;
+
 // Launch geometry of the streaming combine.
 struct LaunchCfg {
     int variant = 0;      // fp32-SUM tuning variant (0 = default); other pairs ignore it
@@ -68,6 +79,15 @@ struct TreeSpec {
     unsigned long long push_seq = 0;
     unsigned* push_counter = nullptr;
     bool push_sys = false;
+    // Result-ready flags: when the tree workgroups of all `done_launches`
+    // launches of one call (this one included; stream-ordered) have stored
+    // their results, store done_seq to every done_flags[j] (system scope).
+    // done_counter: a zeroed kCountWords block of the transport, left zero again.
+    unsigned* done_counter = nullptr;
+    unsigned done_launches = 1;
+    int done_nflags = 0;
+    unsigned long long* done_flags[64] = {};
+    unsigned long long done_seq = 0;
 };
 hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t count,
                             hipStream_t s);
@@ -84,6 +104,15 @@ hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned lon
 hipError_t launch_push_post(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
                             unsigned* counter, hipStream_t s);
+
+// launch_push_post's push and flags (nseg may be 0: wait only), plus ONE
+// workgroup that waits until wait_flags[r] >= seq for r < wait_n, r !=
+// wait_skip (~20 s bound, then 1 -> *wait_err).  Launches after it on `s`
+// read what the flags announce.
+hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
+                            unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
+                            unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,
+                            int* wait_err, hipStream_t s);
 
 // Copy nseg independent byte ranges in one launch (one grid row per segment),
 // used to pull allgather blocks from every peer concurrently.

@@ -246,6 +246,19 @@ struct PostFlags {
     int n;
 };
 
+// "This lane's stores have completed" without a cache maintenance operation:
+// s_waitcnt vmcnt(0) (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  An
+// agent-scope release fence would do the same wait but also write back the
+// whole XCD L2 (buffer_wbl2), once per workgroup -- on this multi-XCD part
+// that made a 2048-workgroup push 20x slower.  Window memory is uncached
+// (MTYPE_UC), so a completed store is at the owner; nothing sits in L2.
+__device__ __forceinline__ void stores_done()
+{
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);      // no compiler motion of stores past the wait
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // The small-allreduce push (k_push_post, and the first workgroups of a fused
 // k_tree launch): see the comment at k_push_post.
 __device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
@@ -274,16 +287,74 @@ __device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlag
         plain = true;
     }
     if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
-    else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // vmcnt(0): this lane's stores completed
+    else stores_done();                                 // vmcnt(0): this lane's stores completed
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == total - 1) {
             if (sys) __threadfence_system();
             for (int k = 0; k < f.n; ++k)
                 __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
         }
+    }
+}
+
+// Count finished workgroup b of nb; true in exactly one workgroup, after all
+// nb have counted.  Thousands of workgroups adding to ONE word serialise
+// (a 4096-workgroup tree took 70 us instead of 38), so workgroup b counts on
+// sub-counter b % kCountSubs (its own 64-byte line, base[kCountSubBase +
+// 16 i]) and only the last of each sub-counter counts on base[0].  Relaxed:
+// each add is issued after the workgroup's stores completed (stores_done),
+// so when the last add is seen, all of them have.  Words are left zero.
+__device__ __forceinline__ bool count_done(unsigned* base, unsigned b, unsigned nb)
+{
+    const unsigned i = b % kCountSubs;
+    const unsigned nsub = nb < kCountSubs ? nb : kCountSubs;
+    const unsigned want = (nb - i + kCountSubs - 1) / kCountSubs;   // workgroups on sub-counter i
+    unsigned* c = base + kCountSubBase + 16 * i;
+    if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want - 1) return false;
+    __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(base, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nsub - 1) return false;
+    __hip_atomic_store(base, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// Bulk variant for multi-MiB segments (the two-step allreduce's pieces): plain
+// 16-byte stores from a full grid, four loads in flight per lane (as
+// k_copy_segs), then push_post_body's fenced count and flag post.  Plain
+// stores to peer windows rely on the windows' uncached mapping like every
+// other bulk transfer of the engine; `sys` (cached windows) writes the L2
+// back at system scope before counting.
+__device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
+                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
+{
+    const char* src = static_cast<const char*>(c.src[sg]);
+    char* dst = static_cast<char*>(c.dst[sg]);
+    const size_t nb = c.nbytes[sg];
+    const size_t stride = (size_t)gx * 256;
+    size_t done = 0;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const size_t nv = nb / 16;
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+        u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+        size_t i = (size_t)bx * 256 + threadIdx.x;
+        for (; i + 3 * stride < nv; i += 4 * stride) {
+            const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
+            d4[i] = a0; d4[i + stride] = a1; d4[i + 2 * stride] = a2; d4[i + 3 * stride] = a3;
+        }
+        for (; i < nv; i += stride) d4[i] = s4[i];
+        done = nv * 16;
+    }
+    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
+    if (sys) __threadfence_system();
+    else stores_done();
+    __syncthreads();
+    // counter: a kCountWords block (count_done); b = this workgroup's index
+    if (threadIdx.x == 0 && count_done(counter, (unsigned)sg + bx * (unsigned)c.n, total)) {
+        if (sys) __threadfence_system();
+        for (int k = 0; k < f.n; ++k)
+            __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -322,24 +393,54 @@ struct TreeArgs {
     unsigned* push_counter;
     CopySegs push;
     PostFlags flags;
+    // result-ready flags (barrier-free two-step allreduce): once every tree
+    // workgroup of all `done_launches` launches has stored its results, post
+    // done_flags (see tree_done)
+    unsigned* done_counter;       // kCountWords block: [0] count_done, [1] launches done
+    unsigned done_launches;
+    PostFlags done_flags;
 };
+
+// End of a tree workgroup when the launch posts result-ready flags: the
+// threadFenceReduction pattern of push_post_body, extended over the launches
+// that together evaluate one call (stream-ordered, so at most one is in
+// flight).  Every lane waits for its own stores (stores_done; cached windows:
+// system fence), thread 0 counts the workgroup, the launch's last workgroup
+// counts the launch, and the last workgroup of the last launch posts the
+// flags with system-scope release stores.  Both words are left zero for the
+// next call.
+__device__ __forceinline__ void tree_done(const TreeArgs& a, unsigned b, unsigned nb)
+{
+    if (a.sys) __threadfence_system();
+    else stores_done();
+    __syncthreads();
+    if (threadIdx.x != 0 || !count_done(a.done_counter, b, nb)) return;
+    // launches of the call: word 1 of the block
+    const unsigned l = __hip_atomic_fetch_add(a.done_counter + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l != a.done_launches - 1) return;
+    __hip_atomic_store(a.done_counter + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.sys) __threadfence_system();
+    for (int k = 0; k < a.done_flags.n; ++k)
+        __hip_atomic_store(a.done_flags.dst[k], a.done_flags.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Arrival wait of the barrier-free small allreduce: thread 0 of every
 // workgroup polls the peers' flags (uncached window memory, system-scope
 // loads) until each reaches the call's sequence number.  Bounded: after
 // ~20 s (s_memrealtime runs at 100 MHz) it reports through *wait_err and the
 // workgroup exits, so a missing peer can never leave a wave running.
-__device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
+__device__ __forceinline__ bool wait_flags_body(const unsigned long long* flags, unsigned long long seq, int n,
+                                                int skip, int* err)
 {
     __shared__ int ok;
     if (threadIdx.x == 0) {
         int good = 1;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        for (int r = 0; r < a.wait_n && good; ++r) {
-            if (r == a.wait_skip) continue;
-            while (__hip_atomic_load(a.wait_flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.wait_seq) {
+        for (int r = 0; r < n && good; ++r) {
+            if (r == skip) continue;
+            while (__hip_atomic_load(flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
-                    __hip_atomic_store(a.wait_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     good = 0;
                     break;
                 }
@@ -351,11 +452,16 @@ __device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
         // lines, so the IN half is read fresh whatever cache type the window
         // is mapped with (the UC mapping makes it a no-op for the data today,
         // but the kernel no longer depends on that allocation property).
-        if (good) (void)__hip_atomic_load(a.wait_flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (good) (void)__hip_atomic_load(flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         ok = good;
     }
     __syncthreads();
     return ok != 0;
+}
+
+__device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
+{
+    return wait_flags_body(a.wait_flags, a.wait_seq, a.wait_n, a.wait_skip, a.wait_err);
 }
 
 // Start-of-kernel system acquire: invalidate this CU's L1 and the XCD's L2
@@ -494,6 +600,7 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
         for (int e = 0; e < a.nextra; ++e) static_cast<T*>(a.extra[e])[first + s] = r;
     }
     if (a.sys) release_system();
+    if (a.done_counter) tree_done(a, b, nb);
 }
 
 // ---- multi-segment copy (allgather phase: blocks pulled from peers) -------------
@@ -538,12 +645,12 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
 // workgroup copies its part of its segment with system-coherent stores
 // (sc0 sc1: written through to the owner's memory, never left dirty in this
 // GPU's L2, however the importer maps the peer window).  EVERY lane then
-// fences (agent-scope release: s_waitcnt vmcnt(0), so its own write-through
-// stores have completed at the owner), the workgroup meets at a barrier, and
-// thread 0 counts the workgroup done with an acq_rel add; the last one
-// acquires all the others' completions and posts `seq` into every peer's flag
-// slot with a system-scope release (the threadFenceReduction pattern: no flag
-// can overtake any workgroup's data).  sys: cached windows, each lane writes
+// waits until its own write-through stores have completed at the owner
+// (stores_done: s_waitcnt vmcnt(0), without the L2 writeback an agent-scope
+// fence adds), the workgroup meets at a barrier, and thread 0 counts the
+// workgroup done; the last one posts `seq` into every peer's flag slot with a
+// system-scope release (the threadFenceReduction pattern: every workgroup's
+// data completed before its count, so no flag can overtake any of it).  sys: cached windows, each lane writes
 // its L2 back at system scope instead.
 // `counter` belongs to the calling transport (one per communicator, reset by
 // the last workgroup); the transport's collectives are issued one at a time
@@ -552,6 +659,23 @@ __global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsi
                                                    int sys)
 {
     push_post_body(c, f, counter, total, sys, blockIdx.x, gridDim.x, blockIdx.y);
+}
+
+// The two-step allreduce's synchronisation points: workgroups [0, total) push
+// (copy_post_body, segment b % n), the last workgroup alone waits for the
+// peers' flags -- one spinning workgroup per rank, so ranks that share a GPU
+// never starve each other's pushes -- and the stream's next launches read
+// what the flags announce.
+__global__ __launch_bounds__(256) void k_push_wait(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
+                                                   int sys, unsigned gx, const unsigned long long* wflags,
+                                                   unsigned long long wseq, int wn, int wskip, int* werr)
+{
+    const unsigned b = blockIdx.x;
+    if (b < total) {
+        copy_post_body(c, f, counter, total, sys, b / (unsigned)c.n, gx, (int)(b % (unsigned)c.n));
+        return;
+    }
+    (void)wait_flags_body(wflags, wseq, wn, wskip, werr);
 }
 
 }  // namespace dev
@@ -917,7 +1041,16 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         a.push_counter = t.push_counter;
         a.push_sys = t.push_sys ? 1 : 0;
     }
-    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.wait_flags && !t.push_nseg) {
+    if (t.done_counter) {
+        if (t.done_nflags < 0 || t.done_nflags > 64 || t.done_launches < 1) return hipErrorInvalidValue;
+        a.done_counter = t.done_counter;
+        a.done_launches = t.done_launches;
+        a.done_flags.n = t.done_nflags;
+        a.done_flags.seq = t.done_seq;
+        for (int i = 0; i < t.done_nflags; ++i) a.done_flags.dst[i] = t.done_flags[i];
+    }
+    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.wait_flags && !t.push_nseg &&
+        !t.done_counter) {
         if (t.src[0] == out) return hipSuccess;
         return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
     }
@@ -988,6 +1121,38 @@ hipError_t launch_push_post(const void* const* src, void* const* dst, const size
     if (gx > 16) gx = 16;
     hipLaunchKernelGGL(k_push_post, dim3((unsigned)gx, (unsigned)nseg), dim3(256), 0, s, c, f, counter,
                        (unsigned)(gx * (size_t)nseg), sys ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
+                            unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
+                            unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,
+                            int* wait_err, hipStream_t s)
+{
+    if (nseg < 0 || nseg > kMaxSegs || nflags < 0 || nflags > 64 || !wait_flags || !wait_err ||
+        (nseg > 0 && !counter))
+        return hipErrorInvalidValue;
+    CopySegs c{};
+    PostFlags f{};
+    size_t maxb = 0;
+    c.n = nseg > 0 ? nseg : 1;
+    for (int i = 0; i < nseg; ++i) {
+        c.src[i] = src[i];
+        c.dst[i] = dst[i];
+        c.nbytes[i] = nbytes[i];
+        if (nbytes[i] > maxb) maxb = nbytes[i];
+    }
+    f.n = nflags;
+    f.seq = seq;
+    for (int i = 0; i < nflags; ++i) f.dst[i] = flags[i];
+    // four 16-byte granules per lane and pass; at most ~2048 pushing workgroups
+    size_t gx = (maxb / 16 + 1023) / 1024;
+    const size_t cap = nseg > 0 ? std::max<size_t>(1, 2048 / (size_t)nseg) : 1;
+    if (gx < 1) gx = 1;
+    if (gx > cap) gx = cap;
+    const unsigned total = nseg > 0 ? (unsigned)(gx * (size_t)nseg) : 0u;
+    hipLaunchKernelGGL(k_push_wait, dim3(total + 1), dim3(256), 0, s, c, f, counter, total, sys ? 1 : 0,
+                       (unsigned)gx, wait_flags, seq, wait_n, wait_skip, wait_err);
     return hipGetLastError();
 }
 

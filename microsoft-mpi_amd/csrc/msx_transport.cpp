@@ -358,9 +358,11 @@ public:
     unsigned* push_counter() override
     {
         if (!counter_) {
+            // kCountBlocks blocks of kCountWords (msx_kernels.h)
             void* c = nullptr;
-            if (hipMalloc(&c, sizeof(unsigned)) != hipSuccess) return nullptr;
-            if (hipMemset(c, 0, sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            const size_t bytes = (size_t)kCountBlocks * kCountWords * sizeof(unsigned);
+            if (hipMalloc(&c, bytes) != hipSuccess) return nullptr;
+            if (hipMemset(c, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                 (void)hipFree(c);
                 return nullptr;
             }
@@ -860,6 +862,12 @@ struct TreeWait {
     const std::vector<size_t>* push_n = nullptr;
     const std::vector<unsigned long long*>* push_flags = nullptr;
     unsigned* push_counter = nullptr;
+    // result-ready flags after the last of `done_launches` launches
+    // (TreeSpec::done_*); done_counter: block 2 of push_counter()
+    unsigned* done_counter = nullptr;
+    unsigned done_launches = 1;
+    const std::vector<unsigned long long*>* done_flags = nullptr;
+    unsigned long long done_seq = 0;
 };
 
 int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>& srcs, size_t esz,
@@ -888,6 +896,15 @@ int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>
             spec.push_seq = wait->seq;
             spec.push_counter = wait->push_counter;
             spec.push_sys = sys_fences();
+        }
+        if (wait->done_counter) {
+            const size_t nf = wait->done_flags ? wait->done_flags->size() : 0;
+            if (nf > 64) { set_error("result flags: too many peers"); return MPI_ERR_INTERN; }
+            spec.done_counter = wait->done_counter;
+            spec.done_launches = wait->done_launches;
+            spec.done_nflags = (int)nf;
+            for (size_t i = 0; i < nf; ++i) spec.done_flags[i] = (*wait->done_flags)[i];
+            spec.done_seq = wait->done_seq;
         }
     }
     if (extra_outs.size() > 31) { set_error("tree combine: too many destinations"); return MPI_ERR_INTERN; }
@@ -1149,6 +1166,27 @@ struct Windows {
     }
 };
 
+// Result-ready flags of the two-step allreduce live in the upper half of the
+// flag area: slot kResultFlags + k of window r = the last call whose result
+// rank k stored into r's OUT area.
+constexpr size_t kResultFlags = 4096;
+
+// Largest message (bytes) of the barrier-free two-step allreduce / reduce
+// (MSX_TWO_STEP_MAX; 0 = always the host-barrier schedule).  The default
+// takes it whenever the message fits the window halves: 2 ranks on one
+// MI355X (scripts/allreduce_probe.sh, profiles/r02/two_step_*) measured
+// 1 MiB 62.6 -> 28.5 us, 4 MiB 64.3 -> 32.5, 16 MiB 75.6 -> 45.8,
+// 64 MiB 154.8 -> 133.0, 128 MiB 265 -> 249; 4 ranks 64 MiB 310 -> 254.
+size_t two_step_max()
+{
+    static const size_t v = [] {
+        size_t b = (size_t)256 << 20;
+        if (const char* e = getenv("MSX_TWO_STEP_MAX")) b = (size_t)atoll(e);
+        return b;
+    }();
+    return v;
+}
+
 // Pinned bounce buffers of the engine (engine worker, or the one inline
 // blocking call): 0 = this rank's contribution, 1 = the result.
 Bounce& engine_bounce(int i)
@@ -1209,6 +1247,7 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
         rc = tp->barrier();
         tp->window_open = false;
     }
+    if (!rd_single) tp->out_quiet = false;      // a host-barrier user of the OUT areas
     return rc;
 }
 
@@ -1586,8 +1625,17 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
     const bool rd_single = (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) &&
                            count * esz <= (Qh & ~(size_t)(16 * esz - 1));
+    // Rabenseifner in two GPU-synchronised steps (see below) when one chunk
+    // holds the message in half a sub-slot per piece and half the OUT area
+    // above the recursive-doubling results: only count, type, p and the
+    // environment decide, so every rank takes the same branch
+    const size_t qh_el = (Qh / esz) & ~(size_t)15;
+    const size_t piece_el = (((count + (size_t)p - 1) / (size_t)p) + 15) & ~(size_t)15;
+    const size_t out_half = ((chunk_bytes() - Qh) / 2) & ~(size_t)255;
+    const bool two_step = algo == A_RABENSEIFNER && p >= 2 && p <= 32 && rd_flags() && tp->has_done() &&
+                          count * esz <= two_step_max() && piece_el <= qh_el && count * esz <= out_half;
     Windows w;
-    if ((rc = get_windows(tp, &w, rd_single)) != MPI_SUCCESS) return rc;
+    if ((rc = get_windows(tp, &w, rd_single || two_step)) != MPI_SUCCESS) return rc;
     // host buffers: device aliases for the call (pinned in place of staging)
     BufInfo bs = classify(src), bd = classify(dst);
     PinHold pins;
@@ -1752,6 +1800,114 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             if (rc == MPI_SUCCESS) rc = tp->barrier();                              // B
         }
         trace("allreduce: done rc=%d", rc);
+        return rc;
+    }
+
+    if (two_step) {
+        // Barrier-free Rabenseifner: the same pieces, trees and result
+        // placement as the host-barrier schedule below, synchronised on the
+        // GPU.  Step 1: push piece r of my vector into rank r's IN half and
+        // post its arrival flag, while one workgroup waits for every peer's
+        // piece of mine (k_push_wait); then evaluate my piece (one launch per
+        // owner tree) into the OUT areas of all receivers, the last workgroup
+        // posting result-ready flags to them (tree_done).  Step 2
+        // (receivers): one workgroup waits for every peer's result flag, then
+        // the OUT half is copied into recvbuf.  One host sync.  Only single
+        // workgroups spin, so ranks sharing a GPU cannot starve each other.
+        // Halves alternate with rd_parity and are reused two flag calls later,
+        // guarded by wait_done as in the recursive-doubling path.
+        if (!tp->out_quiet && (rc = tp->barrier()) != MPI_SUCCESS) return rc;
+        const size_t half = (size_t)tp->rd_parity * Qh;
+        const size_t obase = Qh + (size_t)tp->rd_parity * out_half;
+        const size_t len = count;
+        auto lo_of = [&](int r) { return std::min(len, (size_t)r * piece_el); };
+        auto hi_of = [&](int r) { return std::min(len, (size_t)(r + 1) * piece_el); };
+        const char* mine = nullptr;
+        rc = device_view(bs, src, 0, len * esz, stage, s, &mine);
+        const unsigned long long seq = ++tp->rd_seq;
+        Segs sg;
+        std::vector<unsigned long long*> fl, done;
+        for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
+            if (r == me) continue;
+            if (seq > 2) rc = tp->wait_done(r, seq - 2);
+            if (hi_of(r) > lo_of(r)) {
+                sg.add(mine + lo_of(r) * esz, w.sub(r, me) + half, (hi_of(r) - lo_of(r)) * esz);
+                fl.push_back(w.flags(r) + me);
+            }
+        }
+        std::vector<int> dests;
+        if (want) dests.push_back(me);
+        for (int r = 0; r < p; ++r)
+            if (r != me && (root < 0 || r == root)) dests.push_back(r);
+        for (int d : dests)
+            if (d != me) done.push_back(w.flags(d) + kResultFlags + me);
+        int* err_host = nullptr;
+        int* err_dev = wait_err_word(&err_host);
+        unsigned* counter = tp->push_counter();
+        if (!err_dev || !counter) { set_error("allreduce: flag word allocation failed"); return MPI_ERR_NO_MEM; }
+        *err_host = 0;
+        // my piece, cut where the owner tree changes (block boundaries)
+        const size_t plo = lo_of(me), phi = hi_of(me);
+        struct Range { size_t e0, e1; int owner; };
+        std::vector<Range> ranges;
+        for (size_t e0 = plo; e0 < phi;) {
+            const size_t rs = count / (size_t)pof2;
+            const int j = rs ? (int)std::min((size_t)pof2 - 1, e0 / rs) : pof2 - 1;
+            size_t bst, bl;
+            allreduce_block(p, count, j, &bst, &bl);
+            const size_t e1 = std::min(phi, bst + bl);
+            ranges.push_back({e0, e1, allreduce_block_owner(p, j)});
+            e0 = e1;
+        }
+        for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
+        subs[(size_t)me] = const_cast<char*>(mine) + plo * esz;
+        // step 1a: push my pieces and their arrival flags; one workgroup waits
+        // for the peers' pieces of mine (none when my piece is empty)
+        if (rc == MPI_SUCCESS) {
+            hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
+                                            fl.data(), (int)fl.size(), seq, sys_fences(), counter + kCountWords,
+                                            w.flags(me),
+                                            ranges.empty() ? 0 : p, me, err_dev, s);
+            if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
+        }
+        // step 1b: my piece into every receiver's OUT half; the last workgroup
+        // of the last launch posts the result flags
+        if (rc == MPI_SUCCESS && ranges.empty() && !done.empty()) {
+            hipError_t e = launch_post_flags(done.data(), (int)done.size(), seq, s);
+            if (e != hipSuccess) rc = hip_fail(e, "allreduce result flags");
+        }
+        for (size_t i = 0; i < ranges.size() && rc == MPI_SUCCESS; ++i) {
+            const Range& g = ranges[i];
+            const RankTree t = is_reduce ? tree_reduce_rsag(p, g.owner) : tree_allreduce(p, g.owner);
+            std::vector<char*> extra;
+            for (size_t d = 1; d < dests.size(); ++d) extra.push_back(w.out(dests[d]) + obase + g.e0 * esz);
+            TreeWait tw;
+            tw.done_counter = counter + 2 * kCountWords;
+            tw.done_launches = (unsigned)ranges.size();
+            tw.done_flags = &done;
+            tw.done_seq = seq;
+            rc = run_rank_tree(op.opidx, k, t, subs, esz, g.e0 - plo, g.e1 - g.e0,
+                               w.out(dests[0]) + obase + g.e0 * esz, s, extra, &tw);
+        }
+        if (rc == MPI_SUCCESS && want) {
+            // step 2: every peer's result in my OUT half, then into recvbuf
+            hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq, false, nullptr,
+                                            w.flags(me) + kResultFlags, p, me, err_dev, s);
+            if (e != hipSuccess) rc = hip_fail(e, "allreduce result wait");
+            char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : dst;
+            if (rc == MPI_SUCCESS) rc = copy_async(out, w.out(me) + obase, len * esz, s);
+        }
+        const int rs = sync_stream(s, "allreduce two-step");
+        if (rc == MPI_SUCCESS) rc = rs;
+        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
+            set_error("allreduce: a peer's piece or result did not arrive within 20 s");
+            rc = MPI_ERR_OTHER;
+        }
+        tp->post_done(seq);
+        tp->rd_parity ^= 1;
+        tp->window_open = true;
+        tp->out_quiet = true;
+        trace("allreduce: done (two-step, GPU flags, seq %llu, %zu ranges) rc=%d", seq, ranges.size(), rc);
         return rc;
     }
 

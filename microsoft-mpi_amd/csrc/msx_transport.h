@@ -35,6 +35,11 @@ public:
     // barrier-free allreduce: sequence number of the last flag-synchronised
     // call (the same on every rank: collectives are called in one order)
     unsigned long long rd_seq = 0;
+    // The barrier-free two-step allreduce writes the peers' OUT areas (upper
+    // halves); a host-barrier collective may still be reading its own OUT
+    // area after its last barrier, so the first two-step call after one
+    // barriers first.  Cleared by every host-barrier window user.
+    bool out_quiet = false;
     // lock-step host collectives over the bootstrap hub (all ranks, same n)
     virtual int allgather(const void* mine, size_t n, void* all) = 0;
     virtual int barrier() = 0;
@@ -49,9 +54,10 @@ public:
     // Per-rank device scratch, IPC-mapped once: out[r] = rank r's window.
     virtual int window(size_t bytes, std::vector<char*>& out) = 0;
     virtual hipStream_t stream() = 0;
-    // Completion counter of the fused push (k_push_post): one zeroed device
-    // word per transport, used only by launches on stream(), which the
-    // transport issues one collective at a time.  nullptr if allocation failed.
+    // Completion counters of the fused push (k_push_post, word 0) and of the
+    // two-step allreduce's result flags (words 1-2): zeroed device words per
+    // transport, used only by launches on stream(), which the transport
+    // issues one collective at a time.  nullptr if allocation failed.
     virtual unsigned* push_counter() = 0;
 };
 

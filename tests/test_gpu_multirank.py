@@ -299,8 +299,8 @@ while rc == 0 and not flag.value:
 if rc: fails.append(f"testall rc={rc} {msx.last_error()}")
 else: check("testall allreduce int", fromdev(ra, xa[rank]), ea[rank])
 
-# Back-to-back stress of the barrier-free small allreduce (GPU arrival flags,
-# alternating IN halves; with MSX_RD_FLAGS=0 the host-barrier variant)
+# Back-to-back stress of the barrier-free allreduce paths (GPU arrival flags,
+# alternating IN / OUT halves; with MSX_RD_FLAGS=0 the host-barrier variants)
 # interleaved with the other window users: small rooted reduces (the same
 # arrival-flag path, non-roots push to the root only), a chunked large
 # allreduce (full barrier first), non-blocking calls through the engine
@@ -309,7 +309,9 @@ def ivec(it, r, n):
     return ((np.arange(n, dtype=np.int64) * 7 + it * 31 + r * 1009) % 100003).astype(np.int32)
 
 for it in range(240):
-    n = (1, 5, 64, 1000, 4096, 65536)[it % 6]
+    # recursive doubling / binomial (GPU flags) up to 64 Ki ints, the two-step
+    # Rabenseifner (GPU flags) or, above MSX_TWO_STEP_MAX, the host-barrier one
+    n = (1, 5, 64, 1000, 4096, 65536, 100003, 300001)[it % 8]
     tot = sum(ivec(it, r, n).astype(np.int64) for r in range(p)).astype(np.int32)
     if it % 50 == 49:                      # large: Rabenseifner path, barriers
         n = 1 << 18
@@ -364,7 +366,8 @@ def _free_port():
                                                         (4, 1 << 20, None, None), (5, None, None, None),
                                                         (3, 65536, "rccl", None), (8, None, None, None),
                                                         (7, 1 << 20, None, None), (3, None, None, "0"),
-                                                        (4, 65536, None, "0"), (3, None, None, "unfused")])
+                                                        (4, 65536, None, "0"), (3, None, None, "unfused"),
+                                                        (4, None, None, "ts512k"), (6, None, None, None)])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -382,6 +385,8 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             env["MSX_TRANSPORT"] = transport
         if rd_flags == "unfused":
             env["MSX_FUSED_PUSH"] = "0"             # flag path with a separate push launch
+        elif rd_flags == "ts512k":
+            env["MSX_TWO_STEP_MAX"] = str(512 << 10)   # two-step and host-barrier Rabenseifner alternate
         elif rd_flags is not None:
             env["MSX_RD_FLAGS"] = rd_flags          # host-barrier small allreduce / reduce
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
