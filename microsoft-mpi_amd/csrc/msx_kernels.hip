@@ -484,8 +484,17 @@ template <class F, class V, class LD>
 __device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
 {
     if (a.chain) {
-        V v = load(0);
-        for (int k = 1; k < a.P; ++k) v = F::apply(v, load(k));
+        // every source loaded before the first combine (the loop bound is a
+        // runtime value: a rolled loop waited for each load in turn, 75 us
+        // instead of 8 us for a 4-rank 1 MiB reduce_scatter); same order
+        V x[kMaxLeaves];
+#pragma unroll
+        for (int k = 0; k < kMaxLeaves; ++k)
+            if (k < a.P) x[k] = load(k);
+        V v = x[0];
+#pragma unroll
+        for (int k = 1; k < kMaxLeaves; ++k)
+            if (k < a.P) v = F::apply(v, x[k]);
         return v;
     }
     // leaves >= nleaves are absent (binomial trees over a non-power-of-two p):

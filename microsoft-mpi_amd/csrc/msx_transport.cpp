@@ -2039,8 +2039,17 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
         if (ncclComm_t rcomm = rccl_comm(tp)) return rccl_reduce_scatter(rcomm, c, sendbuf, recvbuf, recvcounts, dt, op);
     const Kind k = type_info(dt)->kind;
     hipStream_t s = tp->stream();
+    // One GPU-synchronised step when every block fits half an IN sub-slot
+    // (decided by recvcounts, type, p and the environment: the same on every
+    // rank): push block r of my input into rank r's IN half with its arrival
+    // flag while one workgroup waits for the peers' blocks of mine
+    // (k_push_wait), evaluate my block, one host sync.  Halves and reuse as
+    // in the two-step allreduce.
+    const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
+    const bool one_step = p >= 2 && p <= 32 && rd_flags() && tp->has_done() && total * esz <= two_step_max() &&
+                          maxcnt <= ((Qh / esz) & ~(size_t)15);
     Windows w;
-    if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
+    if ((rc = get_windows(tp, &w, one_step)) != MPI_SUCCESS) return rc;
     // sub-slot k of IN(r) receives rank k's contribution to r's block, qe
     // elements per round
     size_t qe = w.Q / esz;
@@ -2058,6 +2067,63 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
     alias_host_operands(pins, true, src, total * esz, &bs, in_place ? nullptr : recvbuf, in_place ? 0 : mycnt * esz,
                         &bd);
     char* dst = static_cast<char*>(recvbuf);
+    if (one_step) {
+        const size_t hold_b = in_place ? ((mycnt * esz + 255) & ~(size_t)255) : 0;
+        const size_t stage_b = bs.place == Place::Device ? 0 : total * esz;
+        char* scratch = nullptr;
+        if (hold_b + stage_b) {
+            scratch = dev_scratch(hold_b + stage_b);
+            if (!scratch) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+        }
+        const size_t half = (size_t)tp->rd_parity * Qh;
+        const unsigned long long seq = ++tp->rd_seq;
+        std::vector<char*> subs((size_t)p);
+        Segs sg;
+        std::vector<unsigned long long*> fl;
+        for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
+            const size_t cnt = (size_t)recvcounts[r];
+            const char* v = nullptr;
+            if (cnt)
+                rc = device_view(bs, src, disp[r] * esz, cnt * esz, scratch ? scratch + hold_b + disp[r] * esz : nullptr,
+                                 s, &v);
+            if (r == me) { subs[(size_t)me] = const_cast<char*>(v); continue; }
+            subs[(size_t)r] = w.sub(me, r) + half;
+            if (rc == MPI_SUCCESS && seq > 2) rc = tp->wait_done(r, seq - 2);
+            if (cnt && rc == MPI_SUCCESS) {
+                sg.add(v, w.sub(r, me) + half, cnt * esz);
+                fl.push_back(w.flags(r) + me);
+            }
+        }
+        int* err_host = nullptr;
+        int* err_dev = wait_err_word(&err_host);
+        unsigned* counter = tp->push_counter();
+        if (!err_dev || !counter) { set_error("reduce_scatter: flag word allocation failed"); return MPI_ERR_NO_MEM; }
+        *err_host = 0;
+        if (rc == MPI_SUCCESS) {
+            hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
+                                            fl.data(), (int)fl.size(), seq, sys_fences(), counter + kCountWords,
+                                            w.flags(me), mycnt ? p : 0, me, err_dev, s);
+            if (e != hipSuccess) rc = hip_fail(e, "reduce_scatter push");
+        }
+        if (rc == MPI_SUCCESS && mycnt) {
+            // in place, recvbuf still holds the input the tree reads: result via hold
+            char* out = in_place ? scratch
+                                 : (bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me));
+            rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, mycnt, out, s);
+            if (rc == MPI_SUCCESS && out != static_cast<char*>(bd.dev)) rc = copy_async(dst, out, mycnt * esz, s);
+        }
+        const int rs = sync_stream(s, "reduce_scatter one-step");
+        if (rc == MPI_SUCCESS) rc = rs;
+        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
+            set_error("reduce_scatter: a peer's block did not arrive within 20 s");
+            rc = MPI_ERR_OTHER;
+        }
+        tp->post_done(seq);
+        tp->rd_parity ^= 1;
+        tp->window_open = true;
+        trace("reduce_scatter: done (one step, GPU flags, seq %llu) rc=%d", seq, rc);
+        return rc;
+    }
     // scratch: [hold: in-place results][stage: host-resident input pieces]
     const size_t hold_b = in_place ? ((mycnt * esz + 255) & ~(size_t)255) : 0;
     const size_t stage_b = bs.place == Place::Device ? 0 : (size_t)p * qe * esz;

@@ -326,6 +326,17 @@ for it in range(240):
         elif rank == root:
             check(f"stress reduce {it}", fromdev(rb, tot), tot)
         continue
+    if it % 9 == 4:                        # reduce_scatter_block: one-step (GPU flags) or host barriers
+        full = [ivec(it, r, n * p) for r in range(p)]
+        mine_tot = sum(f[rank * n:(rank + 1) * n].astype(np.int64) for f in full).astype(np.int32)
+        sb = todev(full[rank])
+        rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
+        rc = L.MPI_Reduce_scatter_block(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD)
+        if rc:
+            fails.append(f"stress rsb {it} rc={rc} {msx.last_error()}")
+            break
+        check(f"stress rsb {it} n={n}", fromdev(rb, mine_tot), mine_tot)
+        continue
     if it % 11 == 5:                       # non-blocking, through the worker
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
         req = ctypes.c_int()
