@@ -1170,6 +1170,9 @@ struct Windows {
 // flag area: slot kResultFlags + k of window r = the last call whose result
 // rank k stored into r's OUT area.
 constexpr size_t kResultFlags = 4096;
+// Scan partials' arrival flags: slot kScanFlags + k of window r = (call << 6)
+// | step of the last partial rank k pushed to r (only scan writes them).
+constexpr size_t kScanFlags = 2048;
 
 // Largest message (bytes) of the barrier-free two-step allreduce / reduce
 // (MSX_TWO_STEP_MAX; 0 = always the host-barrier schedule).  The default
@@ -2312,8 +2315,13 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     const size_t esz = (size_t)type_info(dt)->size, bytes = count * esz;
     hipStream_t s = tp->stream();
     const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
+    // GPU-synchronised when the vector fits half an IN sub-slot (count, type,
+    // p and the environment decide: the same on every rank)
+    const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
+    const bool flags = p >= 2 && p <= 32 && rd_flags() && tp->has_done() && bytes <= Qh &&
+                       bytes <= two_step_max();
     Windows w;
-    if ((rc = get_windows(tp, &w)) != MPI_SUCCESS) return rc;
+    if ((rc = get_windows(tp, &w, flags)) != MPI_SUCCESS) return rc;
     // Each step's partial is PUSHED into the consumer's IN window (an xGMI
     // remote write) and combined there from local HBM; two alternating halves
     // of IN: a peer writes step i+2's half only after the barrier of step i+1,
@@ -2332,8 +2340,57 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     void* dstv = bd.place == Place::Device ? bd.dev : recvbuf;
     rc = copy_async(partial, srcv, bytes, s);
     if (rc == MPI_SUCCESS && !exclusive) rc = copy_async(res, srcv, bytes, s);
-    if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan init");
     bool have = !exclusive;
+    if (flags) {
+        // Every step on the stream, one host sync: step i = one k_push_wait
+        // (my partial -> IN(me ^ mask) half, sub-slot me, flag (seq << 6) | i;
+        // one workgroup waits for the partial I consume), then the combines.
+        // Halves alternate and are reused as in the two-step allreduce.
+        const size_t half = (size_t)tp->rd_parity * Qh;
+        const unsigned long long seq = ++tp->rd_seq;
+        int* err_host = nullptr;
+        int* err_dev = wait_err_word(&err_host);
+        unsigned* counter = tp->push_counter();
+        if (!err_dev || !counter) { set_error("scan: flag word allocation failed"); return MPI_ERR_NO_MEM; }
+        *err_host = 0;
+        int step = 0;
+        for (int mask = 1; mask < p && rc == MPI_SUCCESS; mask <<= 1, ++step) {
+            const int dst = me ^ mask;
+            const bool last = (mask << 1) >= p;
+            const bool use = dst < p && !(last && me < dst);
+            const bool feeds = dst < p && !(last && dst < me);
+            const unsigned long long v = (seq << 6) | (unsigned long long)step;
+            if (feeds && seq > 2) rc = tp->wait_done(dst, seq - 2);
+            if (rc != MPI_SUCCESS) break;
+            const void* ps = partial;
+            void* pd = feeds ? static_cast<void*>(w.sub(dst, me) + half) : nullptr;
+            size_t pn = bytes;
+            unsigned long long* pf = feeds ? w.flags(dst) + kScanFlags + me : nullptr;
+            hipError_t e = launch_push_wait(&ps, &pd, &pn, feeds ? 1 : 0, &pf, feeds ? 1 : 0, v, sys_fences(),
+                                            counter + kCountWords,
+                                            use ? w.flags(me) + kScanFlags + dst : w.flags(me), use ? 1 : 0, -1,
+                                            err_dev, s);
+            if (e != hipSuccess) { rc = hip_fail(e, "scan push"); break; }
+            if (!use) continue;
+            const char* tmp = w.sub(me, dst) + half;
+            rc = combine2(op.opidx, k, partial, tmp, partial, count, s);
+            if (rc == MPI_SUCCESS && me > dst)
+                rc = have ? combine2(op.opidx, k, res, tmp, res, count, s) : copy_async(res, tmp, bytes, s);
+            if (me > dst) have = true;
+        }
+        if (rc == MPI_SUCCESS && have) rc = copy_async(dstv, res, bytes, s);
+        const int rs = sync_stream(s, "scan");
+        if (rc == MPI_SUCCESS) rc = rs;
+        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
+            set_error("scan: a peer's partial did not arrive within 20 s");
+            rc = MPI_ERR_OTHER;
+        }
+        tp->post_done(seq);
+        tp->rd_parity ^= 1;
+        tp->window_open = true;
+        return rc;
+    }
+    if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan init");
     int slot = 0;
     for (int mask = 1; mask < p && rc == MPI_SUCCESS; mask <<= 1) {
         const int dst = me ^ mask;

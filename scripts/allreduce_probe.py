@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One rank of a collective timing probe (fp32 SUM, device buffers).
-Usage: MSX_SIZE/MSX_RANK/... python3 scripts/allreduce_probe.py NBYTES ITERS [allreduce|rsb|reduce]
+Usage: MSX_SIZE/MSX_RANK/... python3 scripts/allreduce_probe.py NBYTES ITERS [allreduce|rsb|reduce|scan]
 NBYTES is the per-rank message (allreduce, reduce) or the whole input
 (reduce_scatter_block: NBYTES / p per block)."""
 import ctypes, os, sys, time
@@ -22,6 +22,10 @@ if kind == "allreduce":
 elif kind == "rsb":
     call = lambda: L.MPI_Reduce_scatter_block(a.data_ptr(), b.data_ptr(), n // p, C.MPI_FLOAT, C.MPI_SUM, W)
     check = lambda: bool(torch.all(b[: n // p] == float(p)).item())
+elif kind == "scan":
+    L.MPI_Scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    call = lambda: L.MPI_Scan(a.data_ptr(), b.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, W)
+    check = lambda: bool(torch.all(b == float(r_.value + 1)).item())
 else:
     call = lambda: L.MPI_Reduce(a.data_ptr(), b.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, 0, W)
     check = lambda: r_.value != 0 or bool(torch.all(b == float(p)).item())
