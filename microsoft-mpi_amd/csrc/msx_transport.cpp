@@ -319,6 +319,7 @@ public:
     {
         for (auto& kv : opened_) (void)hipIpcCloseMemHandle(kv.second);
         if (win_) (void)hipFree(win_);
+        if (rwin_) (void)hipFree(rwin_);
         if (counter_) (void)hipFree(counter_);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
@@ -447,6 +448,25 @@ public:
         return MPI_SUCCESS;
     }
 
+    int rma_window(size_t bytes, std::vector<char*>& out) override
+    {
+        // Collective, first passive-target window of the communicator only:
+        // uncached like the engine window (peers write payloads into it)
+        if (!rwin_) {
+            const bool cached = getenv("MSX_WINDOW_CACHED") && atoi(getenv("MSX_WINDOW_CACHED"));
+            hipError_t e = cached ? hipMalloc(&rwin_, bytes) : hipExtMallocWithFlags(&rwin_, bytes, hipDeviceMallocUncached);
+            trace("rma window: %zu bytes rc=%d", bytes, (int)e);
+            if (e != hipSuccess) {
+                rwin_ = nullptr;
+                return hip_fail(e, "rma staging allocation");
+            }
+            int rc = map_peers(rwin_, rwin_peers_);
+            if (rc != MPI_SUCCESS) return rc;
+        }
+        out = rwin_peers_;
+        return MPI_SUCCESS;
+    }
+
 private:
     Hub hub_;
     ShmBarrier shm_;
@@ -456,6 +476,8 @@ private:
     void* win_ = nullptr;
     size_t win_bytes_ = 0;
     std::vector<char*> win_peers_;
+    void* rwin_ = nullptr;                // passive-target staging (rma_window)
+    std::vector<char*> rwin_peers_;
 };
 
 }  // namespace
@@ -1112,12 +1134,12 @@ size_t chunk_bytes()
 // Arrival flags of the barrier-free allreduce live behind the two areas:
 // flag k of window r (8 bytes) = the last call sequence rank k posted to r.
 constexpr size_t kFlagBytes = 64 << 10;
-// Passive-target RMA area behind the flags: p payload slots (written by each
+// Passive-target RMA staging (its own IPC allocation, created by the first
+// passive-target window of a communicator): p payload slots (written by each
 // origin) then p fetch slots (written by each target), rma_bytes() / (2p) each.
 // Every slot-sized piece of a lock / PSCW operation costs one host handshake
 // with the target's service thread (~50 us), so the area is sized for large
-// pieces (MSX_RMA_BYTES, default 512 MiB), bounded so the window stays below
-// the 2 GiB IPC limit.  256 MiB lock / PSCW accumulates, 2 ranks on one MI355X
+// pieces (MSX_RMA_BYTES, default 512 MiB), below the 2 GiB IPC limit.  256 MiB lock / PSCW accumulates, 2 ranks on one MI355X
 // (profiles/r02/rma_area_*.json): 1.27 ms with 64 MiB, 0.66 ms with 256 MiB,
 // 0.53 ms with 512 MiB (= the fence epoch's 0.54 ms).
 size_t rma_bytes()
@@ -1125,7 +1147,7 @@ size_t rma_bytes()
     static size_t v = [] {
         size_t b = (size_t)512 << 20;
         if (const char* e = getenv("MSX_RMA_BYTES")) b = (size_t)atoll(e);
-        const size_t cap = ((size_t)2 << 30) - 2 * chunk_bytes() - kFlagBytes - ((size_t)1 << 20);
+        const size_t cap = ((size_t)2 << 30) - ((size_t)1 << 20);      // IPC mapping limit
         b = std::min(b, cap);
         return std::max(b, (size_t)4 << 20) & ~(size_t)4095;
     }();
@@ -1157,13 +1179,12 @@ struct Windows {
     char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * S; }
     char* out(int r) const { return base[(size_t)r] + C; }
     unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + 2 * C); }
-    size_t rma_slot() const { return (rma_bytes() / (2 * base.size())) & ~(size_t)255; }
-    // rank r's window: payload slot written by origin o / fetch slot written by target t
-    char* rma_in(int r, int o) const { return base[(size_t)r] + 2 * C + kFlagBytes + (size_t)o * rma_slot(); }
-    char* rma_fetch(int r, int t) const
-    {
-        return base[(size_t)r] + 2 * C + kFlagBytes + (base.size() + (size_t)t) * rma_slot();
-    }
+    // passive-target staging (rma_window), when the communicator has one
+    std::vector<char*> rbase;
+    size_t rma_slot() const { return (rma_bytes() / (2 * rbase.size())) & ~(size_t)255; }
+    // rank r's staging: payload slot written by origin o / fetch slot written by target t
+    char* rma_in(int r, int o) const { return rbase[(size_t)r] + (size_t)o * rma_slot(); }
+    char* rma_fetch(int r, int t) const { return rbase[(size_t)r] + (rbase.size() + (size_t)t) * rma_slot(); }
 };
 
 // Result-ready flags of the two-step allreduce live in the upper half of the
@@ -1243,7 +1264,7 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
     w->C = chunk_bytes();
     w->Q = sub_len(w->C, tp->size);
     w->S = w->Q + sub_skew(w->C / (size_t)tp->size);
-    int rc = tp->window(2 * w->C + kFlagBytes + rma_bytes(), w->base);
+    int rc = tp->window(2 * w->C + kFlagBytes, w->base);
     if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
         // the last recursive-doubling call left without its closing barrier:
         // peers may still be reading their IN areas
@@ -3027,6 +3048,7 @@ int passive_init(RmaWin* w)
     ps->p = c->size;
     ps->me = c->rank;
     int rc = get_windows(c->tp, &ps->win);
+    if (rc == MPI_SUCCESS) rc = c->tp->rma_window(rma_bytes(), ps->win.rbase);
     const size_t p = (size_t)ps->p;
     const size_t hdr = ((p * sizeof(std::atomic<uint32_t>) + p * sizeof(std::atomic<int32_t>)) + 63) & ~(size_t)63;
     const size_t pscw = (2 * p * p * sizeof(std::atomic<uint32_t>) + 63) & ~(size_t)63;

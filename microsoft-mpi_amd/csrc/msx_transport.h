@@ -53,6 +53,9 @@ public:
     virtual int map_peers(const void* ptr, std::vector<char*>& out) = 0;
     // Per-rank device scratch, IPC-mapped once: out[r] = rank r's window.
     virtual int window(size_t bytes, std::vector<char*>& out) = 0;
+    // Passive-target staging: a second per-rank window of `bytes`, created
+    // by the first call (collective) and kept for the transport's lifetime.
+    virtual int rma_window(size_t bytes, std::vector<char*>& out) = 0;
     virtual hipStream_t stream() = 0;
     // Completion counters of the fused push (k_push_post, word 0) and of the
     // two-step allreduce's result flags (words 1-2): zeroed device words per
