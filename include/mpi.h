@@ -368,6 +368,11 @@ MPI_METHOD MPI_Comm_group(MPI_Comm comm, MPI_Group* group);
 MPI_METHOD MPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm* newcomm);
 MPI_METHOD MPI_Comm_compare(MPI_Comm comm1, MPI_Comm comm2, int* result);
 MPI_METHOD MPI_Comm_test_inter(MPI_Comm comm, int* flag);
+MPI_METHOD MPI_Comm_remote_size(MPI_Comm comm, int* size);
+MPI_METHOD MPI_Comm_remote_group(MPI_Comm comm, MPI_Group* group);
+MPI_METHOD MPI_Intercomm_create(MPI_Comm local_comm, int local_leader, MPI_Comm peer_comm, int remote_leader,
+                                int tag, MPI_Comm* newintercomm);
+MPI_METHOD MPI_Intercomm_merge(MPI_Comm intercomm, int high, MPI_Comm* newintracomm);
 MPI_METHOD MPI_Group_size(MPI_Group group, int* size);
 MPI_METHOD MPI_Group_rank(MPI_Group group, int* rank);
 MPI_METHOD MPI_Group_free(MPI_Group* group);
@@ -542,6 +547,9 @@ MPI_METHOD PMPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Dat
 MPI_METHOD PMPI_Comm_group(MPI_Comm comm, MPI_Group* group);
 MPI_METHOD PMPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm* newcomm);
 MPI_METHOD PMPI_Comm_compare(MPI_Comm comm1, MPI_Comm comm2, int* result);
+MPI_METHOD PMPI_Intercomm_create(MPI_Comm local_comm, int local_leader, MPI_Comm peer_comm, int remote_leader,
+                                 int tag, MPI_Comm* newintercomm);
+MPI_METHOD PMPI_Intercomm_merge(MPI_Comm intercomm, int high, MPI_Comm* newintracomm);
 MPI_METHOD PMPI_Group_size(MPI_Group group, int* size);
 MPI_METHOD PMPI_Group_rank(MPI_Group group, int* rank);
 MPI_METHOD PMPI_Group_free(MPI_Group* group);

@@ -129,6 +129,17 @@ int v_comm(MPI_Comm c, Comm** out)
     return MPI_SUCCESS;
 }
 
+// MpiaCommValidateIntracomm: an intercommunicator is MPI_ERR_COMM (**commnotintra)
+int v_intracomm(MPI_Comm c, Comm** out)
+{
+    int rc = v_comm(c, out);
+    if (rc == MPI_SUCCESS && (*out)->inter) {
+        set_error("an intercommunicator is not valid here (**commnotintra)");
+        rc = MPI_ERR_COMM;
+    }
+    return rc;
+}
+
 bool dtype_known(MPI_Datatype dt) { return type_size(dt) >= 0; }
 
 // MpiaDatatypeValidate (mpi_api.h:113-169), predefined datatypes only.
@@ -394,7 +405,7 @@ MSX_EXPORT int MPI_Comm_split(MPI_Comm comm, int color, int key, MPI_Comm* newco
 {
     MSX_REQUIRE_INIT("MPI_Comm_split");
     Comm* c;
-    int rc = v_comm(comm, &c);
+    int rc = v_intracomm(comm, &c);     // intercommunicator splits are not supported
     if (rc == MPI_SUCCESS && !newcomm) { set_error("null newcomm"); rc = MPI_ERR_ARG; }
     if (rc == MPI_SUCCESS && color < 0 && color != MPI_UNDEFINED) {
         set_error("color %d is negative and not MPI_UNDEFINED", color);
@@ -414,7 +425,8 @@ MSX_EXPORT int MPI_Comm_dup(MPI_Comm comm, MPI_Comm* newcomm)
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS && !newcomm) { set_error("null newcomm"); rc = MPI_ERR_ARG; }
     Comm* n = nullptr;
-    if (rc == MPI_SUCCESS) rc = engine_comm_split(c, 0, c->rank, &n);   // same group, same order
+    if (rc == MPI_SUCCESS && c->inter) rc = engine_intercomm_dup(c, &n);
+    else if (rc == MPI_SUCCESS) rc = engine_comm_split(c, 0, c->rank, &n);   // same group, same order
     if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_dup", rc);
     *newcomm = comm_register(n);
     return MPI_SUCCESS;
@@ -429,7 +441,7 @@ MSX_EXPORT int MPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm* newcomm
 {
     MSX_REQUIRE_INIT("MPI_Comm_create");
     Comm* c;
-    int rc = v_comm(comm, &c);
+    int rc = v_intracomm(comm, &c);     // MPIR_Comm_create_inter is not supported
     if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_create", rc);
     std::vector<int> members;
     rc = group_members(group, &members);
@@ -463,20 +475,29 @@ MSX_EXPORT int MPI_Comm_compare(MPI_Comm comm1, MPI_Comm comm2, int* result)
     if (rc == MPI_SUCCESS) rc = v_comm(comm2, &c2);
     if (rc == MPI_SUCCESS && !result) { set_error("**nullptr result"); rc = MPI_ERR_ARG; }
     if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_compare", rc);
-    if (comm1 == comm2) {
-        *result = MPI_IDENT;
-    } else if (c1->lpid == c2->lpid) {
-        *result = MPI_CONGRUENT;
-    } else {
-        std::vector<int> a = c1->lpid, b = c2->lpid;
+    auto rel = [](const std::vector<int>& x, const std::vector<int>& y) {
+        if (x == y) return MPI_IDENT;
+        std::vector<int> a = x, b = y;
         std::sort(a.begin(), a.end());
         std::sort(b.begin(), b.end());
-        *result = a == b ? MPI_SIMILAR : MPI_UNEQUAL;
+        return a == b ? MPI_SIMILAR : MPI_UNEQUAL;
+    };
+    if (c1->inter != c2->inter) {
+        *result = MPI_UNEQUAL;
+    } else if (comm1 == comm2) {
+        *result = MPI_IDENT;
+    } else {
+        // groups (and, for intercommunicators, remote groups too: the weaker
+        // relation of the two); identical groups under another handle are
+        // congruent
+        int r = rel(c1->lpid, c2->lpid);
+        if (c1->inter) r = std::max(r, rel(c1->remote_lpid, c2->remote_lpid));
+        *result = r == MPI_IDENT ? MPI_CONGRUENT : r;
     }
     return MPI_SUCCESS;
 }
 
-// api/mpi_comm.cpp:1386-1420: every communicator here is an intracommunicator
+// api/mpi_comm.cpp:1386-1420
 MSX_EXPORT int MPI_Comm_test_inter(MPI_Comm comm, int* flag)
 {
     MSX_REQUIRE_INIT("MPI_Comm_test_inter");
@@ -484,7 +505,81 @@ MSX_EXPORT int MPI_Comm_test_inter(MPI_Comm comm, int* flag)
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS && !flag) { set_error("**nullptr flag"); rc = MPI_ERR_ARG; }
     if (rc != MPI_SUCCESS) return err_return(nullptr, "MPI_Comm_test_inter", rc);
-    *flag = 0;
+    *flag = c->inter ? 1 : 0;
+    return MPI_SUCCESS;
+}
+
+// ---- intercommunicators (api/mpi_comm.cpp:835-960, 1482-1830) ------------------
+MSX_EXPORT int MPI_Comm_remote_size(MPI_Comm comm, int* size)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_remote_size");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !c->inter) { set_error("**commnotinter"); rc = MPI_ERR_COMM; }
+    if (rc == MPI_SUCCESS && !size) { set_error("**nullptr size"); rc = MPI_ERR_ARG; }
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Comm_remote_size", rc);
+    *size = (int)c->remote_lpid.size();
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Comm_remote_group(MPI_Comm comm, MPI_Group* group)
+{
+    MSX_REQUIRE_INIT("MPI_Comm_remote_group");
+    Comm* c;
+    int rc = v_comm(comm, &c);
+    if (rc == MPI_SUCCESS && !c->inter) { set_error("**commnotinter"); rc = MPI_ERR_COMM; }
+    if (rc == MPI_SUCCESS && !group) { set_error("**nullptr group"); rc = MPI_ERR_ARG; }
+    if (rc == MPI_SUCCESS) rc = group_create(c->remote_lpid, group);
+    return err_return(c, "MPI_Comm_remote_group", rc);
+}
+
+// The leaders exchange their groups over the world mailbox; both groups then
+// join one bootstrap hub (the low group's rank 0), which carries the windows
+// and flags of the transfers between the groups.
+MSX_EXPORT int MPI_Intercomm_create(MPI_Comm local_comm, int local_leader, MPI_Comm peer_comm, int remote_leader,
+                                    int tag, MPI_Comm* newintercomm)
+{
+    MSX_REQUIRE_INIT("MPI_Intercomm_create");
+    Comm *c, *peer = nullptr;
+    int rc = v_intracomm(local_comm, &c);
+    if (rc == MPI_SUCCESS && (local_leader < 0 || local_leader >= c->size)) {
+        set_error("**ranklocal %d %d", local_leader, c->size);
+        rc = MPI_ERR_RANK;
+    }
+    if (rc == MPI_SUCCESS && c->rank == local_leader) {
+        rc = v_comm(peer_comm, &peer);
+        if (rc == MPI_SUCCESS && peer->inter) {
+            set_error("an intercommunicator as peer_comm is not supported");
+            rc = MPI_ERR_COMM;
+        }
+        if (rc == MPI_SUCCESS && (remote_leader < 0 || remote_leader >= peer->size)) {
+            set_error("**rankremote %d %d", remote_leader, peer->size);
+            rc = MPI_ERR_RANK;
+        }
+        if (rc == MPI_SUCCESS && peer->rank == remote_leader) {
+            set_error("**ranksdistinct");
+            rc = MPI_ERR_RANK;
+        }
+    }
+    if (rc == MPI_SUCCESS && !newintercomm) { set_error("**nullptr newintercomm"); rc = MPI_ERR_ARG; }
+    Comm* n = nullptr;
+    if (rc == MPI_SUCCESS) rc = engine_intercomm_create(c, local_leader, peer, remote_leader, tag, &n);
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Intercomm_create", rc);
+    *newintercomm = comm_register(n);
+    return MPI_SUCCESS;
+}
+
+MSX_EXPORT int MPI_Intercomm_merge(MPI_Comm intercomm, int high, MPI_Comm* newintracomm)
+{
+    MSX_REQUIRE_INIT("MPI_Intercomm_merge");
+    Comm* c;
+    int rc = v_comm(intercomm, &c);
+    if (rc == MPI_SUCCESS && !c->inter) { set_error("**commnotinter"); rc = MPI_ERR_COMM; }
+    if (rc == MPI_SUCCESS && !newintracomm) { set_error("**nullptr newintracomm"); rc = MPI_ERR_ARG; }
+    Comm* n = nullptr;
+    if (rc == MPI_SUCCESS) rc = engine_intercomm_merge(c, high, &n);
+    if (rc != MPI_SUCCESS) return err_return(c, "MPI_Intercomm_merge", rc);
+    *newintracomm = comm_register(n);
     return MPI_SUCCESS;
 }
 
@@ -511,7 +606,7 @@ MSX_EXPORT int MPI_Barrier(MPI_Comm comm)
     MSX_REQUIRE_INIT("MPI_Barrier");
     Comm* c;
     int rc = v_comm(comm, &c);
-    if (rc == MPI_SUCCESS) rc = coll_barrier(c);
+    if (rc == MPI_SUCCESS) rc = coll_barrier(c->inter ? c->uni : c);   // intercomm: both groups
     return err_return(c, "MPI_Barrier", rc);
 }
 
@@ -625,6 +720,71 @@ MSX_EXPORT int MPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
 // ===========================================================================
 // reduction collectives
 // ===========================================================================
+namespace {
+
+// api/mpi_reduce.cpp:1073-1160: recvbuf / sendbuf rules of MPI_Allreduce
+// (MPI_IN_PLACE is not allowed on an intercommunicator)
+int v_allreduce_bufs(Comm* c, const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype)
+{
+    if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); return MPI_ERR_BUFFER; }
+    if (sendbuf == MPI_IN_PLACE) {
+        if (c->inter) { set_error("**sendbuf_inplace on an intercommunicator"); return MPI_ERR_BUFFER; }
+        return MPI_SUCCESS;
+    }
+    int rc = v_buffer(datatype, sendbuf, count);
+    if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+    return rc;
+}
+
+// api/mpi_reduce.cpp:46-273: MPI_Reduce's checks; on an intercommunicator the
+// root is MPI_ROOT (receives), MPI_PROC_NULL (does nothing) or a remote rank
+// (sends).  *skip: nothing to do on this process.
+int v_reduce(Comm* c, const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype, MPI_Op op, int root,
+             OpRef* r, bool* skip)
+{
+    *skip = false;
+    if (c->inter) {
+        if (root == MPI_PROC_NULL) { *skip = true; return MPI_SUCCESS; }
+        if (root == MPI_ROOT) {
+            int rc = v_dtype_any(recvbuf, count, datatype);
+            return rc == MPI_SUCCESS ? v_op(op, datatype, r) : rc;
+        }
+        if (root < 0 || root >= (int)c->remote_lpid.size()) { set_error("invalid root %d", root); return MPI_ERR_ROOT; }
+        if (count > 0 && sendbuf == MPI_IN_PLACE) { set_error("**sendbuf_inplace"); return MPI_ERR_BUFFER; }
+        int rc = v_dtype_any(sendbuf, count, datatype);
+        return rc == MPI_SUCCESS ? v_op(op, datatype, r) : rc;
+    }
+    if (root < 0 || root >= c->size) { set_error("invalid root %d", root); return MPI_ERR_ROOT; }
+    int rc = v_dtype_any(sendbuf, count, datatype);
+    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, r);
+    if (rc != MPI_SUCCESS) return rc;
+    if (c->rank == root) {
+        if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); return MPI_ERR_BUFFER; }
+        rc = v_buffer(datatype, recvbuf, count);
+        if (rc == MPI_SUCCESS && count > 0 && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+    } else if (count > 0 && sendbuf == MPI_IN_PLACE) {
+        set_error("sendbuf is MPI_IN_PLACE on a non-root rank");
+        rc = MPI_ERR_BUFFER;
+    }
+    return rc;
+}
+
+int run_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t n, MPI_Datatype datatype, const OpRef& r, int root)
+{
+    if (n == 0) return MPI_SUCCESS;
+    return c->inter ? engine_inter_reduce(c, sendbuf, recvbuf, n, datatype, r, root)
+                    : coll_reduce(c, sendbuf, recvbuf, n, datatype, r, root);
+}
+
+int run_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* counts, MPI_Datatype datatype,
+                       const OpRef& r)
+{
+    return c->inter ? engine_inter_reduce_scatter(c, sendbuf, recvbuf, counts, datatype, r)
+                    : coll_reduce_scatter(c, sendbuf, recvbuf, counts, datatype, r);
+}
+
+}  // namespace
+
 MSX_EXPORT int MPI_Allreduce(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype,
                              MPI_Op op, MPI_Comm comm)
 {
@@ -634,15 +794,10 @@ MSX_EXPORT int MPI_Allreduce(const void* sendbuf, void* recvbuf, int count, MPI_
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS) rc = v_dtype_any(recvbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
-    if (rc == MPI_SUCCESS && count > 0) {
-        if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
-        else if (sendbuf != MPI_IN_PLACE) {
-            rc = v_buffer(datatype, sendbuf, count);
-            if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
-        }
-    }
+    if (rc == MPI_SUCCESS && count > 0) rc = v_allreduce_bufs(c, sendbuf, recvbuf, count, datatype);
     if (rc == MPI_SUCCESS && count > 0)
-        rc = coll_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r);
+        rc = c->inter ? engine_inter_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r)
+                      : coll_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r);
     return err_return(c, "MPI_Allreduce", rc);
 }
 
@@ -652,22 +807,10 @@ MSX_EXPORT int MPI_Reduce(const void* sendbuf, void* recvbuf, int count, MPI_Dat
     MSX_REQUIRE_INIT("MPI_Reduce");
     Comm* c;
     OpRef r;
+    bool skip = false;
     int rc = v_comm(comm, &c);
-    if (rc == MPI_SUCCESS && (root < 0 || root >= c->size)) { set_error("invalid root %d", root); rc = MPI_ERR_ROOT; }
-    if (rc == MPI_SUCCESS) rc = v_dtype_any(sendbuf, count, datatype);
-    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
-    if (rc == MPI_SUCCESS) {
-        if (c->rank == root) {
-            if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
-            else rc = v_buffer(datatype, recvbuf, count);
-            if (rc == MPI_SUCCESS && count > 0 && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
-        } else if (count > 0 && sendbuf == MPI_IN_PLACE) {
-            set_error("sendbuf is MPI_IN_PLACE on a non-root rank");
-            rc = MPI_ERR_BUFFER;
-        }
-    }
-    if (rc == MPI_SUCCESS && count > 0)
-        rc = coll_reduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, root);
+    if (rc == MPI_SUCCESS) rc = v_reduce(c, sendbuf, recvbuf, count, datatype, op, root, &r, &skip);
+    if (rc == MPI_SUCCESS && !skip) rc = run_reduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, root);
     return err_return(c, "MPI_Reduce", rc);
 }
 
@@ -689,6 +832,9 @@ int validate_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const i
         else if (sendbuf != MPI_IN_PLACE) {
             rc = v_buffer(datatype, recvbuf, recvcounts[c->rank]);
             if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
+        } else if (c->inter) {                // mpi_reduce.cpp:893-897
+            set_error("**sendbuf_inplace on an intercommunicator");
+            rc = MPI_ERR_BUFFER;
         }
     }
     return rc;
@@ -704,7 +850,7 @@ MSX_EXPORT int MPI_Reduce_scatter(const void* sendbuf, void* recvbuf, const int 
     OpRef r;
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS) rc = validate_reduce_scatter(c, sendbuf, recvbuf, recvcounts, datatype, op, &r);
-    if (rc == MPI_SUCCESS) rc = coll_reduce_scatter(c, sendbuf, recvbuf, recvcounts, datatype, r);
+    if (rc == MPI_SUCCESS) rc = run_reduce_scatter(c, sendbuf, recvbuf, recvcounts, datatype, r);
     return err_return(c, "MPI_Reduce_scatter", rc);
 }
 
@@ -721,7 +867,7 @@ MSX_EXPORT int MPI_Reduce_scatter_block(const void* sendbuf, void* recvbuf, int 
         counts.assign((size_t)c->size, recvcount);
         rc = validate_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, op, &r);
     }
-    if (rc == MPI_SUCCESS) rc = coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
+    if (rc == MPI_SUCCESS) rc = run_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
     return err_return(c, "MPI_Reduce_scatter_block", rc);
 }
 
@@ -735,7 +881,7 @@ int scan_common(const char* fn, const void* sendbuf, void* recvbuf, int count, M
 {
     Comm* c;
     OpRef r;
-    int rc = v_comm(comm, &c);
+    int rc = v_intracomm(comm, &c);      // scans are defined on intracommunicators only
     if (rc == MPI_SUCCESS && nonblocking) {
         if (request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
         else *request = MPI_REQUEST_NULL;
@@ -802,15 +948,15 @@ MSX_EXPORT int MPI_Iallreduce(const void* sendbuf, void* recvbuf, int count, MPI
     if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
     if (rc == MPI_SUCCESS) rc = v_dtype_any(recvbuf, count, datatype);
     if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
-    if (rc == MPI_SUCCESS && count > 0) {
-        if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
-        else if (sendbuf != MPI_IN_PLACE) {
-            rc = v_buffer(datatype, sendbuf, count);
-            if (rc == MPI_SUCCESS && sendbuf == recvbuf) { set_error("sendbuf aliases recvbuf"); rc = MPI_ERR_BUFFER; }
-        }
-    }
-    if (rc == MPI_SUCCESS)
+    if (rc == MPI_SUCCESS && count > 0) rc = v_allreduce_bufs(c, sendbuf, recvbuf, count, datatype);
+    if (rc == MPI_SUCCESS && c->inter) {
+        const size_t n = (size_t)count;
+        rc = request_start_generic(c, [=] {
+            return n ? engine_inter_allreduce(c, sendbuf, recvbuf, n, datatype, r) : MPI_SUCCESS;
+        }, request, datatype);
+    } else if (rc == MPI_SUCCESS) {
         rc = request_start_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, request);
+    }
     return err_return(c, "MPI_Iallreduce", rc);
 }
 
@@ -823,24 +969,12 @@ MSX_EXPORT int MPI_Ireduce(const void* sendbuf, void* recvbuf, int count, MPI_Da
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS && request == nullptr) { set_error("null request"); rc = MPI_ERR_ARG; }
     if (rc == MPI_SUCCESS) *request = MPI_REQUEST_NULL;
-    if (rc == MPI_SUCCESS && (root < 0 || root >= c->size)) { set_error("invalid root"); rc = MPI_ERR_ROOT; }
-    if (rc == MPI_SUCCESS) rc = v_dtype_any(sendbuf, count, datatype);
-    if (rc == MPI_SUCCESS) rc = v_op(op, datatype, &r);
+    bool skip = false;
+    if (rc == MPI_SUCCESS) rc = v_reduce(c, sendbuf, recvbuf, count, datatype, op, root, &r, &skip);
     if (rc == MPI_SUCCESS) {
-        if (c->rank == root) {
-            if (recvbuf == MPI_IN_PLACE) { set_error("recvbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
-            else rc = v_buffer(datatype, recvbuf, count);
-            if (rc == MPI_SUCCESS && count > 0 && sendbuf == recvbuf) { set_error("alias"); rc = MPI_ERR_BUFFER; }
-        } else if (count > 0 && sendbuf == MPI_IN_PLACE) {
-            set_error("sendbuf is MPI_IN_PLACE on a non-root rank");
-            rc = MPI_ERR_BUFFER;
-        }
-    }
-    if (rc == MPI_SUCCESS) {
-        const size_t n = (size_t)count;
-        rc = request_start_generic(c, [=] {
-            return n ? coll_reduce(c, sendbuf, recvbuf, n, datatype, r, root) : MPI_SUCCESS;
-        }, request, datatype);
+        const size_t n = skip ? 0 : (size_t)count;
+        rc = request_start_generic(c, [=] { return run_reduce(c, sendbuf, recvbuf, n, datatype, r, root); },
+                                   request, datatype);
     }
     return err_return(c, "MPI_Ireduce", rc);
 }
@@ -859,7 +993,7 @@ MSX_EXPORT int MPI_Ireduce_scatter(const void* sendbuf, void* recvbuf, const int
     if (rc == MPI_SUCCESS) {
         std::vector<int> counts(recvcounts, recvcounts + c->size);
         rc = request_start_generic(c, [=] {
-            return coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
+            return run_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
         }, request, datatype);
     }
     return err_return(c, "MPI_Ireduce_scatter", rc);
@@ -883,7 +1017,7 @@ MSX_EXPORT int MPI_Ireduce_scatter_block(const void* sendbuf, void* recvbuf, int
     }
     if (rc == MPI_SUCCESS) {
         rc = request_start_generic(c, [=] {
-            return coll_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
+            return run_reduce_scatter(c, sendbuf, recvbuf, counts.data(), datatype, r);
         }, request, datatype);
     }
     return err_return(c, "MPI_Ireduce_scatter_block", rc);
@@ -1176,6 +1310,8 @@ MSX_ALIAS(MPI_Testall) int PMPI_Testall(int, MPI_Request[], int*, MPI_Status[]);
 MSX_ALIAS(MPI_Win_post) int PMPI_Win_post(MPI_Group, int, MPI_Win);
 MSX_ALIAS(MPI_Comm_create) int PMPI_Comm_create(MPI_Comm, MPI_Group, MPI_Comm*);
 MSX_ALIAS(MPI_Comm_compare) int PMPI_Comm_compare(MPI_Comm, MPI_Comm, int*);
+MSX_ALIAS(MPI_Intercomm_create) int PMPI_Intercomm_create(MPI_Comm, int, MPI_Comm, int, int, MPI_Comm*);
+MSX_ALIAS(MPI_Intercomm_merge) int PMPI_Intercomm_merge(MPI_Comm, int, MPI_Comm*);
 MSX_ALIAS(MPI_Win_start) int PMPI_Win_start(MPI_Group, int, MPI_Win);
 MSX_ALIAS(MPI_Win_complete) int PMPI_Win_complete(MPI_Win);
 MSX_ALIAS(MPI_Win_wait) int PMPI_Win_wait(MPI_Win);
@@ -1454,7 +1590,7 @@ MSX_EXPORT int MPI_Win_create(void* base, MPI_Aint size, int disp_unit, MPI_Info
 {
     MSX_REQUIRE_INIT("MPI_Win_create");
     Comm* c;
-    int rc = v_comm(comm, &c);
+    int rc = v_intracomm(comm, &c);
     if (rc == MPI_SUCCESS && info != MPI_INFO_NULL) { set_error("only MPI_INFO_NULL is supported"); rc = MPI_ERR_INFO; }
     if (rc == MPI_SUCCESS && size < 0) { set_error("negative window size"); rc = MPI_ERR_SIZE; }
     if (rc == MPI_SUCCESS && disp_unit <= 0) { set_error("disp_unit must be positive"); rc = MPI_ERR_ARG; }
@@ -1489,7 +1625,7 @@ MSX_EXPORT int MPI_Win_allocate(MPI_Aint size, int disp_unit, MPI_Info info, MPI
 {
     MSX_REQUIRE_INIT("MPI_Win_allocate");
     Comm* c;
-    int rc = v_comm(comm, &c);
+    int rc = v_intracomm(comm, &c);
     if (rc == MPI_SUCCESS && info != MPI_INFO_NULL) { set_error("only MPI_INFO_NULL is supported"); rc = MPI_ERR_INFO; }
     if (rc == MPI_SUCCESS && size < 0) { set_error("negative window size (**rmasize)"); rc = MPI_ERR_SIZE; }
     if (rc == MPI_SUCCESS && disp_unit <= 0) { set_error("disp_unit must be positive"); rc = MPI_ERR_ARG; }

@@ -104,6 +104,7 @@ int world_init()
     g_self.lpid.assign(1, rank);
     if (size > 1) {
         int rc = transport_create(rank, size, &g_world.tp);
+        if (rc == MPI_SUCCESS) rc = engine_mailbox_init(g_world.tp, rank, size);   // MPI_Intercomm_create
         if (rc != MPI_SUCCESS) return rc;
     }
     g_init.store(true);

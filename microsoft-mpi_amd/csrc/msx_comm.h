@@ -22,6 +22,16 @@ struct Comm {
     // process id (MPI_COMM_WORLD rank) of every member, by rank in this
     // communicator: the lrank_to_lpid map of the comm's group (mpid/group.cpp)
     std::vector<int> lpid;
+    // Intercommunicator (MPI_Intercomm_create): rank / size / lpid describe
+    // the local group; `local` is the local group as an intracommunicator of
+    // its own (the reference's inter.local_comm), `uni` both groups in one
+    // intracommunicator, the low group first -- the data plane between the
+    // groups (point-to-point transfers over its windows).
+    bool inter = false;
+    bool is_low = false;              // this group is first in `uni`
+    std::vector<int> remote_lpid;     // the remote group
+    Comm* local = nullptr;
+    Comm* uni = nullptr;
 };
 
 // MPI_COMM_WORLD, MPI_COMM_SELF or a derived communicator; nullptr otherwise.
@@ -66,6 +76,8 @@ int local_combine(const OpRef& op, MPI_Datatype dt, const void* in, void* inout,
 
 // Copy `bytes` between any two buffers (host or device), blocking.
 int copy_any(void* dst, const void* src, size_t bytes);
+// MPIR_Localcopy: count elements of dt (derived types through the pack kernels).
+int local_copy(const void* src, void* dst, size_t count, MPI_Datatype dt);
 
 // Non-blocking requests (stream/event backed).
 struct Request;

@@ -225,6 +225,28 @@ FAPI void mpi_comm_test_inter_(const MPI_Fint* comm, MPI_Fint* flag, MPI_Fint* i
     *flag = to_flog(f);
 }
 FNAMES(comm_test_inter, COMM_TEST_INTER)
+FAPI void mpi_comm_remote_size_(const MPI_Fint* comm, MPI_Fint* size, MPI_Fint* ierr)
+{
+    *ierr = MPI_Comm_remote_size(*comm, size);
+}
+FNAMES(comm_remote_size, COMM_REMOTE_SIZE)
+FAPI void mpi_comm_remote_group_(const MPI_Fint* comm, MPI_Fint* group, MPI_Fint* ierr)
+{
+    *ierr = MPI_Comm_remote_group(*comm, group);
+}
+FNAMES(comm_remote_group, COMM_REMOTE_GROUP)
+FAPI void mpi_intercomm_create_(const MPI_Fint* local_comm, const MPI_Fint* local_leader, const MPI_Fint* peer_comm,
+                                const MPI_Fint* remote_leader, const MPI_Fint* tag, MPI_Fint* newintercomm,
+                                MPI_Fint* ierr)
+{
+    *ierr = MPI_Intercomm_create(*local_comm, *local_leader, *peer_comm, *remote_leader, *tag, newintercomm);
+}
+FNAMES(intercomm_create, INTERCOMM_CREATE)
+FAPI void mpi_intercomm_merge_(const MPI_Fint* intercomm, const MPI_Fint* high, MPI_Fint* newintracomm, MPI_Fint* ierr)
+{
+    *ierr = MPI_Intercomm_merge(*intercomm, *high, newintracomm);   // LOGICAL: nonzero = .TRUE.
+}
+FNAMES(intercomm_merge, INTERCOMM_MERGE)
 FAPI void mpi_group_size_(const MPI_Fint* group, MPI_Fint* size, MPI_Fint* ierr) { *ierr = MPI_Group_size(*group, size); }
 FNAMES(group_size, GROUP_SIZE)
 FAPI void mpi_group_rank_(const MPI_Fint* group, MPI_Fint* rank, MPI_Fint* ierr) { *ierr = MPI_Group_rank(*group, rank); }

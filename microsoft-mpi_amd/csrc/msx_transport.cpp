@@ -3292,6 +3292,564 @@ const char* engine_transport_name(Transport* tp)
 
 std::shared_future<int> engine_async(std::function<int()> fn) { return worker().submit(std::move(fn)); }
 
+// ===========================================================================
+// intercommunicators (api/mpi_comm.cpp:1482-1610 MPI_Intercomm_create,
+// :1653-1830 MPI_Intercomm_merge; reduce.cpp:778-863 MPIR_Reduce_inter,
+// 1821-1990 MPIR_Reduce_scatter[_block]_inter, 4109-4175 MPIR_Allreduce_inter)
+// ===========================================================================
+namespace {
+
+// ---- world mailbox: one inbox per process in node shared memory ----------
+constexpr size_t kMailBytes = 16384;
+struct MailSlot {
+    std::atomic<uint32_t> state;      // 0 empty, 1 being written, 2 full
+    int32_t src, tag, len, pad_;
+    char data[kMailBytes];
+};
+struct Mailbox {
+    MailSlot* slots = nullptr;
+    int me = 0, p = 0;
+    std::deque<std::tuple<int, int, std::vector<char>>> pending;   // received, not yet matched
+};
+Mailbox g_mail;
+
+// move a message waiting in my inbox (if any) to the pending list
+void mail_drain()
+{
+    MailSlot& s = g_mail.slots[g_mail.me];
+    if (s.state.load(std::memory_order_acquire) != 2) return;
+    g_mail.pending.emplace_back(s.src, s.tag, std::vector<char>(s.data, s.data + s.len));
+    s.state.store(0, std::memory_order_release);
+    futex_wake_all(&s.state);
+}
+
+int mail_send(int dst, int tag, const void* data, size_t n)
+{
+    if (!g_mail.slots || dst < 0 || dst >= g_mail.p) { set_error("mailbox: no process %d", dst); return MPI_ERR_INTERN; }
+    if (n > kMailBytes) { set_error("mailbox: %zu-byte message exceeds %zu", n, kMailBytes); return MPI_ERR_INTERN; }
+    MailSlot& s = g_mail.slots[dst];
+    const double t_end = now_s() + 600.0;
+    for (int spin = 0;; ++spin) {
+        uint32_t z = 0;
+        if (s.state.compare_exchange_strong(z, 1, std::memory_order_acq_rel)) {
+            s.src = g_mail.me;
+            s.tag = tag;
+            s.len = (int32_t)n;
+            memcpy(s.data, data, n);
+            s.state.store(2, std::memory_order_release);
+            futex_wake_all(&s.state);
+            return MPI_SUCCESS;
+        }
+        mail_drain();                 // a peer sending to me must never wait for my send
+        if (now_s() > t_end) { set_error("mailbox: process %d's inbox stayed full for 600 s", dst); return MPI_ERR_OTHER; }
+        if (spin < 1000) sched_yield();
+        else futex_wait_ms(&s.state, z, 10);
+    }
+}
+
+int mail_recv(int src, int tag, std::vector<char>* out)
+{
+    const double t_end = now_s() + 600.0;
+    for (int spin = 0;; ++spin) {
+        mail_drain();
+        for (auto it = g_mail.pending.begin(); it != g_mail.pending.end(); ++it)
+            if (std::get<0>(*it) == src && std::get<1>(*it) == tag) {
+                *out = std::move(std::get<2>(*it));
+                g_mail.pending.erase(it);
+                return MPI_SUCCESS;
+            }
+        if (now_s() > t_end) { set_error("mailbox: no message from process %d (tag %d) in 600 s", src, tag); return MPI_ERR_OTHER; }
+        if (spin < 1000) sched_yield();
+        else futex_wait_ms(&g_mail.slots[g_mail.me].state, 0, 10);
+    }
+}
+
+// every member of c gets root's v (same length everywhere)
+int group_bcast(Comm* c, std::vector<int32_t>& v, int root)
+{
+    if (c->size == 1 || v.empty()) return MPI_SUCCESS;
+    std::vector<int32_t> all(v.size() * (size_t)c->size);
+    const int rc = c->tp->allgather(v.data(), v.size() * sizeof(int32_t), all.data());
+    if (rc == MPI_SUCCESS) std::copy(all.begin() + (long)root * (long)v.size(), all.begin() + (long)(root + 1) * (long)v.size(), v.begin());
+    return rc;
+}
+
+// A private duplicate of intracommunicator c (same group, own transport).
+int dup_intra(Comm* c, Comm** out)
+{
+    auto* n = new Comm();
+    n->rank = c->rank;
+    n->size = c->size;
+    n->lpid = c->lpid;
+    n->errhandler = c->errhandler;
+    if (c->tp) {
+        int nr = 0, ns = 0;
+        std::vector<int> members;
+        const int rc = transport_split(c->tp, 0, c->rank, &nr, &ns, &n->tp, &members);
+        if (rc != MPI_SUCCESS) { delete n; return rc; }
+    }
+    *out = n;
+    return MPI_SUCCESS;
+}
+
+void free_intra(Comm* c)
+{
+    if (!c) return;
+    if (c->tp) {
+        (void)c->tp->barrier();                         // no peer still uses its windows
+        transport_destroy(c->tp);
+    }
+    delete c;
+}
+
+// Separate scratch of the intercommunicator paths (the intra schedules they
+// call use dev_scratch themselves).
+char* inter_scratch(size_t bytes)
+{
+    static char* p = nullptr;
+    static size_t cap = 0;
+    if (bytes > cap) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) { p = nullptr; return nullptr; }
+        cap = bytes;
+    }
+    return p;
+}
+
+// ---- point-to-point between the groups over the union's windows ----------
+// Rank `from` moves `bytes` to rank `to` of the union communicator u through
+// sub-slot `from` of the receiver's IN area, in chunks of half a sub-slot
+// alternating between the halves.  Chunk c of the pair (both sides count the
+// pair's chunks in the same order: MPI orders collectives) carries data flag
+// c (slot kP2PData + from at the receiver); the receiver acknowledges with
+// flag c (slot kP2PAck + to at the sender) after copying it out, and the
+// sender waits for ack c - 2 before reusing a half.  All waits are single
+// GPU workgroups on the union's stream; the caller syncs the stream.
+constexpr size_t kP2PData = 1024, kP2PAck = 1536;
+
+int p2p_chunks(Comm* u, size_t bytes, size_t* chunk)
+{
+    const size_t Qh = (sub_len(chunk_bytes(), u->size) / 2) & ~(size_t)255;
+    *chunk = Qh;
+    return (int)((bytes + Qh - 1) / Qh);
+}
+
+int p2p_send(Comm* u, int to, const char* src, size_t bytes, int* err_dev)
+{
+    Windows w;
+    int rc = get_windows(u->tp, &w, true);
+    if (rc != MPI_SUCCESS) return rc;
+    hipStream_t s = u->tp->stream();
+    unsigned* counter = u->tp->push_counter();
+    if (!counter) { set_error("p2p: counter allocation failed"); return MPI_ERR_NO_MEM; }
+    size_t Qh;
+    const int n = p2p_chunks(u, bytes, &Qh);
+    uint64_t& sent = u->tp->p2p_sent(to);
+    for (int i = 0; i < n && rc == MPI_SUCCESS; ++i) {
+        const uint64_t c = ++sent;
+        const size_t off = (size_t)i * Qh, len = std::min(Qh, bytes - off);
+        if (c > 2) {                                  // the half's previous chunk was copied out
+            hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, c - 2, false, nullptr,
+                                            w.flags(u->rank) + kP2PAck + to, 1, -1, err_dev, s);
+            if (e != hipSuccess) { rc = hip_fail(e, "p2p ack wait"); break; }
+        }
+        const void* ps = src + off;
+        void* pd = w.sub(to, u->rank) + (size_t)(c & 1) * Qh;
+        unsigned long long* pf = w.flags(to) + kP2PData + u->rank;
+        hipError_t e = launch_push_wait(&ps, &pd, &len, 1, &pf, 1, c, sys_fences(), counter + kCountWords,
+                                        w.flags(u->rank), 0, -1, err_dev, s);
+        if (e != hipSuccess) rc = hip_fail(e, "p2p push");
+    }
+    return rc;
+}
+
+int p2p_recv(Comm* u, int from, char* dst, size_t bytes, int* err_dev)
+{
+    Windows w;
+    int rc = get_windows(u->tp, &w, true);
+    if (rc != MPI_SUCCESS) return rc;
+    hipStream_t s = u->tp->stream();
+    size_t Qh;
+    const int n = p2p_chunks(u, bytes, &Qh);
+    uint64_t& got = u->tp->p2p_recv(from);
+    for (int i = 0; i < n && rc == MPI_SUCCESS; ++i) {
+        const uint64_t c = ++got;
+        const size_t off = (size_t)i * Qh, len = std::min(Qh, bytes - off);
+        hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, c, false, nullptr,
+                                        w.flags(u->rank) + kP2PData + from, 1, -1, err_dev, s);
+        if (e != hipSuccess) { rc = hip_fail(e, "p2p data wait"); break; }
+        rc = copy_async(dst + off, w.sub(u->rank, from) + (size_t)(c & 1) * Qh, len, s);
+        unsigned long long* ack = w.flags(from) + kP2PAck + u->rank;
+        if (rc == MPI_SUCCESS) {
+            e = launch_post_flags(&ack, 1, c, s);
+            if (e != hipSuccess) rc = hip_fail(e, "p2p ack");
+        }
+    }
+    return rc;
+}
+
+int p2p_finish(Comm* u, int rc, int* err_host)
+{
+    const int rs = sync_stream(u->tp->stream(), "intercommunicator transfer");
+    if (rc == MPI_SUCCESS) rc = rs;
+    if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
+        set_error("intercommunicator: the peer's data did not arrive within 20 s");
+        rc = MPI_ERR_OTHER;
+    }
+    return rc;
+}
+
+// union rank of rank r of the local (mine = true) or remote group
+int urank_of(const Comm* ic, bool mine, int r)
+{
+    const bool low = mine ? ic->is_low : !ic->is_low;
+    const int nlow = ic->is_low ? ic->size : (int)ic->remote_lpid.size();
+    return low ? r : nlow + r;
+}
+
+// ---- intracommunicator broadcast / scatterv through the windows -----------
+// (the local steps of the reference's inter algorithms: MPIR_Bcast_intra,
+// scatterv from rank 0).  Root writes block r into rank r's IN sub-slot
+// `root` (peer pointers), barrier, receivers copy out, barrier; chunked by
+// the sub-slot.  Buffers may be host or device memory.
+int do_scatterv(Comm* c, int root, const char* src, const std::vector<size_t>& off, const std::vector<size_t>& len,
+                char* dst)
+{
+    if (c->size == 1) return len[0] ? copy_any(dst, src + off[0], len[0]) : MPI_SUCCESS;
+    Windows w;
+    int rc = get_windows(c->tp, &w);
+    if (rc != MPI_SUCCESS) return rc;
+    hipStream_t s = c->tp->stream();
+    size_t maxlen = 0;
+    for (size_t l : len) maxlen = std::max(maxlen, l);
+    for (size_t o = 0; o < maxlen && rc == MPI_SUCCESS; o += w.Q) {
+        if (c->rank == root)
+            for (int r = 0; r < c->size && rc == MPI_SUCCESS; ++r) {
+                if (o >= len[(size_t)r]) continue;
+                const size_t n = std::min(w.Q, len[(size_t)r] - o);
+                rc = r == root ? copy_async(dst + o, src + off[(size_t)r] + o, n, s)
+                               : copy_async(w.sub(r, root), src + off[(size_t)r] + o, n, s);
+            }
+        if (rc == MPI_SUCCESS) rc = sync_stream(s, "scatter push");
+        if (rc == MPI_SUCCESS) rc = c->tp->barrier();
+        const size_t mine = len[(size_t)c->rank];
+        if (rc == MPI_SUCCESS && c->rank != root && o < mine) {
+            rc = copy_async(dst + o, w.sub(c->rank, root), std::min(w.Q, mine - o), s);
+            if (rc == MPI_SUCCESS) rc = sync_stream(s, "scatter collect");
+        }
+        if (rc == MPI_SUCCESS) rc = c->tp->barrier();
+    }
+    return rc;
+}
+
+int do_bcast(Comm* c, int root, char* buf, size_t bytes)
+{
+    std::vector<size_t> off((size_t)c->size, 0), len((size_t)c->size, bytes);
+    return do_scatterv(c, root, buf, off, len, buf);
+}
+
+// the intracommunicator reduce of one group to its rank 0 (reference order:
+// MPIR_Reduce_intra on inter.local_comm)
+int local_reduce0(Comm* lc, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt, const OpRef& op)
+{
+    if (lc->size == 1) return local_copy(sendbuf, recvbuf, count, dt);
+    if (op.opidx == O_NULL) return host_user_reduce(lc, sendbuf, recvbuf, count, dt, op, 0);
+    return do_allreduce(lc, sendbuf, recvbuf, count, dt, op, 0);
+}
+
+// bytes a transfer of count elements of dt moves (packed for a derived type)
+size_t wire_bytes(MPI_Datatype dt, size_t count)
+{
+    return dtype_is_derived(dt) ? (size_t)dtype_lookup(dt)->size * count : (size_t)type_size(dt) * count;
+}
+
+// MPIR_Reduce_inter: the remote group reduces to its rank 0, which sends to root
+int do_inter_reduce(Comm* ic, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt, const OpRef& op,
+                    int root)
+{
+    if (root == MPI_PROC_NULL || count == 0) return MPI_SUCCESS;
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    Comm* u = ic->uni;
+    const bool derived = dtype_is_derived(dt);
+    const size_t wb = wire_bytes(dt, count);
+    int* err_host = nullptr;
+    int* err_dev = wait_err_word(&err_host);
+    if (!err_dev) { set_error("intercommunicator: flag word allocation failed"); return MPI_ERR_NO_MEM; }
+    *err_host = 0;
+    if (root == MPI_ROOT) {
+        // receive the remote group's result from its rank 0
+        char* land = static_cast<char*>(recvbuf);
+        if (derived) {
+            land = inter_scratch(wb);
+            if (!land) { set_error("intercommunicator: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+        }
+        rc = p2p_finish(u, p2p_recv(u, urank_of(ic, false, 0), land, wb, err_dev), err_host);
+        if (rc == MPI_SUCCESS && derived) rc = dt_copy_any(land, (int64_t)wb, MPI_BYTE, recvbuf, (int64_t)count, dt);
+        return rc;
+    }
+    // my group sends: local reduce to rank 0 into a private buffer, then rank 0 -> root
+    int64_t lo = 0, hi = (int64_t)wb;
+    if (derived) dt_span(dtype_lookup(dt), (int64_t)count, &lo, &hi);
+    const size_t span = (size_t)(hi - lo);
+    char* tmp = nullptr;
+    if (ic->rank == 0) {
+        tmp = inter_scratch(span + (derived ? wb : 0) + 256);
+        if (!tmp) { set_error("intercommunicator: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+    }
+    rc = local_reduce0(ic->local, sendbuf, tmp ? tmp - lo : nullptr, count, dt, op);
+    if (rc != MPI_SUCCESS || ic->rank != 0) return rc;
+    const char* wire = tmp;
+    if (derived) {                                    // pack the typed result
+        char* packed = tmp + ((span + 255) & ~(size_t)255);
+        rc = dt_copy_any(tmp - lo, (int64_t)count, dt, packed, (int64_t)wb, MPI_BYTE);
+        wire = packed;
+    }
+    if (rc == MPI_SUCCESS) rc = p2p_finish(u, p2p_send(u, urank_of(ic, false, root), wire, wb, err_dev), err_host);
+    return rc;
+}
+
+}  // namespace
+
+int engine_mailbox_init(Transport* world, int rank, int size)
+{
+    if (size < 2 || !world) return MPI_SUCCESS;
+    void* m = nullptr;
+    int rc = shm_collective(world, (size_t)size * sizeof(MailSlot), &m);
+    if (rc != MPI_SUCCESS) return rc;
+    g_mail.slots = static_cast<MailSlot*>(m);
+    g_mail.me = rank;
+    g_mail.p = size;
+    return MPI_SUCCESS;
+}
+
+int engine_intercomm_create(Comm* local, int leader, Comm* peer, int remote_leader, int tag, Comm** out)
+{
+    *out = nullptr;
+    return worker().run([=]() -> int {
+        // 1. rank 0 of each group opens a bootstrap socket; its group learns the port
+        int lfd = -1;
+        std::vector<int32_t> pv{0};
+        if (local->rank == 0) {
+            int pt = 0;
+            lfd = listen_ephemeral(&pt);
+            pv[0] = lfd >= 0 ? pt : -1;
+        }
+        int rc = group_bcast(local, pv, 0);
+        const int32_t gport = pv[0];
+        // 2. the leaders swap {leader process id, group port, group size, members}
+        std::vector<int32_t> hdr{MPI_SUCCESS, 0, 0, 0}, rem;
+        if (rc == MPI_SUCCESS && local->rank == leader) {
+            std::vector<int32_t> msg{local->lpid[(size_t)leader], gport, local->size};
+            msg.insert(msg.end(), local->lpid.begin(), local->lpid.end());
+            const int rl = peer->lpid[(size_t)remote_leader];
+            int r2 = mail_send(rl, tag, msg.data(), msg.size() * sizeof(int32_t));
+            std::vector<char> got;
+            if (r2 == MPI_SUCCESS) r2 = mail_recv(rl, tag, &got);
+            if (r2 == MPI_SUCCESS && got.size() >= 3 * sizeof(int32_t)) {
+                std::vector<int32_t> g(got.size() / sizeof(int32_t));
+                memcpy(g.data(), got.data(), g.size() * sizeof(int32_t));
+                hdr = {MPI_SUCCESS, g[0], g[1], g[2]};
+                rem.assign(g.begin() + 3, g.end());
+            } else {
+                hdr[0] = r2 != MPI_SUCCESS ? r2 : MPI_ERR_INTERN;
+            }
+        }
+        if (rc == MPI_SUCCESS) rc = group_bcast(local, hdr, leader);
+        if (rc == MPI_SUCCESS && hdr[0] != MPI_SUCCESS) rc = hdr[0];
+        if (rc == MPI_SUCCESS && (hdr[2] <= 0 || hdr[3] <= 0)) {
+            set_error("MPI_Intercomm_create: the remote group did not publish its bootstrap socket");
+            rc = MPI_ERR_OTHER;
+        }
+        if (rc == MPI_SUCCESS) {
+            rem.resize((size_t)hdr[3]);
+            rc = group_bcast(local, rem, leader);
+        }
+        if (rc != MPI_SUCCESS) {
+            if (lfd >= 0) close(lfd);
+            return rc;
+        }
+        // 3. both groups in one communicator, the group with the lower leader id first
+        const bool low = local->lpid[(size_t)leader] < hdr[1];
+        const int nr = hdr[3], nlow = low ? local->size : nr;
+        const int usize = local->size + nr, urank = low ? local->rank : nlow + local->rank;
+        if (!(low && local->rank == 0) && lfd >= 0) {
+            close(lfd);
+            lfd = -1;
+        }
+        auto* t = new IpcTransport();
+        rc = t->init(urank, usize, low ? gport : hdr[2], lfd);
+        if (rc != MPI_SUCCESS) {
+            delete t;
+            return rc;
+        }
+        auto* u = new Comm();
+        u->rank = urank;
+        u->size = usize;
+        u->tp = t;
+        u->lpid = low ? local->lpid : rem;
+        const std::vector<int>& second = low ? rem : local->lpid;
+        u->lpid.insert(u->lpid.end(), second.begin(), second.end());
+        // 4. the intercommunicator's own local group
+        Comm* lc = nullptr;
+        rc = dup_intra(local, &lc);
+        if (rc != MPI_SUCCESS) {
+            free_intra(u);
+            return rc;
+        }
+        auto* ic = new Comm();
+        ic->inter = true;
+        ic->rank = local->rank;
+        ic->size = local->size;
+        ic->lpid = local->lpid;
+        ic->remote_lpid.assign(rem.begin(), rem.end());
+        ic->is_low = low;
+        ic->local = lc;
+        ic->uni = u;
+        ic->errhandler = local->errhandler;
+        *out = ic;
+        return MPI_SUCCESS;
+    });
+}
+
+int engine_intercomm_merge(Comm* ic, int high, Comm** out)
+{
+    *out = nullptr;
+    return worker().run([=]() -> int {
+        // every union member's (high, process id of its group's rank 0)
+        const int32_t mine[3] = {high ? 1 : 0, ic->lpid[0], ic->is_low ? 1 : 0};
+        std::vector<int32_t> all((size_t)ic->uni->size * 3);
+        int rc = ic->uni->tp->allgather(mine, sizeof(mine), all.data());
+        if (rc != MPI_SUCCESS) return rc;
+        int lsum = 0, rhigh = -1, r0 = -1;
+        for (int r = 0; r < ic->uni->size; ++r) {
+            const int32_t* e = &all[(size_t)r * 3];
+            if ((e[2] != 0) == ic->is_low) lsum += e[0];
+            else { rhigh = e[0]; r0 = e[1]; }
+        }
+        if (lsum != 0 && lsum != ic->size) {          // **notsame high
+            set_error("MPI_Intercomm_merge: high differs within the local group");
+            return MPI_ERR_ARG;
+        }
+        // equal high values: the group whose rank 0 has the lower process id first
+        const int eff = (high ? 1 : 0) != rhigh ? (high ? 1 : 0) : (ic->lpid[0] > r0 ? 1 : 0);
+        int nr = 0, ns = 0;
+        Transport* t = nullptr;
+        std::vector<int> members;
+        rc = transport_split(ic->uni->tp, 0, (eff << 20) | ic->rank, &nr, &ns, &t, &members);
+        if (rc != MPI_SUCCESS) return rc;
+        auto* c = new Comm();
+        c->rank = nr;
+        c->size = ns;
+        c->tp = t;
+        for (int m : members) c->lpid.push_back(ic->uni->lpid[(size_t)m]);
+        c->errhandler = ic->errhandler;
+        *out = c;
+        return MPI_SUCCESS;
+    });
+}
+
+int engine_intercomm_dup(Comm* ic, Comm** out)
+{
+    *out = nullptr;
+    return worker().run([=]() -> int {
+        Comm *lc = nullptr, *u = nullptr;
+        int rc = dup_intra(ic->local, &lc);
+        if (rc == MPI_SUCCESS) rc = dup_intra(ic->uni, &u);
+        if (rc != MPI_SUCCESS) {
+            free_intra(lc);
+            return rc;
+        }
+        auto* n = new Comm();
+        n->inter = true;
+        n->rank = ic->rank;
+        n->size = ic->size;
+        n->lpid = ic->lpid;
+        n->remote_lpid = ic->remote_lpid;
+        n->is_low = ic->is_low;
+        n->local = lc;
+        n->uni = u;
+        n->errhandler = ic->errhandler;
+        *out = n;
+        return MPI_SUCCESS;
+    });
+}
+
+int engine_inter_reduce(Comm* ic, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                        const OpRef& op, int root)
+{
+    return worker().run([=] { return do_inter_reduce(ic, sendbuf, recvbuf, count, dt, op, root); });
+}
+
+// MPIR_Allreduce_inter (reduce.cpp:4109-4175): reduce from the high group to
+// the low group's rank 0, then from the low group to the high group's rank 0,
+// then a broadcast within each group
+int engine_inter_allreduce(Comm* ic, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                           const OpRef& op)
+{
+    return worker().run([=]() -> int {
+        const int into_me = ic->rank == 0 ? MPI_ROOT : MPI_PROC_NULL;
+        int rc = ic->is_low ? do_inter_reduce(ic, sendbuf, recvbuf, count, dt, op, into_me)
+                            : do_inter_reduce(ic, sendbuf, recvbuf, count, dt, op, 0);
+        if (rc == MPI_SUCCESS)
+            rc = ic->is_low ? do_inter_reduce(ic, sendbuf, recvbuf, count, dt, op, 0)
+                            : do_inter_reduce(ic, sendbuf, recvbuf, count, dt, op, into_me);
+        if (rc != MPI_SUCCESS || ic->size == 1) return rc;
+        if (!dtype_is_derived(dt)) return do_bcast(ic->local, 0, static_cast<char*>(recvbuf), wire_bytes(dt, count));
+        // derived type: broadcast the packed result, unpack everywhere
+        const size_t wb = wire_bytes(dt, count);
+        char* packed = inter_scratch(wb + 256);
+        if (!packed) { set_error("intercommunicator: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+        if (ic->rank == 0) rc = dt_copy_any(recvbuf, (int64_t)count, dt, packed, (int64_t)wb, MPI_BYTE);
+        if (rc == MPI_SUCCESS) rc = do_bcast(ic->local, 0, packed, wb);
+        if (rc == MPI_SUCCESS && ic->rank != 0) rc = dt_copy_any(packed, (int64_t)wb, MPI_BYTE, recvbuf, (int64_t)count, dt);
+        return rc;
+    });
+}
+
+// MPIR_Reduce_scatter_inter (reduce.cpp:1852-1990): the whole vector of
+// total = sum(recvcounts) elements is reduced to rank 0 of each group (low
+// group first), then scattered within the group
+int engine_inter_reduce_scatter(Comm* ic, const void* sendbuf, void* recvbuf, const int* recvcounts,
+                                MPI_Datatype dt, const OpRef& op)
+{
+    std::vector<int> counts(recvcounts, recvcounts + ic->size);
+    return worker().run([=]() -> int {
+        size_t total = 0;
+        for (int c : counts) total += (size_t)c;
+        if (total == 0) return MPI_SUCCESS;
+        if (dtype_is_derived(dt)) {
+            set_error("MPI_Reduce_scatter on an intercommunicator: derived datatypes are not supported");
+            return MPI_ERR_TYPE;
+        }
+        const size_t esz = (size_t)type_size(dt);
+        // rank 0's landing buffer for the remote group's reduction (device)
+        char* tmp = nullptr;
+        std::vector<char> keep;
+        if (ic->rank == 0) {
+            if (hipMalloc(&tmp, total * esz) != hipSuccess) { set_error("reduce_scatter: allocation failed"); return MPI_ERR_NO_MEM; }
+        }
+        const int into_me = ic->rank == 0 ? MPI_ROOT : MPI_PROC_NULL;
+        int rc = ic->is_low ? do_inter_reduce(ic, sendbuf, tmp, total, dt, op, into_me)
+                            : do_inter_reduce(ic, sendbuf, tmp, total, dt, op, 0);
+        if (rc == MPI_SUCCESS)
+            rc = ic->is_low ? do_inter_reduce(ic, sendbuf, tmp, total, dt, op, 0)
+                            : do_inter_reduce(ic, sendbuf, tmp, total, dt, op, into_me);
+        std::vector<size_t> off((size_t)ic->size), len((size_t)ic->size);
+        size_t o = 0;
+        for (int r = 0; r < ic->size; ++r) {
+            off[(size_t)r] = o * esz;
+            len[(size_t)r] = (size_t)counts[(size_t)r] * esz;
+            o += (size_t)counts[(size_t)r];
+        }
+        if (rc == MPI_SUCCESS) rc = do_scatterv(ic->local, 0, tmp, off, len, static_cast<char*>(recvbuf));
+        if (tmp) (void)hipFree(tmp);
+        return rc;
+    });
+}
+
 int engine_comm_split(Comm* parent, int color, int key, Comm** out)
 {
     *out = nullptr;
@@ -3322,6 +3880,12 @@ int engine_comm_free(Comm* c)
 {
     return worker().run([c]() -> int {
         int rc = MPI_SUCCESS;
+        if (c->inter) {
+            free_intra(c->local);
+            free_intra(c->uni);
+            c->local = c->uni = nullptr;
+            return MPI_SUCCESS;
+        }
         if (c->tp) {
             rc = c->tp->barrier();                          // no peer still uses its windows
             transport_destroy(c->tp);

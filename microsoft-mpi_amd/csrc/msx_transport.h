@@ -62,6 +62,21 @@ public:
     // transport, used only by launches on stream(), which the transport
     // issues one collective at a time.  nullptr if allocation failed.
     virtual unsigned* push_counter() = 0;
+    // chunks sent to / received from each peer over the windows (the
+    // intercommunicator point-to-point channel; both sides count alike)
+    uint64_t& p2p_sent(int peer)
+    {
+        if (p2p_sent_.size() < (size_t)size) p2p_sent_.resize((size_t)size, 0);
+        return p2p_sent_[(size_t)peer];
+    }
+    uint64_t& p2p_recv(int peer)
+    {
+        if (p2p_recv_.size() < (size_t)size) p2p_recv_.resize((size_t)size, 0);
+        return p2p_recv_[(size_t)peer];
+    }
+
+private:
+    std::vector<uint64_t> p2p_sent_, p2p_recv_;
 };
 
 int transport_create(int rank, int size, Transport** out);
@@ -234,6 +249,23 @@ std::shared_future<int> engine_async(std::function<int()> fn);
 // its collectives): *out = the new communicator, or nullptr for
 // MPI_COMM_NULL (color MPI_UNDEFINED).  The handle is assigned by the caller.
 int engine_comm_split(Comm* parent, int color, int key, Comm** out);
+// World shared-memory mailbox (collective at MPI_Init, p > 1): small host
+// messages between any two processes, matched by (source process, tag).
+int engine_mailbox_init(Transport* world, int rank, int size);
+// MPI_Intercomm_create over `local` (collective over both groups); the
+// leaders exchange their groups through the mailbox.  `peer` / `remote_leader`
+// are significant at the local leader only.
+int engine_intercomm_create(Comm* local, int local_leader, Comm* peer, int remote_leader, int tag, Comm** out);
+int engine_intercomm_merge(Comm* inter, int high, Comm** out);
+int engine_intercomm_dup(Comm* inter, Comm** out);
+// Intercommunicator reductions (reduce.cpp:778-863, 1821-1990, 4109-4175):
+// root = MPI_ROOT / MPI_PROC_NULL / a remote rank as MPI_Reduce defines them.
+int engine_inter_reduce(Comm* ic, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                        const OpRef& op, int root);
+int engine_inter_allreduce(Comm* ic, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
+                           const OpRef& op);
+int engine_inter_reduce_scatter(Comm* ic, const void* sendbuf, void* recvbuf, const int* recvcounts,
+                                MPI_Datatype dt, const OpRef& op);
 // MPI_Comm_free (collective): tears down the communicator's transport.
 int engine_comm_free(Comm* c);
 

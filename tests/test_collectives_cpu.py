@@ -593,3 +593,127 @@ def test_groups_five_processes():
         assert inc == [4, 1, 3] and exc == [0, 2] and rinc == [4, 2, 0, 1] and rexc == [3]
         assert un == [4, 1, 3, 2, 0] and it == [4, 1] and df == [2, 0]
         assert sg == ([3, 1] if rank % 2 else [4, 2, 0])
+
+
+INTER_WORKER = r'''
+import ctypes, json, os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
+import msx
+C = msx.C
+L = msx.init(errors_return=True)
+r = ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r))
+rank = r.value
+W = C.MPI_COMM_WORLD
+I = lambda: ctypes.c_int()
+out = {}
+def world_ranks(g):
+    n = I(); L.MPI_Group_size(g, ctypes.byref(n))
+    wg = I(); L.MPI_Comm_group(W, ctypes.byref(wg))
+    a = (ctypes.c_int * max(n.value, 1))(*range(n.value)); o = (ctypes.c_int * max(n.value, 1))()
+    L.MPI_Group_translate_ranks(g, n.value, a, wg.value, o)
+    L.MPI_Group_free(ctypes.byref(wg))
+    return list(o)[:n.value]
+def members(comm):
+    g = I(); L.MPI_Comm_group(comm, ctypes.byref(g)); m = world_ranks(g.value); L.MPI_Group_free(ctypes.byref(g)); return m
+
+# A = {0, 1, 2}, B = {3, 4, 5}; B's leader is its local rank 1 (world 4)
+loc = I()
+assert L.MPI_Comm_split(W, 0 if rank < 3 else 1, rank, ctypes.byref(loc)) == 0
+inA = rank < 3
+ic = I()
+rc = L.MPI_Intercomm_create(loc.value, 0 if inA else 1, W, 4 if inA else 0, 7, ctypes.byref(ic))
+assert rc == 0, (rc, msx.last_error())
+f, n, rs, lr = I(), I(), I(), I()
+L.MPI_Comm_test_inter(ic.value, ctypes.byref(f)); L.MPI_Comm_size(ic.value, ctypes.byref(n))
+L.MPI_Comm_remote_size(ic.value, ctypes.byref(rs)); L.MPI_Comm_rank(ic.value, ctypes.byref(lr))
+rg = I(); assert L.MPI_Comm_remote_group(ic.value, ctypes.byref(rg)) == 0
+out["inter"] = [f.value, n.value, rs.value, lr.value, world_ranks(rg.value), members(ic.value)]
+L.MPI_Group_free(ctypes.byref(rg))
+cmp = []
+d = I(); assert L.MPI_Comm_dup(ic.value, ctypes.byref(d)) == 0
+for a, b in ((ic.value, ic.value), (ic.value, d.value), (ic.value, W)):
+    c = I(); L.MPI_Comm_compare(a, b, ctypes.byref(c)); cmp.append(c.value)
+out["compare"] = cmp
+L.MPI_Comm_test_inter(d.value, ctypes.byref(f)); out["dup_inter"] = f.value
+assert L.MPI_Barrier(ic.value) == 0 and L.MPI_Barrier(d.value) == 0
+# merges: A low, B high / both equal (rank 0's process id decides) / A high
+merged = []
+for ha, hb in ((0, 1), (0, 0), (1, 0)):
+    m = I()
+    assert L.MPI_Intercomm_merge(ic.value, ha if inA else hb, ctypes.byref(m)) == 0, msx.last_error()
+    mr, ms = I(), I(); L.MPI_Comm_rank(m.value, ctypes.byref(mr)); L.MPI_Comm_size(m.value, ctypes.byref(ms))
+    L.MPI_Comm_test_inter(m.value, ctypes.byref(f))
+    merged.append([mr.value, ms.value, f.value, members(m.value)])
+    assert L.MPI_Barrier(m.value) == 0
+    L.MPI_Comm_free(ctypes.byref(m))
+out["merge"] = merged
+# inconsistent high within a group
+m = I()
+out["merge_notsame"] = L.MPI_Intercomm_merge(ic.value, 1 if rank in (0, 3) else 0, ctypes.byref(m))
+buf = (ctypes.c_int * 4)()
+errs = [L.MPI_Comm_remote_size(W, ctypes.byref(n)), L.MPI_Intercomm_merge(W, 0, ctypes.byref(m)),
+        L.MPI_Scan(ctypes.c_void_p(ctypes.addressof(buf)), ctypes.c_void_p(ctypes.addressof(buf)), 0, C.MPI_INT,
+                   C.MPI_SUM, ic.value),
+        L.MPI_Win_create(ctypes.c_void_p(ctypes.addressof(buf)), 16, 4, C.MPI_INFO_NULL, ic.value, ctypes.byref(m)),
+        L.MPI_Comm_split(ic.value, 0, 0, ctypes.byref(m)),
+        L.MPI_Intercomm_create(loc.value, 7, W, 0, 1, ctypes.byref(m)),
+        L.MPI_Allreduce(ctypes.c_void_p(-1), ctypes.c_void_p(ctypes.addressof(buf)), 4, C.MPI_INT, C.MPI_SUM, ic.value),
+        L.MPI_Reduce(ctypes.c_void_p(ctypes.addressof(buf)), None, 4, C.MPI_INT, C.MPI_SUM, 3, ic.value),
+        L.MPI_Reduce(ctypes.c_void_p(ctypes.addressof(buf)), None, 4, C.MPI_INT, C.MPI_SUM, C.MPI_PROC_NULL, ic.value)]
+out["errs"] = errs
+# a second pair of intercommunicators through a peer communicator that does
+# not contain every process: P = {0..3} -> {0,1} x {2,3}; Q = {4,5} -> {4} x {5}
+pq = I(); assert L.MPI_Comm_split(W, 0 if rank < 4 else 1, rank, ctypes.byref(pq)) == 0
+pr = I(); L.MPI_Comm_rank(pq.value, ctypes.byref(pr))
+half = I()
+if rank < 4:
+    assert L.MPI_Comm_split(pq.value, pr.value // 2, pr.value, ctypes.byref(half)) == 0
+    remote = 2 if pr.value < 2 else 0
+else:
+    assert L.MPI_Comm_split(pq.value, pr.value, 0, ctypes.byref(half)) == 0
+    remote = 1 - pr.value
+ic2 = I()
+assert L.MPI_Intercomm_create(half.value, 0, pq.value, remote, 11, ctypes.byref(ic2)) == 0, msx.last_error()
+g2 = I(); L.MPI_Comm_remote_group(ic2.value, ctypes.byref(g2))
+out["ic2_remote"] = world_ranks(g2.value)
+L.MPI_Group_free(ctypes.byref(g2))
+for c in (ic2, half, pq, d, ic, loc):
+    assert L.MPI_Comm_free(ctypes.byref(c)) == 0 and c.value == C.MPI_COMM_NULL
+print("J", rank, json.dumps(out), flush=True)
+assert L.MPI_Finalize() == 0
+'''
+
+
+def test_intercommunicators_six_processes():
+    """MPI_Intercomm_create (api/mpi_comm.cpp:1482-1610: leaders exchange the
+    groups, here over the world mailbox; a peer communicator that does not
+    contain every process), MPI_Comm_remote_size / remote_group /
+    test_inter, MPI_Comm_compare on intercommunicators (api/mpi_comm.cpp:82-134),
+    MPI_Comm_dup, MPI_Barrier over both groups, MPI_Intercomm_merge ordering
+    (:1680-1830: high = false first; equal high -> the group whose rank 0 has
+    the lower process id first; **notsame), and the intracommunicator-only
+    checks.  No GPU: creation and synchronisation only."""
+    port = _free_port()
+    outs = _spawn(INTER_WORKER, 6, lambda r: {"MSX_SIZE": "6", "MSX_RANK": str(r), "MSX_BOOTSTRAP_PORT": str(port),
+                                             "MSX_BOOTSTRAP_ADDR": "127.0.0.1"})
+    for rc, o, e in outs:
+        assert rc == 0, (o + e)[-3000:]
+        line = [l for l in o.splitlines() if l.startswith("J ")][0].split(" ", 2)
+        rank, d = int(line[1]), json.loads(line[2])
+        A, B = [0, 1, 2], [3, 4, 5]
+        inA = rank < 3
+        assert d["inter"] == [1, 3, 3, rank % 3, B if inA else A, A if inA else B]
+        assert d["compare"] == [C.MPI_IDENT, C.MPI_CONGRUENT, C.MPI_UNEQUAL]
+        assert d["dup_inter"] == 1
+        m01, m00, m10 = d["merge"]
+        assert m01 == [rank, 6, 0, list(range(6))]
+        assert m00 == [rank, 6, 0, list(range(6))]
+        assert m10 == [(rank + 3) % 6, 6, 0, B + A]
+        assert d["merge_notsame"] == C.MPI_ERR_ARG
+        # remote_size / merge of an intracommunicator, scan / window / split of an
+        # intercommunicator, a local leader out of range, MPI_IN_PLACE allreduce
+        # on an intercommunicator, a root outside the remote group, MPI_PROC_NULL
+        assert d["errs"] == [C.MPI_ERR_COMM, C.MPI_ERR_COMM, C.MPI_ERR_COMM, C.MPI_ERR_COMM, C.MPI_ERR_COMM,
+                             C.MPI_ERR_RANK, C.MPI_ERR_BUFFER, C.MPI_ERR_ROOT, C.MPI_SUCCESS]
+        assert d["ic2_remote"] == {0: [2, 3], 1: [2, 3], 2: [0, 1], 3: [0, 1], 4: [5], 5: [4]}[rank]
