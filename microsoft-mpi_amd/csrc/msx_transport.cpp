@@ -3501,6 +3501,20 @@ int p2p_finish(Comm* u, int rc, int* err_host)
     return rc;
 }
 
+// The union's windows are mapped collectively (every member allocates and
+// imports), but a transfer between the groups involves only its two ends.  So
+// every member maps them while the whole union is present: when the
+// intercommunicator is created or duplicated.  Without a GPU there is nothing
+// to map (and no reduction can run).
+int map_union(Comm* u)
+{
+    if (device_count_noinit() <= 0) return MPI_SUCCESS;
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    Windows w;
+    return get_windows(u->tp, &w, true);
+}
+
 // union rank of rank r of the local (mine = true) or remote group
 int urank_of(const Comm* ic, bool mine, int r)
 {
@@ -3692,6 +3706,11 @@ int engine_intercomm_create(Comm* local, int leader, Comm* peer, int remote_lead
         u->lpid = low ? local->lpid : rem;
         const std::vector<int>& second = low ? rem : local->lpid;
         u->lpid.insert(u->lpid.end(), second.begin(), second.end());
+        rc = map_union(u);
+        if (rc != MPI_SUCCESS) {
+            free_intra(u);
+            return rc;
+        }
         // 4. the intercommunicator's own local group
         Comm* lc = nullptr;
         rc = dup_intra(local, &lc);
@@ -3758,8 +3777,10 @@ int engine_intercomm_dup(Comm* ic, Comm** out)
         Comm *lc = nullptr, *u = nullptr;
         int rc = dup_intra(ic->local, &lc);
         if (rc == MPI_SUCCESS) rc = dup_intra(ic->uni, &u);
+        if (rc == MPI_SUCCESS) rc = map_union(u);
         if (rc != MPI_SUCCESS) {
             free_intra(lc);
+            free_intra(u);
             return rc;
         }
         auto* n = new Comm();

@@ -1,0 +1,197 @@
+"""GPU: reductions on intercommunicators, 5 ranks sharing one GPU.
+
+Group A = world {0, 1}, group B = world {2, 3, 4}, joined by
+MPI_Intercomm_create over MPI_COMM_WORLD.  The reference's inter algorithms
+(reduce.cpp:778-863 MPIR_Reduce_inter, 1852-1990 MPIR_Reduce_scatter_inter,
+4109-4175 MPIR_Allreduce_inter) reduce the REMOTE group's data to its rank 0
+with MPIR_Reduce_intra and send it across; so every expected value is the
+oracle's step-by-step reduce schedule (root 0) over the remote group's inputs,
+bit for bit (fp32 / fp64 SUM included).  MSX_CHUNK_BYTES is small so one
+transfer across the groups takes many chunks and the point-to-point channel's
+acknowledgements gate the reuse of its halves."""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+import msx
+
+pytestmark = pytest.mark.gpu
+REPO = msx.REPO_ROOT
+
+WORKER = r'''
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd")); sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np, torch
+import msx, oracle
+from _cases import gen, KIND
+C = msx.C
+L = msx.init(errors_return=True)
+r_ = ctypes.c_int()
+L.MPI_Comm_rank(C.MPI_COMM_WORLD, ctypes.byref(r_))
+rank = r_.value
+W = C.MPI_COMM_WORLD
+A, B = [0, 1], [2, 3, 4]
+inA = rank in A
+mine, other = (A, B) if inA else (B, A)
+lr = mine.index(rank)
+fails = []
+
+def ok(rc, tag):
+    print("done", tag, rc, file=sys.stderr, flush=True)
+    if rc:
+        fails.append(f"{tag} rc={rc} {msx.last_error()}")
+    return rc == 0
+
+def raw(a):
+    return np.frombuffer(bytearray(a.tobytes()), dtype=a.dtype)
+
+def todev(a):
+    t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
+    if a.nbytes:
+        t.copy_(torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()))
+    torch.cuda.synchronize()      # the library's streams do not order after torch's
+    return t
+
+def fromdev(t, like, n=None):
+    n = like.size if n is None else n
+    return np.frombuffer(bytearray(t[: n * like.dtype.itemsize].cpu().numpy().tobytes()), like.dtype)
+
+def check(tag, got, exp):
+    print("step", tag, file=sys.stderr, flush=True)
+    if got.tobytes() != exp.tobytes():
+        fails.append(tag)
+
+def inputs(opn, dtn, count, seed):
+    rng = np.random.default_rng(seed)
+    return [raw(gen(KIND[dtn], opn, count, rng)) for _ in range(5)]
+
+def remote_reduce(op, dt, xs, group):
+    # MPIR_Reduce_intra of `group` (local ranks in world order) to its rank 0
+    e = np.zeros_like(xs[0])
+    assert oracle.reduce(op, dt, 0, [xs[r] for r in group], e) == 0
+    return e
+
+loc = ctypes.c_int()
+ok(L.MPI_Comm_split(W, 0 if inA else 1, rank, ctypes.byref(loc)), "split")
+ic = ctypes.c_int()
+ok(L.MPI_Intercomm_create(loc.value, 0, W, B[0] if inA else A[0], 9, ctypes.byref(ic)), "intercomm_create")
+IC = ic.value
+
+CASES = [("MPI_SUM", "MPI_FLOAT", 1000), ("MPI_SUM", "MPI_FLOAT", 300001), ("MPI_SUM", "MPI_DOUBLE", 70001),
+         ("MPI_MAX", "MPI_DOUBLE", 50), ("MPI_BXOR", "MPI_INT", 262144), ("MPI_MAXLOC", "MPI_FLOAT_INT", 4099),
+         ("MPI_PROD", "MPI_C_FLOAT_COMPLEX", 2048), ("MPI_BAND", "MPI_UINT64_T", 131072)]
+for i, (opn, dtn, count) in enumerate(CASES):
+    op, dt = getattr(C, opn), getattr(C, dtn)
+    xs = inputs(opn, dtn, count, 500 + i)
+    send = todev(xs[rank])
+    # MPI_Reduce into A's local rank 1 (B sends), then into B's local rank 2 (A sends)
+    for root_group, root_lr in ((A, 1), (B, 2)):
+        recv = todev(np.zeros_like(xs[0]))
+        if (rank in root_group):
+            root = C.MPI_ROOT if lr == root_lr else C.MPI_PROC_NULL
+        else:
+            root = root_lr
+        ok(L.MPI_Reduce(send.data_ptr(), recv.data_ptr(), count, dt, op, root, IC), f"reduce {opn} {dtn} {count}")
+        if root == C.MPI_ROOT:
+            check(f"reduce {opn} {dtn} {count} into {root_group}", fromdev(recv, xs[0]),
+                  remote_reduce(op, dt, xs, other))
+    # MPI_Allreduce: each group receives the other group's reduction
+    recv = todev(np.zeros_like(xs[0]))
+    ok(L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), count, dt, op, IC), f"allreduce {opn} {dtn} {count}")
+    check(f"allreduce {opn} {dtn} {count}", fromdev(recv, xs[0]), remote_reduce(op, dt, xs, other))
+
+# host buffers (pageable numpy arrays) and the non-blocking form
+xs = inputs("MPI_SUM", "MPI_FLOAT", 200000, 77)
+hsend = xs[rank].copy(); hrecv = np.zeros_like(hsend)
+ok(L.MPI_Allreduce(hsend.ctypes.data, hrecv.ctypes.data, hsend.size, C.MPI_FLOAT, C.MPI_SUM, IC), "host allreduce")
+check("host allreduce", hrecv, remote_reduce(C.MPI_SUM, C.MPI_FLOAT, xs, other))
+send = todev(xs[rank]); recv = todev(np.zeros_like(xs[0]))
+req = ctypes.c_int()
+ok(L.MPI_Iallreduce(send.data_ptr(), recv.data_ptr(), xs[0].size, C.MPI_FLOAT, C.MPI_SUM, IC, ctypes.byref(req)),
+   "iallreduce")
+ok(L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)), "wait")
+check("iallreduce", fromdev(recv, xs[0]), remote_reduce(C.MPI_SUM, C.MPI_FLOAT, xs, other))
+
+# MPI_Reduce_scatter: both groups' recvcounts total T; my group's block r of the
+# other group's reduction lands on my local rank r (a zero count included)
+T = 60000
+counts = {0: [20000, 40000], 1: [15000, 0, 45000]}[0 if inA else 1]
+xs = inputs("MPI_SUM", "MPI_DOUBLE", T, 88)
+full = remote_reduce(C.MPI_SUM, C.MPI_DOUBLE, xs, other)
+send = todev(xs[rank]); recv = todev(np.zeros(max(counts[lr], 1), np.float64))
+ok(L.MPI_Reduce_scatter(send.data_ptr(), recv.data_ptr(), (ctypes.c_int * len(counts))(*counts), C.MPI_DOUBLE,
+                        C.MPI_SUM, IC), "reduce_scatter")
+o = sum(counts[:lr])
+check("reduce_scatter", fromdev(recv, full, counts[lr]), full[o:o + counts[lr]])
+# MPI_Reduce_scatter_block: recvcount 3k in A (2 ranks) and 2k in B (3 ranks)
+k = 4096
+rc_blk = 3 * k if inA else 2 * k
+xs = inputs("MPI_MAX", "MPI_INT", 6 * k, 99)
+full = remote_reduce(C.MPI_MAX, C.MPI_INT, xs, other)
+send = todev(xs[rank]); recv = todev(np.zeros(rc_blk, np.int32))
+ok(L.MPI_Reduce_scatter_block(send.data_ptr(), recv.data_ptr(), rc_blk, C.MPI_INT, C.MPI_MAX, IC), "rsb")
+check("reduce_scatter_block", fromdev(recv, full, rc_blk), full[lr * rc_blk:(lr + 1) * rc_blk])
+
+# the merged intracommunicator runs the ordinary GPU schedules (B first: high)
+m = ctypes.c_int()
+ok(L.MPI_Intercomm_merge(IC, 0 if inA else 1, ctypes.byref(m)), "merge")
+order = A + B
+xs = inputs("MPI_SUM", "MPI_FLOAT", 100003, 111)
+send = todev(xs[rank]); recv = todev(np.zeros_like(xs[0]))
+ok(L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), xs[0].size, C.MPI_FLOAT, C.MPI_SUM, m.value), "merged allreduce")
+e = np.zeros_like(xs[0])
+oracle.allreduce(C.MPI_SUM, C.MPI_FLOAT, [xs[r] for r in order], [e if r == rank else np.zeros_like(e) for r in order])
+check("merged allreduce", fromdev(recv, xs[0]), e)
+ok(L.MPI_Comm_free(ctypes.byref(m)), "free merged")
+ok(L.MPI_Comm_free(ctypes.byref(ic)), "free intercomm")
+ok(L.MPI_Comm_free(ctypes.byref(loc)), "free local")
+print("RESULT", rank, 5, len(fails), fails[:5], flush=True)
+L.MPI_Finalize()
+'''
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("chunk", [None, 1 << 20])
+def test_intercommunicator_reductions_five_ranks(chunk):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = _free_port()
+    procs = []
+    for r in range(5):
+        env = dict(os.environ)
+        env.update({"MSX_SIZE": "5", "MSX_RANK": str(r), "MSX_DEVICE": "0",
+                    "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
+                    "MSX_BOOTSTRAP_TIMEOUT": "180"})
+        if chunk:
+            env["MSX_CHUNK_BYTES"] = str(chunk)     # transfers across the groups take many chunks
+        procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    results = []
+    deadline = time.monotonic() + 150        # one hung rank must not hold the others
+    for pr in procs:
+        try:
+            o, e = pr.communicate(timeout=max(1.0, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            o, e = pr.communicate()
+        results.append((pr.returncode, o, e))
+    for rc, o, e in results:
+        assert rc == 0, (o + e)[-3000:]
+        line = [l for l in o.splitlines() if l.startswith("RESULT")]
+        assert line, (o + e)[-3000:]
+        assert line[0].split()[3] == "0", line[0]
