@@ -362,8 +362,10 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
     out["tree8/MPI_SUM/MPI_FLOAT"] = entry(time_tree())
     out["tree8_pow2_stride/MPI_SUM/MPI_FLOAT"] = entry(time_tree(srcs_pow2))
     if tree_sweep:
-        for mode, name in enumerate(("interleaved", "upfront", "upfront_nt", "interleaved_nt")):
-            for cap in (1024, 2048, 4096, 8192, 65536):
+        for mode, name in ((8, "generic"), (1, "generic_upfront"), (2, "generic_upfront_nt"),
+                           (3, "generic_interleaved_nt"), (4, "fixed_u1"), (5, "fixed_u2"), (6, "fixed_u4"),
+                           (7, "fixed_u2_nt")):
+            for cap in (0, 1024, 4096, 65536):
                 L.msx_tune_tree(mode, cap)
                 out[f"tree8_sweep/{name}/cap{cap}"] = entry(time_tree())
         L.msx_tune_tree(0, 0)

@@ -88,9 +88,12 @@ int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count
 int msx_tune_set(int variant, int grid_cap);
 int msx_tune_variant_count(void);
 /* collective tree combine (msx_reduce_tree_dev and the engine), fp32 SUM only:
- * mode 0 = default (loads interleaved with the combines), 1 = all sources
- * loaded up front, 2 = up front + non-temporal, 3 = interleaved +
- * non-temporal; grid_cap 0 = default. */
+ * mode 0 = default (compile-time source count for full trees and chains of
+ * 2/4/8 sources, else the generic kernel), 1 = generic with all sources
+ * loaded up front, 2 = up front + non-temporal, 3 = generic interleaved +
+ * non-temporal, 4/5/6 = compile-time source count with 1/2/4 vectors per lane,
+ * 7 = as 5 with non-temporal loads, 8 = generic kernel (loads interleaved with
+ * the combines); grid_cap 0 = default. */
 int msx_tune_tree(int mode, int grid_cap);
 const char* msx_tune_variant_name(int variant);
 /* HBM ceiling probe (measurement only): the default combine's launch geometry
@@ -98,6 +101,10 @@ const char* msx_tune_variant_name(int variant);
  * pointers): mode 0 reads a and b, 1 writes b, 2 copies a -> b, 3 reads a.
  * Stream-ordered; b's contents are unspecified afterwards. */
 int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream);
+/* device allocation for measurements: uncached = the engine windows' memory
+ * type (hipDeviceMallocUncached), else plain hipMalloc; msx_probe_free releases */
+int msx_probe_alloc(int64_t bytes, int uncached, void** out);
+int msx_probe_free(void* p);
 
 /* host staging chunk size (bytes) for MPI_Reduce_local on host buffers */
 int msx_set_staging_chunk(int64_t bytes);

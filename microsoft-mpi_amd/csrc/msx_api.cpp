@@ -2230,6 +2230,24 @@ MSX_EXPORT int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, vo
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "probe launch");
 }
 
+// Device memory with the engine windows' cache type (measurement only): the
+// collective trees read uncached window memory, so the bench times them there.
+MSX_EXPORT int msx_probe_alloc(int64_t bytes, int uncached, void** out)
+{
+    if (bytes <= 0 || !out) return MPI_ERR_ARG;
+    *out = nullptr;
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    hipError_t e = uncached ? hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached)
+                            : hipMalloc(out, (size_t)bytes);
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "probe allocation");
+}
+
+MSX_EXPORT int msx_probe_free(void* p)
+{
+    return p && hipFree(p) != hipSuccess ? MPI_ERR_ARG : MPI_SUCCESS;
+}
+
 MSX_EXPORT int msx_tune_variant_count(void) { return combine_variant_count(); }
 MSX_EXPORT const char* msx_tune_variant_name(int v) { return combine_variant_name(v); }
 

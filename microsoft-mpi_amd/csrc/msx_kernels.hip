@@ -230,387 +230,13 @@ __global__ __launch_bounds__(BLOCK) void k_combine_lds(const T* __restrict__ in,
     }
 }
 
-// ---- copy-segment and flag descriptors (k_copy_segs, k_push_post, k_tree) -------
-constexpr int kMaxSegs = 32;
-struct CopySegs {
-    const void* src[kMaxSegs];
-    void* dst[kMaxSegs];
-    size_t nbytes[kMaxSegs];
-    int n;
-    int sys;
-};
+}  // namespace dev
+}  // namespace msx
 
-struct PostFlags {
-    unsigned long long* dst[64];
-    unsigned long long seq;
-    int n;
-};
+#include "msx_tree_dev.h"
 
-// "This lane's stores have completed" without a cache maintenance operation:
-// s_waitcnt vmcnt(0) (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  An
-// agent-scope release fence would do the same wait but also write back the
-// whole XCD L2 (buffer_wbl2), once per workgroup -- on this multi-XCD part
-// that made a 2048-workgroup push 20x slower.  Window memory is uncached
-// (MTYPE_UC), so a completed store is at the owner; nothing sits in L2.
-__device__ __forceinline__ void stores_done()
-{
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);      // no compiler motion of stores past the wait
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// The small-allreduce push (k_push_post, and the first workgroups of a fused
-// k_tree launch): see the comment at k_push_post.
-__device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
-                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
-{
-    const char* src = static_cast<const char*>(c.src[sg]);
-    char* dst = static_cast<char*>(c.dst[sg]);
-    const size_t nb = c.nbytes[sg];
-    const size_t stride = (size_t)gx * 256;
-    size_t done = 0;
-    bool plain = false;
-    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
-        const size_t nv = nb / 16;
-        for (size_t i = (size_t)bx * 256 + threadIdx.x; i < nv; i += stride) {
-            const u32x4 v = reinterpret_cast<const u32x4*>(src)[i];
-            unsigned long long* d = reinterpret_cast<unsigned long long*>(dst) + 2 * i;
-            __hip_atomic_store(d, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(d + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        done = nv * 16;
-    }
-    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) {
-        dst[i] = src[i];
-        plain = true;
-    }
-    if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
-    else stores_done();                                 // vmcnt(0): this lane's stores completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == total - 1) {
-            if (sys) __threadfence_system();
-            for (int k = 0; k < f.n; ++k)
-                __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
-        }
-    }
-}
-
-// Count finished workgroup b of nb; true in exactly one workgroup, after all
-// nb have counted.  Thousands of workgroups adding to ONE word serialise
-// (a 4096-workgroup tree took 70 us instead of 38), so workgroup b counts on
-// sub-counter b % kCountSubs (its own 64-byte line, base[kCountSubBase +
-// 16 i]) and only the last of each sub-counter counts on base[0].  Relaxed:
-// each add is issued after the workgroup's stores completed (stores_done),
-// so when the last add is seen, all of them have.  Words are left zero.
-__device__ __forceinline__ bool count_done(unsigned* base, unsigned b, unsigned nb)
-{
-    const unsigned i = b % kCountSubs;
-    const unsigned nsub = nb < kCountSubs ? nb : kCountSubs;
-    const unsigned want = (nb - i + kCountSubs - 1) / kCountSubs;   // workgroups on sub-counter i
-    unsigned* c = base + kCountSubBase + 16 * i;
-    if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want - 1) return false;
-    __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(base, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nsub - 1) return false;
-    __hip_atomic_store(base, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-}
-
-// Bulk variant for multi-MiB segments (the two-step allreduce's pieces): plain
-// 16-byte stores from a full grid, four loads in flight per lane (as
-// k_copy_segs), then push_post_body's fenced count and flag post.  Plain
-// stores to peer windows rely on the windows' uncached mapping like every
-// other bulk transfer of the engine; `sys` (cached windows) writes the L2
-// back at system scope before counting.
-__device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
-                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
-{
-    const char* src = static_cast<const char*>(c.src[sg]);
-    char* dst = static_cast<char*>(c.dst[sg]);
-    const size_t nb = c.nbytes[sg];
-    const size_t stride = (size_t)gx * 256;
-    size_t done = 0;
-    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
-        const size_t nv = nb / 16;
-        const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-        u32x4* d4 = reinterpret_cast<u32x4*>(dst);
-        size_t i = (size_t)bx * 256 + threadIdx.x;
-        for (; i + 3 * stride < nv; i += 4 * stride) {
-            const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
-            d4[i] = a0; d4[i + stride] = a1; d4[i + 2 * stride] = a2; d4[i + 3 * stride] = a3;
-        }
-        for (; i < nv; i += stride) d4[i] = s4[i];
-        done = nv * 16;
-    }
-    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
-    if (sys) __threadfence_system();
-    else stores_done();
-    __syncthreads();
-    // counter: a kCountWords block (count_done); b = this workgroup's index
-    if (threadIdx.x == 0 && count_done(counter, (unsigned)sg + bx * (unsigned)c.n, total)) {
-        if (sys) __threadfence_system();
-        for (int k = 0; k < f.n; ++k)
-            __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-// ---- reference-order multi-input combine ----------------------------------------
-// One pass over up to 2*kMaxLeaves inputs that reproduces the association AND
-// the inout/in roles of the reference's multi-step schedules:
-//   tree  (chain == 0): leaf_k = pair_k ? f(s[2k], s[2k+1]) : s[2k], k < P (pow2),
-//         then the balanced tree ((l0 op l1) op (l2 op l3)) op ... with the left
-//         operand always in the `inout` role (recursive doubling / halving,
-//         reduce.cpp:3890-4009, 1088-1175; the non-power-of-two fold is the
-//         leaf pair, reduce.cpp:3835-3871);
-//   chain (chain == 1): ((s0 op s1) op s2) op ... op s[P-1] (pairwise exchange,
-//         reduce.cpp:1258-1318).
-constexpr int kMaxLeaves = 16;
-constexpr int kMaxExtraOut = 31;
-struct TreeArgs {
-    const void* s[2 * kMaxLeaves];
-    void* extra[kMaxExtraOut];   // further destinations of the result (peer windows)
-    int nextra;
-    int P;
-    int nleaves;   // leaves present (<= P); the rest of the P-leaf tree is empty
-    unsigned pairmask;
-    int chain;
-    int sys;   // sources/outputs shared with other GPUs: system-coherent access
-    const unsigned long long* wait_flags;   // see TreeSpec
-    unsigned long long wait_seq;
-    int wait_n;
-    int wait_skip;
-    int* wait_err;
-    // fused push (barrier-free small allreduce): the first npush workgroups
-    // copy this rank's contribution into the peers' IN halves and post the
-    // arrival flags (push_post_body) instead of evaluating the tree
-    unsigned npush;
-    unsigned push_gx;     // workgroups per push segment
-    int push_sys;
-    unsigned* push_counter;
-    CopySegs push;
-    PostFlags flags;
-    // result-ready flags (barrier-free two-step allreduce): once every tree
-    // workgroup of all `done_launches` launches has stored its results, post
-    // done_flags (see tree_done)
-    unsigned* done_counter;       // kCountWords block: [0] count_done, [1] launches done
-    unsigned done_launches;
-    PostFlags done_flags;
-};
-
-// End of a tree workgroup when the launch posts result-ready flags: the
-// threadFenceReduction pattern of push_post_body, extended over the launches
-// that together evaluate one call (stream-ordered, so at most one is in
-// flight).  Every lane waits for its own stores (stores_done; cached windows:
-// system fence), thread 0 counts the workgroup, the launch's last workgroup
-// counts the launch, and the last workgroup of the last launch posts the
-// flags with system-scope release stores.  Both words are left zero for the
-// next call.
-__device__ __forceinline__ void tree_done(const TreeArgs& a, unsigned b, unsigned nb)
-{
-    if (a.sys) __threadfence_system();
-    else stores_done();
-    __syncthreads();
-    if (threadIdx.x != 0 || !count_done(a.done_counter, b, nb)) return;
-    // launches of the call: word 1 of the block
-    const unsigned l = __hip_atomic_fetch_add(a.done_counter + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (l != a.done_launches - 1) return;
-    __hip_atomic_store(a.done_counter + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.sys) __threadfence_system();
-    for (int k = 0; k < a.done_flags.n; ++k)
-        __hip_atomic_store(a.done_flags.dst[k], a.done_flags.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Arrival wait of the barrier-free small allreduce: thread 0 of every
-// workgroup polls the peers' flags (uncached window memory, system-scope
-// loads) until each reaches the call's sequence number.  Bounded: after
-// ~20 s (s_memrealtime runs at 100 MHz) it reports through *wait_err and the
-// workgroup exits, so a missing peer can never leave a wave running.
-__device__ __forceinline__ bool wait_flags_body(const unsigned long long* flags, unsigned long long seq, int n,
-                                                int skip, int* err)
-{
-    __shared__ int ok;
-    if (threadIdx.x == 0) {
-        int good = 1;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        for (int r = 0; r < n && good; ++r) {
-            if (r == skip) continue;
-            while (__hip_atomic_load(flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
-                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    good = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        // The acquire that pairs with the pusher's system-scope release of the
-        // flag: invalidates this CU's L1 and the XCD's L2 copies of peer-written
-        // lines, so the IN half is read fresh whatever cache type the window
-        // is mapped with (the UC mapping makes it a no-op for the data today,
-        // but the kernel no longer depends on that allocation property).
-        if (good) (void)__hip_atomic_load(flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        ok = good;
-    }
-    __syncthreads();
-    return ok != 0;
-}
-
-__device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
-{
-    return wait_flags_body(a.wait_flags, a.wait_seq, a.wait_n, a.wait_skip, a.wait_err);
-}
-
-// Start-of-kernel system acquire: invalidate this CU's L1 and the XCD's L2
-// lines for memory other GPUs may have written since (peer HBM over xGMI).
-__device__ __forceinline__ void acquire_system()
-{
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    __syncthreads();
-}
-
-// End-of-kernel system release: write this XCD's dirty L2 lines back so peers
-// reading over xGMI see them (one fence per workgroup).
-__device__ __forceinline__ void release_system()
-{
-    __syncthreads();
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-}
-
-template <class F, class V, class LD>
-__device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
-{
-    if (a.chain) {
-        // every source loaded before the first combine (the loop bound is a
-        // runtime value: a rolled loop waited for each load in turn, 75 us
-        // instead of 8 us for a 4-rank 1 MiB reduce_scatter); same order
-        V x[kMaxLeaves];
-#pragma unroll
-        for (int k = 0; k < kMaxLeaves; ++k)
-            if (k < a.P) x[k] = load(k);
-        V v = x[0];
-#pragma unroll
-        for (int k = 1; k < kMaxLeaves; ++k)
-            if (k < a.P) v = F::apply(v, x[k]);
-        return v;
-    }
-    // leaves >= nleaves are absent (binomial trees over a non-power-of-two p):
-    // a node whose right subtree is empty passes its left value up unchanged.
-    V v[kMaxLeaves];
-#pragma unroll
-    for (int k = 0; k < kMaxLeaves; ++k) {
-        if (k < a.nleaves) {
-            v[k] = load(2 * k);
-            if ((a.pairmask >> k) & 1u) v[k] = F::apply(v[k], load(2 * k + 1));
-        }
-    }
-#pragma unroll
-    for (int w = 1; w < kMaxLeaves; w *= 2) {
-#pragma unroll
-        for (int k = 0; k + w < kMaxLeaves; k += 2 * w)
-            if (k + w < a.nleaves) v[k] = F::apply(v[k], v[k + w]);
-    }
-    return v[0];
-}
-
-// The same tree over 16-byte vectors, with every source vector loaded
-// (non-temporal: each is read once) before the first combine, so all of them
-// are in flight together.
-template <class F, bool NT>
-__device__ __forceinline__ u32x4 tree_vec(const TreeArgs& a, size_t i)
-{
-    auto ld_src = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
-    u32x4 v[kMaxLeaves], w[kMaxLeaves];
-    if (a.chain) {
-#pragma unroll
-        for (int k = 0; k < kMaxLeaves; ++k)
-            if (k < a.P) v[k] = ld_src(k);
-        __builtin_amdgcn_sched_barrier(0);
-        u32x4 r = v[0];
-#pragma unroll
-        for (int k = 1; k < kMaxLeaves; ++k)
-            if (k < a.P) r = F::apply(r, v[k]);
-        return r;
-    }
-#pragma unroll
-    for (int k = 0; k < kMaxLeaves; ++k) {
-        if (k < a.nleaves) {
-            v[k] = ld_src(2 * k);
-            if ((a.pairmask >> k) & 1u) w[k] = ld_src(2 * k + 1);
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < kMaxLeaves; ++k)
-        if (k < a.nleaves && ((a.pairmask >> k) & 1u)) v[k] = F::apply(v[k], w[k]);
-#pragma unroll
-    for (int d = 1; d < kMaxLeaves; d *= 2) {
-#pragma unroll
-        for (int k = 0; k + d < kMaxLeaves; k += 2 * d)
-            if (k + d < a.nleaves) v[k] = F::apply(v[k], v[k + d]);
-    }
-    return v[0];
-}
-
-template <int OP, class VT> struct VecFn {
-    __device__ static u32x4 apply(u32x4 io, u32x4 in) { return apply_vec<OP, VT>(io, in); }
-};
-
-// UPFRONT: all source vectors loaded before the first combine (tree_vec), else
-// loads interleaved with the combines as the tree consumes them (tree_eval);
-// NT: non-temporal source loads.  The fp32 SUM tuning sweep times all four
-// (p = 8, 32 MiB each): interleaved plain loads 51.7 us (5.8 TB/s), up front
-// 57.1 us -- holding every source vector costs 146 VGPRs instead of 77, half
-// the waves per SIMD -- and non-temporal loads 3-8 % slower either way.
-template <int OP, class T, class VT, int BLOCK, bool UPFRONT = false, bool NT = false>
-__global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out, size_t nvec,
-                                                size_t tail, int vec_ok)
-{
-    constexpr size_t EPV = 16 / sizeof(T);
-    unsigned b = blockIdx.x, nb = gridDim.x;
-    if (a.npush) {
-        // fused push: the first npush workgroups push this rank's vector and
-        // post its flags; they never wait, so the peers' trees always progress
-        if (b < a.npush) {
-            // segment b % n: every peer's push starts at once (see k_copy_segs)
-            const unsigned ns = (unsigned)a.push.n;
-            push_post_body(a.push, a.flags, a.push_counter, a.npush, a.push_sys, b / ns, a.push_gx, (int)(b % ns));
-            return;
-        }
-        b -= a.npush;
-        nb -= a.npush;
-    }
-    const size_t stride = (size_t)nb * BLOCK;
-    const size_t bid = xcd_tile(b, nb);      // XCD-contiguous (see combine_body)
-    if (a.wait_flags && !arrival_wait(a)) return;
-    if (a.sys) acquire_system();
-    if (vec_ok) {
-        for (size_t i = bid * BLOCK + threadIdx.x; i < nvec; i += stride) {
-            u32x4 r;
-            if constexpr (UPFRONT) {
-                r = tree_vec<VecFn<OP, VT>, NT>(a, i);
-            } else {
-                auto load = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
-                r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
-            }
-            reinterpret_cast<u32x4*>(out)[i] = r;
-            for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
-        }
-    }
-    const size_t first = vec_ok ? nvec * EPV : 0;
-    const size_t nsc = vec_ok ? tail : tail + nvec * EPV;
-    for (size_t s = (size_t)b * BLOCK + threadIdx.x; s < nsc; s += stride) {
-        auto load = [&](int k) { return reinterpret_cast<const T*>(a.s[k])[first + s]; };
-        const T r = tree_eval<Fn<OP>, T>(a, load);
-        out[first + s] = r;
-        for (int e = 0; e < a.nextra; ++e) static_cast<T*>(a.extra[e])[first + s] = r;
-    }
-    if (a.sys) release_system();
-    if (a.done_counter) tree_done(a, b, nb);
-}
+namespace msx {
+namespace dev {
 
 // ---- multi-segment copy (allgather phase: blocks pulled from peers) -------------
 __global__ __launch_bounds__(64) void k_post_flags(PostFlags f)
@@ -698,7 +324,6 @@ using namespace dev;
 
 constexpr int kBlock = 256;
 constexpr int kUnroll = 1;
-constexpr int kTreeGridCap = 4096;
 
 template <class T>
 inline void split(const void* in, const void* io, size_t count, size_t& head, size_t& nvec,
@@ -876,74 +501,13 @@ hipError_t dispatch_loc(Kind k, const void* in, void* io, size_t n, hipStream_t 
     }
 }
 
-// ---- tree dispatch ----
-TreeTune g_tree_tune;
-
-template <int OP, class T, class VT, bool UPFRONT = false, bool NT = false>
-hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
-{
-    bool ok = ((uintptr_t)out & 15) == 0;
-    for (int k = 0; k < nsrc; ++k) ok = ok && a.s[k] && (((uintptr_t)a.s[k] & 15) == 0);
-    for (int e = 0; e < a.nextra; ++e) ok = ok && (((uintptr_t)a.extra[e] & 15) == 0);
-    constexpr size_t ES = sizeof(T);
-    const size_t epv = 16 / ES;
-    const size_t nvec = count / epv, tail = count - nvec * epv;
-    const size_t work = ok ? nvec + tail : count;
-    size_t grid = (work + kBlock - 1) / kBlock;
-    const size_t cap = g_tree_tune.grid_cap > 0 ? (size_t)g_tree_tune.grid_cap : (size_t)kTreeGridCap;
-    if (grid > cap) grid = cap;
-    if (grid == 0) return hipSuccess;
-    grid += a.npush;                         // fused push workgroups come first
-    hipLaunchKernelGGL((k_tree<OP, T, VT, kBlock, UPFRONT, NT>), dim3((unsigned)grid), dim3(kBlock), 0, s, a,
-                       static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
-    return hipGetLastError();
-}
-
-template <int OP>
-hipError_t tree_arith(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
-{
-    switch (k) {
-    case K_I8:  return run_tree<OP, int8_t, int8_t>(a, ns, out, n, s);
-    case K_U8:  return run_tree<OP, uint8_t, uint8_t>(a, ns, out, n, s);
-    case K_I16: return run_tree<OP, int16_t, int16_t>(a, ns, out, n, s);
-    case K_U16: return run_tree<OP, uint16_t, uint16_t>(a, ns, out, n, s);
-    case K_I32: return run_tree<OP, int32_t, int32_t>(a, ns, out, n, s);
-    case K_U32: return run_tree<OP, uint32_t, uint32_t>(a, ns, out, n, s);
-    case K_I64: return run_tree<OP, int64_t, int64_t>(a, ns, out, n, s);
-    case K_U64: return run_tree<OP, uint64_t, uint64_t>(a, ns, out, n, s);
-    case K_F32: return run_tree<OP, float, float>(a, ns, out, n, s);
-    case K_F64: return run_tree<OP, double, double>(a, ns, out, n, s);
-    default: break;
-    }
-    if constexpr (OP == O_SUM || OP == O_PROD) {
-        if (k == K_C32) return run_tree<OP, c32, c32>(a, ns, out, n, s);
-        if (k == K_C64) return run_tree<OP, c64, c64>(a, ns, out, n, s);
-    }
-    if constexpr (OP == O_LAND || OP == O_LOR || OP == O_LXOR) {
-        if (k == K_BOOL) return run_tree<OP, uint8_t, uint8_t>(a, ns, out, n, s);
-    }
-    return hipErrorInvalidValue;
-}
-
-template <int OP>
-hipError_t tree_loc(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
-{
-    switch (k) {
-    case K_LOC_II: return run_tree<OP, loc_ii, loc_ii>(a, ns, out, n, s);
-    case K_LOC_FI: return run_tree<OP, loc_fi, loc_fi>(a, ns, out, n, s);
-    case K_LOC_SI: return run_tree<OP, loc_si, loc_si>(a, ns, out, n, s);
-    case K_LOC_DI: return run_tree<OP, loc_di, loc_di>(a, ns, out, n, s);
-    case K_LOC_FF: return run_tree<OP, loc_ff, loc_ff>(a, ns, out, n, s);
-    case K_LOC_DD: return run_tree<OP, loc_dd, loc_dd>(a, ns, out, n, s);
-    default: return hipErrorInvalidValue;
-    }
-}
-
 }  // namespace
+
+TreeTune g_tree_tune;
 
 int tree_tune_set(int mode, int grid_cap)
 {
-    if (mode < 0 || mode > 3 || grid_cap < 0) return -1;
+    if (mode < 0 || mode > 8 || grid_cap < 0) return -1;
     g_tree_tune.mode = mode;
     g_tree_tune.grid_cap = grid_cap;
     return 0;
@@ -1063,27 +627,20 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         if (t.src[0] == out) return hipSuccess;
         return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
     }
-    if (opidx == O_SUM && k == K_F32 && g_tree_tune.mode != 0) {
-        switch (g_tree_tune.mode) {
-        case 1: return run_tree<O_SUM, float, float, true, false>(a, ns, out, n, s);
-        case 2: return run_tree<O_SUM, float, float, true, true>(a, ns, out, n, s);
-        case 3: return run_tree<O_SUM, float, float, false, true>(a, ns, out, n, s);
-        default: return hipErrorInvalidValue;
-        }
-    }
+    if (opidx == O_SUM && k == K_F32 && g_tree_tune.mode != 0) return tree_tune_f32_sum(g_tree_tune.mode, a, ns, out, n, s);
     switch (opidx) {
-    case O_SUM:  return tree_arith<O_SUM>(k, a, ns, out, n, s);
-    case O_MAX:  return tree_arith<O_MAX>(k, a, ns, out, n, s);
-    case O_MIN:  return tree_arith<O_MIN>(k, a, ns, out, n, s);
-    case O_PROD: return tree_arith<O_PROD>(k, a, ns, out, n, s);
-    case O_LAND: return tree_arith<O_LAND>(k, a, ns, out, n, s);
-    case O_LOR:  return tree_arith<O_LOR>(k, a, ns, out, n, s);
-    case O_LXOR: return tree_arith<O_LXOR>(k, a, ns, out, n, s);
-    case O_BAND: return run_tree<O_BAND, uint8_t, uint32_t>(a, ns, out, n * kind_size(k), s);
-    case O_BOR:  return run_tree<O_BOR, uint8_t, uint32_t>(a, ns, out, n * kind_size(k), s);
-    case O_BXOR: return run_tree<O_BXOR, uint8_t, uint32_t>(a, ns, out, n * kind_size(k), s);
-    case O_MAXLOC: return tree_loc<O_MAXLOC>(k, a, ns, out, n, s);
-    case O_MINLOC: return tree_loc<O_MINLOC>(k, a, ns, out, n, s);
+    case O_SUM:    return tree_dispatch<O_SUM>(k, a, ns, out, n, s);
+    case O_MAX:    return tree_dispatch<O_MAX>(k, a, ns, out, n, s);
+    case O_MIN:    return tree_dispatch<O_MIN>(k, a, ns, out, n, s);
+    case O_PROD:   return tree_dispatch<O_PROD>(k, a, ns, out, n, s);
+    case O_LAND:   return tree_dispatch<O_LAND>(k, a, ns, out, n, s);
+    case O_LOR:    return tree_dispatch<O_LOR>(k, a, ns, out, n, s);
+    case O_LXOR:   return tree_dispatch<O_LXOR>(k, a, ns, out, n, s);
+    case O_BAND:   return tree_dispatch<O_BAND>(k, a, ns, out, n, s);
+    case O_BOR:    return tree_dispatch<O_BOR>(k, a, ns, out, n, s);
+    case O_BXOR:   return tree_dispatch<O_BXOR>(k, a, ns, out, n, s);
+    case O_MAXLOC: return tree_dispatch<O_MAXLOC>(k, a, ns, out, n, s);
+    case O_MINLOC: return tree_dispatch<O_MINLOC>(k, a, ns, out, n, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -1,0 +1,472 @@
+// msx_tree_dev.h — device code shared by msx_kernels.hip (push / flag / copy
+// kernels) and the msx_tree_*.hip parts (the reference-order tree combine
+// k_tree, instantiated per MPI_Op in separate translation units so they
+// compile in parallel).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "msx_dev_ops.h"
+#include "msx_kernels.h"
+
+namespace msx {
+namespace dev {
+
+// ---- copy-segment and flag descriptors (k_copy_segs, k_push_post, k_tree) -------
+constexpr int kMaxSegs = 32;
+struct CopySegs {
+    const void* src[kMaxSegs];
+    void* dst[kMaxSegs];
+    size_t nbytes[kMaxSegs];
+    int n;
+    int sys;
+};
+
+struct PostFlags {
+    unsigned long long* dst[64];
+    unsigned long long seq;
+    int n;
+};
+
+// "This lane's stores have completed" without a cache maintenance operation:
+// s_waitcnt vmcnt(0) (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15).  An
+// agent-scope release fence would do the same wait but also write back the
+// whole XCD L2 (buffer_wbl2), once per workgroup -- on this multi-XCD part
+// that made a 2048-workgroup push 20x slower.  Window memory is uncached
+// (MTYPE_UC), so a completed store is at the owner; nothing sits in L2.
+__device__ __forceinline__ void stores_done()
+{
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);      // no compiler motion of stores past the wait
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// The small-allreduce push (k_push_post, and the first workgroups of a fused
+// k_tree launch): see the comment at k_push_post.
+__device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
+                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
+{
+    const char* src = static_cast<const char*>(c.src[sg]);
+    char* dst = static_cast<char*>(c.dst[sg]);
+    const size_t nb = c.nbytes[sg];
+    const size_t stride = (size_t)gx * 256;
+    size_t done = 0;
+    bool plain = false;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const size_t nv = nb / 16;
+        for (size_t i = (size_t)bx * 256 + threadIdx.x; i < nv; i += stride) {
+            const u32x4 v = reinterpret_cast<const u32x4*>(src)[i];
+            unsigned long long* d = reinterpret_cast<unsigned long long*>(dst) + 2 * i;
+            __hip_atomic_store(d, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(d + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        done = nv * 16;
+    }
+    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) {
+        dst[i] = src[i];
+        plain = true;
+    }
+    if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
+    else stores_done();                                 // vmcnt(0): this lane's stores completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == total - 1) {
+            if (sys) __threadfence_system();
+            for (int k = 0; k < f.n; ++k)
+                __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
+        }
+    }
+}
+
+// Count finished workgroup b of nb; true in exactly one workgroup, after all
+// nb have counted.  Thousands of workgroups adding to ONE word serialise
+// (a 4096-workgroup tree took 70 us instead of 38), so workgroup b counts on
+// sub-counter b % kCountSubs (its own 64-byte line, base[kCountSubBase +
+// 16 i]) and only the last of each sub-counter counts on base[0].  Relaxed:
+// each add is issued after the workgroup's stores completed (stores_done),
+// so when the last add is seen, all of them have.  Words are left zero.
+__device__ __forceinline__ bool count_done(unsigned* base, unsigned b, unsigned nb)
+{
+    const unsigned i = b % kCountSubs;
+    const unsigned nsub = nb < kCountSubs ? nb : kCountSubs;
+    const unsigned want = (nb - i + kCountSubs - 1) / kCountSubs;   // workgroups on sub-counter i
+    unsigned* c = base + kCountSubBase + 16 * i;
+    if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want - 1) return false;
+    __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(base, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nsub - 1) return false;
+    __hip_atomic_store(base, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// Bulk variant for multi-MiB segments (the two-step allreduce's pieces): plain
+// 16-byte stores from a full grid, four loads in flight per lane (as
+// k_copy_segs), then push_post_body's fenced count and flag post.  Plain
+// stores to peer windows rely on the windows' uncached mapping like every
+// other bulk transfer of the engine; `sys` (cached windows) writes the L2
+// back at system scope before counting.
+__device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
+                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
+{
+    const char* src = static_cast<const char*>(c.src[sg]);
+    char* dst = static_cast<char*>(c.dst[sg]);
+    const size_t nb = c.nbytes[sg];
+    const size_t stride = (size_t)gx * 256;
+    size_t done = 0;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const size_t nv = nb / 16;
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+        u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+        size_t i = (size_t)bx * 256 + threadIdx.x;
+        for (; i + 3 * stride < nv; i += 4 * stride) {
+            const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
+            d4[i] = a0; d4[i + stride] = a1; d4[i + 2 * stride] = a2; d4[i + 3 * stride] = a3;
+        }
+        for (; i < nv; i += stride) d4[i] = s4[i];
+        done = nv * 16;
+    }
+    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
+    if (sys) __threadfence_system();
+    else stores_done();
+    __syncthreads();
+    // counter: a kCountWords block (count_done); b = this workgroup's index
+    if (threadIdx.x == 0 && count_done(counter, (unsigned)sg + bx * (unsigned)c.n, total)) {
+        if (sys) __threadfence_system();
+        for (int k = 0; k < f.n; ++k)
+            __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// ---- reference-order multi-input combine ----------------------------------------
+// One pass over up to 2*kMaxLeaves inputs that reproduces the association AND
+// the inout/in roles of the reference's multi-step schedules:
+//   tree  (chain == 0): leaf_k = pair_k ? f(s[2k], s[2k+1]) : s[2k], k < P (pow2),
+//         then the balanced tree ((l0 op l1) op (l2 op l3)) op ... with the left
+//         operand always in the `inout` role (recursive doubling / halving,
+//         reduce.cpp:3890-4009, 1088-1175; the non-power-of-two fold is the
+//         leaf pair, reduce.cpp:3835-3871);
+//   chain (chain == 1): ((s0 op s1) op s2) op ... op s[P-1] (pairwise exchange,
+//         reduce.cpp:1258-1318).
+constexpr int kMaxLeaves = 16;
+constexpr int kMaxExtraOut = 31;
+struct TreeArgs {
+    const void* s[2 * kMaxLeaves];
+    void* extra[kMaxExtraOut];   // further destinations of the result (peer windows)
+    int nextra;
+    int P;
+    int nleaves;   // leaves present (<= P); the rest of the P-leaf tree is empty
+    unsigned pairmask;
+    int chain;
+    int sys;   // sources/outputs shared with other GPUs: system-coherent access
+    const unsigned long long* wait_flags;   // see TreeSpec
+    unsigned long long wait_seq;
+    int wait_n;
+    int wait_skip;
+    int* wait_err;
+    // fused push (barrier-free small allreduce): the first npush workgroups
+    // copy this rank's contribution into the peers' IN halves and post the
+    // arrival flags (push_post_body) instead of evaluating the tree
+    unsigned npush;
+    unsigned push_gx;     // workgroups per push segment
+    int push_sys;
+    unsigned* push_counter;
+    CopySegs push;
+    PostFlags flags;
+    // result-ready flags (barrier-free two-step allreduce): once every tree
+    // workgroup of all `done_launches` launches has stored its results, post
+    // done_flags (see tree_done)
+    unsigned* done_counter;       // kCountWords block: [0] count_done, [1] launches done
+    unsigned done_launches;
+    PostFlags done_flags;
+};
+
+// End of a tree workgroup when the launch posts result-ready flags: the
+// threadFenceReduction pattern of push_post_body, extended over the launches
+// that together evaluate one call (stream-ordered, so at most one is in
+// flight).  Every lane waits for its own stores (stores_done; cached windows:
+// system fence), thread 0 counts the workgroup, the launch's last workgroup
+// counts the launch, and the last workgroup of the last launch posts the
+// flags with system-scope release stores.  Both words are left zero for the
+// next call.
+__device__ __forceinline__ void tree_done(const TreeArgs& a, unsigned b, unsigned nb)
+{
+    if (a.sys) __threadfence_system();
+    else stores_done();
+    __syncthreads();
+    if (threadIdx.x != 0 || !count_done(a.done_counter, b, nb)) return;
+    // launches of the call: word 1 of the block
+    const unsigned l = __hip_atomic_fetch_add(a.done_counter + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l != a.done_launches - 1) return;
+    __hip_atomic_store(a.done_counter + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.sys) __threadfence_system();
+    for (int k = 0; k < a.done_flags.n; ++k)
+        __hip_atomic_store(a.done_flags.dst[k], a.done_flags.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Arrival wait of the barrier-free small allreduce: thread 0 of every
+// workgroup polls the peers' flags (uncached window memory, system-scope
+// loads) until each reaches the call's sequence number.  Bounded: after
+// ~20 s (s_memrealtime runs at 100 MHz) it reports through *wait_err and the
+// workgroup exits, so a missing peer can never leave a wave running.
+__device__ __forceinline__ bool wait_flags_body(const unsigned long long* flags, unsigned long long seq, int n,
+                                                int skip, int* err)
+{
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        int good = 1;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (int r = 0; r < n && good; ++r) {
+            if (r == skip) continue;
+            while (__hip_atomic_load(flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    good = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        // The acquire that pairs with the pusher's system-scope release of the
+        // flag: invalidates this CU's L1 and the XCD's L2 copies of peer-written
+        // lines, so the IN half is read fresh whatever cache type the window
+        // is mapped with (the UC mapping makes it a no-op for the data today,
+        // but the kernel no longer depends on that allocation property).
+        if (good) (void)__hip_atomic_load(flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
+__device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
+{
+    return wait_flags_body(a.wait_flags, a.wait_seq, a.wait_n, a.wait_skip, a.wait_err);
+}
+
+// Start-of-kernel system acquire: invalidate this CU's L1 and the XCD's L2
+// lines for memory other GPUs may have written since (peer HBM over xGMI).
+__device__ __forceinline__ void acquire_system()
+{
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __syncthreads();
+}
+
+// End-of-kernel system release: write this XCD's dirty L2 lines back so peers
+// reading over xGMI see them (one fence per workgroup).
+__device__ __forceinline__ void release_system()
+{
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+template <class F, class V, class LD>
+__device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
+{
+    if (a.chain) {
+        // every source loaded before the first combine (the loop bound is a
+        // runtime value: a rolled loop waited for each load in turn, 75 us
+        // instead of 8 us for a 4-rank 1 MiB reduce_scatter); same order
+        V x[kMaxLeaves];
+#pragma unroll
+        for (int k = 0; k < kMaxLeaves; ++k)
+            if (k < a.P) x[k] = load(k);
+        V v = x[0];
+#pragma unroll
+        for (int k = 1; k < kMaxLeaves; ++k)
+            if (k < a.P) v = F::apply(v, x[k]);
+        return v;
+    }
+    // leaves >= nleaves are absent (binomial trees over a non-power-of-two p):
+    // a node whose right subtree is empty passes its left value up unchanged.
+    V v[kMaxLeaves];
+#pragma unroll
+    for (int k = 0; k < kMaxLeaves; ++k) {
+        if (k < a.nleaves) {
+            v[k] = load(2 * k);
+            if ((a.pairmask >> k) & 1u) v[k] = F::apply(v[k], load(2 * k + 1));
+        }
+    }
+#pragma unroll
+    for (int w = 1; w < kMaxLeaves; w *= 2) {
+#pragma unroll
+        for (int k = 0; k + w < kMaxLeaves; k += 2 * w)
+            if (k + w < a.nleaves) v[k] = F::apply(v[k], v[k + w]);
+    }
+    return v[0];
+}
+
+// The same tree over 16-byte vectors, with every source vector loaded
+// (non-temporal: each is read once) before the first combine, so all of them
+// are in flight together.
+template <class F, bool NT>
+__device__ __forceinline__ u32x4 tree_vec(const TreeArgs& a, size_t i)
+{
+    auto ld_src = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
+    u32x4 v[kMaxLeaves], w[kMaxLeaves];
+    if (a.chain) {
+#pragma unroll
+        for (int k = 0; k < kMaxLeaves; ++k)
+            if (k < a.P) v[k] = ld_src(k);
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 r = v[0];
+#pragma unroll
+        for (int k = 1; k < kMaxLeaves; ++k)
+            if (k < a.P) r = F::apply(r, v[k]);
+        return r;
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxLeaves; ++k) {
+        if (k < a.nleaves) {
+            v[k] = ld_src(2 * k);
+            if ((a.pairmask >> k) & 1u) w[k] = ld_src(2 * k + 1);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < kMaxLeaves; ++k)
+        if (k < a.nleaves && ((a.pairmask >> k) & 1u)) v[k] = F::apply(v[k], w[k]);
+#pragma unroll
+    for (int d = 1; d < kMaxLeaves; d *= 2) {
+#pragma unroll
+        for (int k = 0; k + d < kMaxLeaves; k += 2 * d)
+            if (k + d < a.nleaves) v[k] = F::apply(v[k], v[k + d]);
+    }
+    return v[0];
+}
+
+template <int OP, class VT> struct VecFn {
+    __device__ static u32x4 apply(u32x4 io, u32x4 in) { return apply_vec<OP, VT>(io, in); }
+};
+
+// The full balanced tree over NL sources (no pairs, no absent leaves: every
+// power-of-two p of the allreduce / reduce_scatter / reduce trees), or with
+// CHAIN the left-deep chain over NL sources (pairwise exchange), with the
+// source count known at compile time: no runtime leaf tests, NL*U source
+// vectors per lane issued before the first combine, tiles of BLOCK*U vectors.
+// Same association and operand roles as tree_vec / tree_eval.  The generic
+// kernel's runtime leaf tests cost 25 % (p = 8, fp32 SUM, 32 MiB per source:
+// 55 us generic vs 44.6 us here, scripts/tree_probe.py).
+template <class F, int NL, int U, int BLOCK, bool NT, bool CHAIN>
+__device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict__ out, size_t nvec, size_t bid,
+                                           size_t nb)
+{
+    constexpr size_t TILE = (size_t)BLOCK * U;
+    const u32x4* src[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k)   // tree leaf k sits in slot 2k (slot 2k+1: its pair); chain source k in slot k
+        src[k] = reinterpret_cast<const u32x4*>(a.s[CHAIN ? k : 2 * k]);
+    auto reduce = [](u32x4* v) {
+        if constexpr (CHAIN) {
+#pragma unroll
+            for (int k = 1; k < NL; ++k) v[0] = F::apply(v[0], v[k]);
+        } else {
+#pragma unroll
+            for (int d = 1; d < NL; d *= 2) {
+#pragma unroll
+                for (int k = 0; k + d < NL; k += 2 * d) v[k] = F::apply(v[k], v[k + d]);
+            }
+        }
+        return v[0];
+    };
+    for (size_t t0 = bid * TILE; t0 < nvec; t0 += nb * TILE) {
+        const size_t i0 = t0 + threadIdx.x;
+        if (t0 + TILE <= nvec) {
+            u32x4 v[U][NL];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int k = 0; k < NL; ++k) v[u][k] = ld<NT>(src[k] + i0 + (size_t)u * BLOCK);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32x4 r = reduce(v[u]);
+                out[i0 + (size_t)u * BLOCK] = r;
+                for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i0 + (size_t)u * BLOCK] = r;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t i = i0 + (size_t)u * BLOCK;
+                if (i < nvec) {
+                    u32x4 v[NL];
+#pragma unroll
+                    for (int k = 0; k < NL; ++k) v[k] = ld<NT>(src[k] + i);
+                    const u32x4 r = reduce(v);
+                    out[i] = r;
+                    for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
+                }
+            }
+        }
+    }
+}
+
+// UPFRONT: all source vectors loaded before the first combine (tree_vec), else
+// loads interleaved with the combines as the tree consumes them (tree_eval);
+// NT: non-temporal source loads.  The fp32 SUM tuning sweep times all four
+// (p = 8, 32 MiB each): interleaved plain loads 51.7 us (5.8 TB/s), up front
+// 57.1 us -- holding every source vector costs 146 VGPRs instead of 77, half
+// the waves per SIMD -- and non-temporal loads 3-8 % slower either way.
+template <int OP, class T, class VT, int BLOCK, bool UPFRONT = false, bool NT = false, int NL = 0, int U = 1,
+          bool CHAIN = false>
+__global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out, size_t nvec,
+                                                size_t tail, int vec_ok)
+{
+    constexpr size_t EPV = 16 / sizeof(T);
+    unsigned b = blockIdx.x, nb = gridDim.x;
+    if (a.npush) {
+        // fused push: the first npush workgroups push this rank's vector and
+        // post its flags; they never wait, so the peers' trees always progress
+        if (b < a.npush) {
+            // segment b % n: every peer's push starts at once (see k_copy_segs)
+            const unsigned ns = (unsigned)a.push.n;
+            push_post_body(a.push, a.flags, a.push_counter, a.npush, a.push_sys, b / ns, a.push_gx, (int)(b % ns));
+            return;
+        }
+        b -= a.npush;
+        nb -= a.npush;
+    }
+    const size_t stride = (size_t)nb * BLOCK;
+    const size_t bid = xcd_tile(b, nb);      // XCD-contiguous (see combine_body)
+    if (a.wait_flags && !arrival_wait(a)) return;
+    if (a.sys) acquire_system();
+    if constexpr (NL > 0) {
+        if (vec_ok) tree_fixed<VecFn<OP, VT>, NL, U, BLOCK, NT, CHAIN>(a, reinterpret_cast<u32x4*>(out), nvec, bid, nb);
+    } else if (vec_ok) {
+        for (size_t i = bid * BLOCK + threadIdx.x; i < nvec; i += stride) {
+            u32x4 r;
+            if constexpr (UPFRONT) {
+                r = tree_vec<VecFn<OP, VT>, NT>(a, i);
+            } else {
+                auto load = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
+                r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
+            }
+            reinterpret_cast<u32x4*>(out)[i] = r;
+            for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
+        }
+    }
+    const size_t first = vec_ok ? nvec * EPV : 0;
+    const size_t nsc = vec_ok ? tail : tail + nvec * EPV;
+    for (size_t s = (size_t)b * BLOCK + threadIdx.x; s < nsc; s += stride) {
+        auto load = [&](int k) { return reinterpret_cast<const T*>(a.s[k])[first + s]; };
+        const T r = tree_eval<Fn<OP>, T>(a, load);
+        out[first + s] = r;
+        for (int e = 0; e < a.nextra; ++e) static_cast<T*>(a.extra[e])[first + s] = r;
+    }
+    if (a.sys) release_system();
+    if (a.done_counter) tree_done(a, b, nb);
+}
+
+}  // namespace dev
+
+// host side: the per-op tree launchers (msx_tree_*.hip) and the tuning knob
+extern TreeTune g_tree_tune;
+template <int OP>
+hipError_t tree_dispatch(Kind k, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s);
+// fp32 SUM tuning modes of msx_tune_tree (msx_tree_sum.hip)
+hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s);
+
+}  // namespace msx

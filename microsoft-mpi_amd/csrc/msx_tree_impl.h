@@ -1,0 +1,117 @@
+// msx_tree_impl.h — host-side launch of k_tree (msx_tree_dev.h) for one MPI_Op
+// per translation unit: msx_tree_sum.hip (SUM, PROD and the fp32 SUM tuning
+// modes), msx_tree_cmp.hip (MAX, MIN, MAXLOC, MINLOC), msx_tree_logic.hip
+// (LAND, LOR, LXOR, BAND, BOR, BXOR).  Included by those files only.
+#pragma once
+#include "msx_tree_dev.h"
+
+namespace msx {
+namespace {
+
+using namespace dev;
+
+constexpr int kTreeBlock = 256;
+constexpr int kTreeGridCap = 4096;          // generic kernel: grid-stride beyond this
+constexpr int kFixedGridCap = 1 << 20;      // compile-time-source kernel: one tile per workgroup
+
+template <int OP, class T, class VT, bool UPFRONT = false, bool NT = false, int NL = 0, int U = 1,
+          bool CHAIN = false>
+hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
+{
+    bool ok = ((uintptr_t)out & 15) == 0;
+    for (int k = 0; k < nsrc; ++k) ok = ok && a.s[k] && (((uintptr_t)a.s[k] & 15) == 0);
+    for (int e = 0; e < a.nextra; ++e) ok = ok && (((uintptr_t)a.extra[e] & 15) == 0);
+    constexpr size_t ES = sizeof(T);
+    const size_t epv = 16 / ES;
+    const size_t nvec = count / epv, tail = count - nvec * epv;
+    const size_t work = ok ? (nvec + U - 1) / U + tail : count;
+    size_t grid = (work + kTreeBlock - 1) / kTreeBlock;
+    const size_t cap = g_tree_tune.grid_cap > 0 ? (size_t)g_tree_tune.grid_cap
+                                                : (size_t)(NL > 0 ? kFixedGridCap : kTreeGridCap);
+    if (grid > cap) grid = cap;
+    if (grid == 0) return hipSuccess;
+    grid += a.npush;                         // fused push workgroups come first
+    hipLaunchKernelGGL((k_tree<OP, T, VT, kTreeBlock, UPFRONT, NT, NL, U, CHAIN>), dim3((unsigned)grid),
+                       dim3(kTreeBlock), 0, s, a, static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
+    return hipGetLastError();
+}
+
+// The compile-time-source kernel when the call is a full power-of-two tree or
+// a chain of 2, 4 or 8 sources (p = 2, 4, 8: the node sizes); the generic
+// kernel otherwise (non-power-of-two folds, binomial trees with absent
+// leaves, other chain lengths, p = 16).
+template <int OP, class T, class VT, int U = 1, bool NT = false>
+hipError_t run_tree_auto(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
+{
+    if (a.chain) {
+        switch (a.P) {
+        case 2: return run_tree<OP, T, VT, false, NT, 2, U, true>(a, nsrc, out, count, s);
+        case 4: return run_tree<OP, T, VT, false, NT, 4, U, true>(a, nsrc, out, count, s);
+        case 8: return run_tree<OP, T, VT, false, NT, 8, U, true>(a, nsrc, out, count, s);
+        default: break;
+        }
+    } else if (a.pairmask == 0 && a.nleaves == a.P) {
+        switch (a.P) {
+        case 2: return run_tree<OP, T, VT, false, NT, 2, U>(a, nsrc, out, count, s);
+        case 4: return run_tree<OP, T, VT, false, NT, 4, U>(a, nsrc, out, count, s);
+        case 8: return run_tree<OP, T, VT, false, NT, 8, U>(a, nsrc, out, count, s);
+        default: break;
+        }
+    }
+    return run_tree<OP, T, VT>(a, nsrc, out, count, s);
+}
+
+template <int OP>
+hipError_t tree_arith(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
+{
+    switch (k) {
+    case K_I8:  return run_tree_auto<OP, int8_t, int8_t>(a, ns, out, n, s);
+    case K_U8:  return run_tree_auto<OP, uint8_t, uint8_t>(a, ns, out, n, s);
+    case K_I16: return run_tree_auto<OP, int16_t, int16_t>(a, ns, out, n, s);
+    case K_U16: return run_tree_auto<OP, uint16_t, uint16_t>(a, ns, out, n, s);
+    case K_I32: return run_tree_auto<OP, int32_t, int32_t>(a, ns, out, n, s);
+    case K_U32: return run_tree_auto<OP, uint32_t, uint32_t>(a, ns, out, n, s);
+    case K_I64: return run_tree_auto<OP, int64_t, int64_t>(a, ns, out, n, s);
+    case K_U64: return run_tree_auto<OP, uint64_t, uint64_t>(a, ns, out, n, s);
+    case K_F32: return run_tree_auto<OP, float, float>(a, ns, out, n, s);
+    case K_F64: return run_tree_auto<OP, double, double>(a, ns, out, n, s);
+    default: break;
+    }
+    if constexpr (OP == O_SUM || OP == O_PROD) {
+        if (k == K_C32) return run_tree_auto<OP, c32, c32>(a, ns, out, n, s);
+        if (k == K_C64) return run_tree_auto<OP, c64, c64>(a, ns, out, n, s);
+    }
+    if constexpr (OP == O_LAND || OP == O_LOR || OP == O_LXOR) {
+        if (k == K_BOOL) return run_tree_auto<OP, uint8_t, uint8_t>(a, ns, out, n, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int OP>
+hipError_t tree_loc(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
+{
+    switch (k) {
+    case K_LOC_II: return run_tree_auto<OP, loc_ii, loc_ii>(a, ns, out, n, s);
+    case K_LOC_FI: return run_tree_auto<OP, loc_fi, loc_fi>(a, ns, out, n, s);
+    case K_LOC_SI: return run_tree_auto<OP, loc_si, loc_si>(a, ns, out, n, s);
+    case K_LOC_DI: return run_tree_auto<OP, loc_di, loc_di>(a, ns, out, n, s);
+    case K_LOC_FF: return run_tree_auto<OP, loc_ff, loc_ff>(a, ns, out, n, s);
+    case K_LOC_DD: return run_tree_auto<OP, loc_dd, loc_dd>(a, ns, out, n, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+template <int OP>
+hipError_t tree_dispatch(Kind k, const TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
+{
+    if constexpr (OP == O_BAND || OP == O_BOR || OP == O_BXOR)     // raw bytes on 32-bit lanes
+        return run_tree_auto<OP, uint8_t, uint32_t>(a, ns, out, n * kind_size(k), s);
+    else if constexpr (OP == O_MAXLOC || OP == O_MINLOC)
+        return tree_loc<OP>(k, a, ns, out, n, s);
+    else
+        return tree_arith<OP>(k, a, ns, out, n, s);
+}
+
+}  // namespace msx

@@ -1,0 +1,29 @@
+// msx_tree_sum.hip — k_tree launchers (SUM, PROD; the fp32 SUM tuning modes of msx_tune_tree), see msx_tree_impl.h.
+#include "msx_tree_impl.h"
+
+namespace msx {
+
+template hipError_t tree_dispatch<O_SUM>(Kind, const dev::TreeArgs&, int, void*, size_t, hipStream_t);
+template hipError_t tree_dispatch<O_PROD>(Kind, const dev::TreeArgs&, int, void*, size_t, hipStream_t);
+
+// msx_tune_tree modes (fp32 SUM): 1/2/3 the generic kernel with
+// loads up front / up front + non-temporal / interleaved + non-temporal,
+// 4/5/6 the compile-time-source kernel with 1/2/4 vectors per lane, 7 = 5 with
+// non-temporal loads, 8 the generic kernel as it is (the dispatch before the
+// compile-time-source kernel); mode 0 (not routed here) is the default dispatch.
+hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
+{
+    switch (mode) {
+    case 1: return run_tree<O_SUM, float, float, true, false>(a, ns, out, n, s);
+    case 2: return run_tree<O_SUM, float, float, true, true>(a, ns, out, n, s);
+    case 3: return run_tree<O_SUM, float, float, false, true>(a, ns, out, n, s);
+    case 4: return run_tree_auto<O_SUM, float, float, 1, false>(a, ns, out, n, s);
+    case 5: return run_tree_auto<O_SUM, float, float, 2, false>(a, ns, out, n, s);
+    case 6: return run_tree_auto<O_SUM, float, float, 4, false>(a, ns, out, n, s);
+    case 7: return run_tree_auto<O_SUM, float, float, 2, true>(a, ns, out, n, s);
+    case 8: return run_tree<O_SUM, float, float>(a, ns, out, n, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace msx

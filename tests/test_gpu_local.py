@@ -309,6 +309,57 @@ def test_tree_combine_reference_association(L):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), l0.view(np.uint32))
 
 
+@pytest.mark.parametrize("p", [2, 8, 16])
+def test_tree_every_legal_pair(L, p):
+    """msx_reduce_tree_dev for every legal (op, type) pair: p = 2 and 8 run the
+    compile-time-source kernel, p = 16 the generic one; both must evaluate
+    ((s0 op s1) op (s2 op s3)) ... with the left operand as `inout`, bit for
+    bit as the oracle's pairwise Op<T> calls (edge values, ragged size)."""
+    rng = np.random.default_rng(1000 + p)
+    n = 1027
+    for op, dt in legal_pairs(oracle):
+        kind = KIND[dt]
+        xs = [_raw(gen(kind, op, n, rng)) for _ in range(p)]
+        dv = [_dev(x) for x in xs]
+        arr = (ctypes.c_void_p * p)(*[d[1] for d in dv])
+        out = torch.zeros(xs[0].nbytes + 64, dtype=torch.uint8, device="cuda")
+        assert L.msx_reduce_tree_dev(arr, p, out.data_ptr(), n, h(dt), h(op), _stream()) == 0, msx.last_error()
+        torch.cuda.synchronize()
+        lv = [_raw(x) for x in xs]
+        while len(lv) > 1:
+            nxt = []
+            for i in range(0, len(lv), 2):
+                left = _raw(lv[i])
+                assert oracle.reduce_local(h(op), h(dt), lv[i + 1], left) == 0
+                nxt.append(left)
+            lv = nxt
+        got = out[:xs[0].nbytes].cpu().numpy().tobytes()
+        assert got == lv[0].tobytes(), f"{op} {dt} p={p}"
+
+
+def test_tree_tuning_modes_agree(L):
+    # every msx_tune_tree mode evaluates the same fp32 SUM tree (p = 8, ragged
+    # 3 Mi + 5 elements, one source misaligned -> scalar path for mode 4..7)
+    rng = np.random.default_rng(77)
+    n = (3 << 20) + 5
+    xs = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(8)]
+    lv = list(xs)
+    while len(lv) > 1:
+        lv = [lv[i] + lv[i + 1] for i in range(0, len(lv), 2)]
+    want = lv[0].view(np.uint32)
+    for offset in (0, 4):
+        dv = [_dev(x, offset if r == 3 else 0) for r, x in enumerate(xs)]
+        arr = (ctypes.c_void_p * 8)(*[d[1] for d in dv])
+        for mode in range(9):
+            for cap in (0, 1024):
+                assert L.msx_tune_tree(mode, cap) == 0
+                out = torch.zeros(n, dtype=torch.float32, device="cuda")
+                assert L.msx_reduce_tree_dev(arr, 8, out.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
+                torch.cuda.synchronize()
+                assert np.array_equal(out.cpu().numpy().view(np.uint32), want), (mode, cap, offset)
+    assert L.msx_tune_tree(0, 0) == 0
+
+
 def test_benchmark_size_fp32_sum_bit_exact(L):
     # config 2 (BASELINE.json): 256 MiB fp32 per operand, device resident.
     n = 64 << 20
