@@ -98,7 +98,9 @@ int msx_tune_tree(int mode, int grid_cap);
 const char* msx_tune_variant_name(int variant);
 /* HBM ceiling probe (measurement only): the default combine's launch geometry
  * with another stream mix over `bytes` per stream (16-B aligned device
- * pointers): mode 0 reads a and b, 1 writes b, 2 copies a -> b, 3 reads a.
+ * pointers): mode 0 reads a and b, 1 writes b, 2 copies a -> b, 3 reads a;
+ * 4 copies a -> b with the engine's segment-copy kernel (k_copy_segs), 5 with
+ * hipMemcpyAsync.
  * Stream-ordered; b's contents are unspecified afterwards. */
 int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream);
 /* device allocation for measurements: uncached = the engine windows' memory

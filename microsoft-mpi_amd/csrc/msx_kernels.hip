@@ -17,6 +17,7 @@
 // float result is the single correctly-rounded IEEE op the reference performs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <type_traits>
 
@@ -250,9 +251,16 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
     // One 1-D grid, workgroup b serving segment b % n: consecutive workgroups
     // go to different segments, so the dispatcher starts every segment (every
     // peer link, when the segments are remote) at once instead of filling the
-    // GPU with the first few segments' workgroups.
-    const int sg = (int)(blockIdx.x % (unsigned)c.n);
-    const size_t bx = blockIdx.x / (unsigned)c.n, gx = gridDim.x / (unsigned)c.n;
+    // GPU with the first few segments' workgroups.  One 4-KiB tile per
+    // workgroup and lane (16-B non-temporal loads), as the HBM probe's copy:
+    // the earlier grid-stride form (<= 512 workgroups per segment, 4 loads in
+    // flight per lane) copied 256 MiB locally at 5.5 TB/s of traffic, this
+    // form at the probe's ~8 TB/s (scripts/copy_probe.py).  A single segment
+    // (a local copy) takes the XCD-contiguous tile order of the combine.
+    const unsigned n = (unsigned)c.n;
+    const int sg = (int)(blockIdx.x % n);
+    const size_t gx = gridDim.x / n;
+    const size_t bx = n == 1 ? (size_t)xcd_tile(blockIdx.x, gridDim.x) : (size_t)(blockIdx.x / n);
     if (c.sys) acquire_system();
     const char* src = static_cast<const char*>(c.src[sg]);
     char* dst = static_cast<char*>(c.dst[sg]);
@@ -264,12 +272,7 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
         const size_t nv = nb / 16;
         const u32x4* s = reinterpret_cast<const u32x4*>(src);
         u32x4* d = reinterpret_cast<u32x4*>(dst);
-        size_t i = bx * 256 + threadIdx.x;
-        for (; i + 3 * stride < nv; i += 4 * stride) {
-            u32x4 a0 = s[i], a1 = s[i + stride], a2 = s[i + 2 * stride], a3 = s[i + 3 * stride];
-            d[i] = a0; d[i + stride] = a1; d[i + 2 * stride] = a2; d[i + 3 * stride] = a3;
-        }
-        for (; i < nv; i += stride) d[i] = s[i];
+        for (size_t i = bx * 256 + threadIdx.x; i < nv; i += stride) d[i] = ld<true>(s + i);
         done = nv * 16;
     }
     for (size_t i = done + bx * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
@@ -647,7 +650,9 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
 
 hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s)
 {
-    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 3) return hipErrorInvalidValue;
+    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 5) return hipErrorInvalidValue;
+    if (mode == 4) return launch_copy_segs(&a, &b, &bytes, 1, false, s);      // the engine's copy kernel
+    if (mode == 5) return hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, s);   // HIP's blit
     const size_t nvec = bytes / 16;
     const size_t grid = (nvec + 255) / 256;
     if (grid == 0) return hipSuccess;
@@ -749,9 +754,18 @@ hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size
             if (c.nbytes[i] > maxb) maxb = c.nbytes[i];
         }
         if (maxb == 0) continue;
-        size_t gx = (maxb / 16 + 1023) / 1024;
+        // one 4-KiB tile per workgroup, grid-stride beyond MSX_COPY_GRID_CAP
+        // workgroups in all
+        static const size_t cap = [] {
+            const char* e = getenv("MSX_COPY_GRID_CAP");
+            const long long v = e ? atoll(e) : 0;
+            return v > 0 ? (size_t)v : ((size_t)1 << 22);
+        }();
+        size_t gx = (maxb / 16 + 255) / 256;
         if (gx < 1) gx = 1;
-        if (gx > 512) gx = 512;
+        size_t gmax = cap / (size_t)c.n;
+        if (gmax < 1) gmax = 1;
+        if (gx > gmax) gx = gmax;
         hipLaunchKernelGGL(k_copy_segs, dim3((unsigned)(gx * (size_t)c.n)), dim3(256), 0, s, c);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

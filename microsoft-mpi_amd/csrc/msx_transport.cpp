@@ -1275,9 +1275,34 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
     return rc;
 }
 
+// Copies of at least MSX_KERNEL_COPY_MIN bytes (1 MiB) within this GPU's
+// memory (HBM buffers, its own window; 0 disables) run on the engine's copy
+// kernel: 256 MiB local copies take 68 us there and 99 us as hipMemcpyAsync's
+// blit (scripts/copy_probe.py).  Host memory keeps hipMemcpyAsync (DMA).
+size_t kernel_copy_min()
+{
+    static const size_t v = [] {
+        const char* e = getenv("MSX_KERNEL_COPY_MIN");
+        return e ? (size_t)atoll(e) : ((size_t)1 << 20);
+    }();
+    return v;
+}
+
 int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
 {
     if (!bytes) return MPI_SUCCESS;
+    if (kernel_copy_min() && bytes >= kernel_copy_min()) {
+        const BufInfo bs = classify(src), bd = classify(dst);
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        // both on this GPU (a peer's window or another GPU's buffer: the blit)
+        if (bs.place == Place::Device && bd.place == Place::Device && bs.device == cur && bd.device == cur) {
+            const void* ps = bs.dev;
+            void* pd = bd.dev;
+            hipError_t e = launch_copy_segs(&ps, &pd, &bytes, 1, sys_fences(), s);
+            return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy kernel");
+        }
+    }
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s);
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "stage copy");
 }
