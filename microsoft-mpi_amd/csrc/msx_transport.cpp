@@ -2338,16 +2338,63 @@ int host_user_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MP
     return img_store(m, count, res[me].data() - m.lo, recvbuf);
 }
 
-int combine2(int opidx, Kind k, const char* inout_src, const char* in, char* out, size_t n, hipStream_t s)
+int combine2(int opidx, Kind k, const char* inout_src, const char* in, char* out, size_t n, hipStream_t s,
+             char* out2 = nullptr)
 {
     TreeSpec t;
     t.P = 2;
     t.src[0] = inout_src;
     t.src[2] = in;
     t.sys = sys_fences();
+    if (out2) {                          // the same result stored twice
+        t.extra[0] = out2;
+        t.nextra = 1;
+    }
     hipError_t e = launch_tree_spec(opidx, k, t, out, n, s);
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "scan combine");
 }
+
+// One fused scan step (small vectors): the first workgroups push `psrc` into
+// the consumer's window and post its flag (k_tree's fused push; psrc == null:
+// nothing to push), the tree workgroups wait for the partial this rank
+// consumes (wflag >= v) and store a op tmp into out (and out2).  out must not
+// alias psrc: the tree does not wait for this launch's own push.
+int scan_fused_step(int opidx, Kind k, const char* a, const char* tmp, char* out, char* out2, size_t count,
+                    hipStream_t s, const unsigned long long* wflag, unsigned long long v, int* err,
+                    const void* psrc, void* pdst, size_t pbytes, unsigned long long* pflag, unsigned* pcounter)
+{
+    TreeSpec t;
+    t.P = 2;
+    t.src[0] = a;
+    t.src[2] = tmp;
+    t.sys = sys_fences();
+    if (out2) {
+        t.extra[0] = out2;
+        t.nextra = 1;
+    }
+    t.wait_flags = wflag;
+    t.wait_seq = v;
+    t.wait_n = 1;
+    t.wait_skip = -1;
+    t.wait_err = err;
+    if (psrc) {
+        t.push_nseg = 1;
+        t.push_src[0] = psrc;
+        t.push_dst[0] = pdst;
+        t.push_n[0] = pbytes;
+        t.push_nflags = 1;
+        t.push_flags[0] = pflag;
+        t.push_seq = v;
+        t.push_counter = pcounter;
+        t.push_sys = sys_fences();
+    }
+    hipError_t e = launch_tree_spec(opidx, k, t, out, count, s);
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "scan step");
+}
+
+// vectors up to this size take the fused scan steps (as the barrier-free
+// small allreduce: the fused push's system-coherent 8-byte stores)
+constexpr size_t kScanFuseMax = (size_t)256 << 10;
 
 int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
             const OpRef& op, bool exclusive)
@@ -2375,23 +2422,31 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     size_t ce = w.C / 2 / esz;
     ce -= ce % 16;
     if (ce == 0) { set_error("scan: window too small"); return MPI_ERR_INTERN; }
-    char* partial = dev_scratch(2 * bytes + 256);
+    const size_t bstride = (bytes + 255) & ~(size_t)255;
+    char* partial = dev_scratch(5 * bstride + 256);
     if (!partial) { set_error("scan: scratch allocation failed"); return MPI_ERR_NO_MEM; }
-    char* res = partial + ((bytes + 255) & ~(size_t)255);
+    char* res = partial + bstride;
+    char* partial2 = res + bstride;      // fused steps: the partial alternates with this one
+    char* src_stage = partial2 + bstride;   // host operands the kernels cannot address
+    char* dst_stage = src_stage + bstride;
     BufInfo bs = classify(src), bd = classify(recvbuf);
     PinHold pins;                        // host buffers: device aliases for the call
     pins.sync_before_release(s);
     alias_host_operands(pins, true, src, bytes, &bs, recvbuf, bytes, &bd);
     const char* srcv = bs.place == Place::Device ? static_cast<const char*>(bs.dev) : src;
     void* dstv = bd.place == Place::Device ? bd.dev : recvbuf;
-    rc = copy_async(partial, srcv, bytes, s);
-    if (rc == MPI_SUCCESS && !exclusive) rc = copy_async(res, srcv, bytes, s);
     bool have = !exclusive;
     if (flags) {
         // Every step on the stream, one host sync: step i = one k_push_wait
         // (my partial -> IN(me ^ mask) half, sub-slot me, flag (seq << 6) | i;
         // one workgroup waits for the partial I consume), then the combines.
         // Halves alternate and are reused as in the two-step allreduce.
+        // Launches are kept to the minimum (each costs a few us on its own GPU
+        // and tens of us when ranks share one): step 0 reads the send buffer
+        // in place; while partial and result hold the same value (inclusive
+        // scan until this rank first folds a higher rank's partial) one
+        // combine stores both; the last step stores the result straight into
+        // recvbuf and drops the partial nobody reads again.
         const size_t half = (size_t)tp->rd_parity * Qh;
         const unsigned long long seq = ++tp->rd_seq;
         int* err_host = nullptr;
@@ -2399,6 +2454,18 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
         unsigned* counter = tp->push_counter();
         if (!err_dev || !counter) { set_error("scan: flag word allocation failed"); return MPI_ERR_NO_MEM; }
         *err_host = 0;
+        // the kernels read the send buffer and write recvbuf in place when
+        // they are device memory (or pinned aliases); host memory is staged
+        const bool src_dev = bs.place == Place::Device, dst_dev = bd.place == Place::Device;
+        if (!src_dev) {
+            rc = copy_async(src_stage, src, bytes, s);
+            srcv = src_stage;
+        }
+        const char* cur_p = srcv;                       // current partial
+        const char* cur_r = exclusive ? nullptr : srcv; // current result (have)
+        bool same = !exclusive;                         // partial and result hold one value
+        char* outv = dst_dev ? static_cast<char*>(dstv) : dst_stage;
+        const bool fuse = fused_push() && bytes <= kScanFuseMax;
         int step = 0;
         for (int mask = 1; mask < p && rc == MPI_SUCCESS; mask <<= 1, ++step) {
             const int dst = me ^ mask;
@@ -2408,10 +2475,56 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
             const unsigned long long v = (seq << 6) | (unsigned long long)step;
             if (feeds && seq > 2) rc = tp->wait_done(dst, seq - 2);
             if (rc != MPI_SUCCESS) break;
-            const void* ps = partial;
+            const void* ps = cur_p;
             void* pd = feeds ? static_cast<void*>(w.sub(dst, me) + half) : nullptr;
             size_t pn = bytes;
             unsigned long long* pf = feeds ? w.flags(dst) + kScanFlags + me : nullptr;
+            if (fuse && use) {
+                // push (if any), wait and the first combine in one launch; the
+                // new partial goes to the buffer the push is NOT reading
+                const char* tmp = w.sub(me, dst) + half;
+                const unsigned long long* wf = w.flags(me) + kScanFlags + dst;
+                char* np = last ? nullptr : (cur_p == partial ? partial2 : partial);
+                const void* fps = feeds ? ps : nullptr;
+                if (me > dst) {
+                    char* nr = last ? outv : res;
+                    if (have && same) {
+                        rc = np ? scan_fused_step(op.opidx, k, cur_p, tmp, np, nr, count, s, wf, v, err_dev, fps, pd,
+                                                  pn, pf, counter)
+                                : scan_fused_step(op.opidx, k, cur_r, tmp, nr, nullptr, count, s, wf, v, err_dev, fps,
+                                                  pd, pn, pf, counter);
+                    } else {
+                        if (np) {
+                            rc = scan_fused_step(op.opidx, k, cur_p, tmp, np, nullptr, count, s, wf, v, err_dev, fps,
+                                                 pd, pn, pf, counter);
+                            if (rc == MPI_SUCCESS)
+                                rc = have ? combine2(op.opidx, k, cur_r, tmp, nr, count, s)
+                                          : copy_async(nr, tmp, bytes, s);
+                        } else if (have) {   // last step: only the result (no push: dst < me)
+                            rc = scan_fused_step(op.opidx, k, cur_r, tmp, nr, nullptr, count, s, wf, v, err_dev,
+                                                 nullptr, nullptr, 0, nullptr, nullptr);
+                        } else {             // Exscan's first fold is a copy: wait, then copy
+                            hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, v, false,
+                                                            nullptr, wf, 1, -1, err_dev, s);
+                            rc = e == hipSuccess ? copy_async(nr, tmp, bytes, s) : hip_fail(e, "scan wait");
+                        }
+                        same = false;
+                    }
+                    cur_r = nr;
+                    have = true;
+                } else {
+                    rc = scan_fused_step(op.opidx, k, cur_p, tmp, np, nullptr, count, s, wf, v, err_dev, fps, pd, pn,
+                                         pf, counter);
+                    same = false;
+                }
+                cur_p = np;
+                continue;
+            }
+            if (fuse && feeds) {             // push only: data and flag in one launch
+                hipError_t e = launch_push_post(&ps, &pd, &pn, 1, &pf, 1, v, sys_fences(), counter, s);
+                if (e != hipSuccess) rc = hip_fail(e, "scan push");
+                continue;
+            }
             hipError_t e = launch_push_wait(&ps, &pd, &pn, feeds ? 1 : 0, &pf, feeds ? 1 : 0, v, sys_fences(),
                                             counter + kCountWords,
                                             use ? w.flags(me) + kScanFlags + dst : w.flags(me), use ? 1 : 0, -1,
@@ -2419,12 +2532,32 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
             if (e != hipSuccess) { rc = hip_fail(e, "scan push"); break; }
             if (!use) continue;
             const char* tmp = w.sub(me, dst) + half;
-            rc = combine2(op.opidx, k, partial, tmp, partial, count, s);
-            if (rc == MPI_SUCCESS && me > dst)
-                rc = have ? combine2(op.opidx, k, res, tmp, res, count, s) : copy_async(res, tmp, bytes, s);
-            if (me > dst) have = true;
+            // the partial is read again only by a later step's push or combine
+            char* np = last ? nullptr : partial;
+            if (me > dst) {
+                char* nr = last ? outv : res;
+                if (have && same) {                      // one combine, stored twice
+                    rc = np ? combine2(op.opidx, k, cur_p, tmp, np, count, s, nr)
+                            : combine2(op.opidx, k, cur_r, tmp, nr, count, s);
+                } else {
+                    if (np) rc = combine2(op.opidx, k, cur_p, tmp, np, count, s);
+                    if (rc == MPI_SUCCESS)
+                        rc = have ? combine2(op.opidx, k, cur_r, tmp, nr, count, s) : copy_async(nr, tmp, bytes, s);
+                    same = false;
+                }
+                cur_p = np;
+                cur_r = nr;
+                have = true;
+            } else {                                     // never the last step (use)
+                rc = combine2(op.opidx, k, cur_p, tmp, partial, count, s);
+                cur_p = partial;
+                same = false;
+            }
         }
-        if (rc == MPI_SUCCESS && have) rc = copy_async(dstv, res, bytes, s);
+        // a result that never left the send buffer or the scratch (rank 0 of an
+        // inclusive scan, or a last step that did not fold) goes to recvbuf
+        if (rc == MPI_SUCCESS && have && (cur_r != outv || !dst_dev))
+            rc = copy_async(dst_dev ? static_cast<void*>(outv) : recvbuf, cur_r, bytes, s);
         const int rs = sync_stream(s, "scan");
         if (rc == MPI_SUCCESS) rc = rs;
         if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
@@ -2436,6 +2569,8 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
         tp->window_open = true;
         return rc;
     }
+    rc = copy_async(partial, srcv, bytes, s);
+    if (rc == MPI_SUCCESS && !exclusive) rc = copy_async(res, srcv, bytes, s);
     if (rc == MPI_SUCCESS) rc = sync_stream(s, "scan init");
     int slot = 0;
     for (int mask = 1; mask < p && rc == MPI_SUCCESS; mask <<= 1) {

@@ -158,6 +158,20 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
             fails.append(f"iscan {opn} excl={excl} rc={rc} {msx.last_error()}")
         elif not (excl and rank == 0):
             check(f"iscan {opn} {dtn} excl={excl}", fromdev(rb2, xs[rank]), exp[rank])
+        # MPI_IN_PLACE: the input is read from recvbuf, the result replaces it
+        rb3 = todev(xs[rank])
+        rc = fn(ctypes.c_void_p(-1), rb3.data_ptr(), count, dt, op, C.MPI_COMM_WORLD)
+        if rc != 0:
+            fails.append(f"scan in place {opn} excl={excl} rc={rc} {msx.last_error()}")
+        elif not (excl and rank == 0):
+            check(f"scan in place {opn} {dtn} excl={excl}", fromdev(rb3, xs[rank]), exp[rank])
+        # small pageable host buffers (below the pin threshold): staged for the kernels
+        hs, hr = raw(xs[rank]), raw(np.zeros_like(xs[rank]))
+        rc = fn(hs.ctypes.data, hr.ctypes.data, count, dt, op, C.MPI_COMM_WORLD)
+        if rc != 0:
+            fails.append(f"scan host {opn} excl={excl} rc={rc} {msx.last_error()}")
+        elif not (excl and rank == 0):
+            check(f"scan host {opn} {dtn} excl={excl}", hr, exp[rank])
 
 # Host (pageable) buffers above MSX_HOST_PIN_MIN: pinned for the call and used
 # in place by the kernels (allreduce send/recv and in place, reduce_scatter,
