@@ -362,6 +362,24 @@ MPI_METHOD MPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Data
 MPI_METHOD MPI_Compare_and_swap(const void* origin_addr, const void* compare_addr,
                                 void* result_addr, MPI_Datatype datatype, int target_rank,
                                 MPI_Aint target_disp, MPI_Win win);
+/* request-based RMA (api/mpi_rma.cpp:187,486,813,1215): passive-target
+ * epochs; the operation is flushed to its target and the request returned
+ * complete */
+MPI_METHOD MPI_Rput(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                    int target_rank, MPI_Aint target_disp, int target_count,
+                    MPI_Datatype target_datatype, MPI_Win win, MPI_Request* request);
+MPI_METHOD MPI_Rget(void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                    int target_rank, MPI_Aint target_disp, int target_count,
+                    MPI_Datatype target_datatype, MPI_Win win, MPI_Request* request);
+MPI_METHOD MPI_Raccumulate(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                           int target_rank, MPI_Aint target_disp, int target_count,
+                           MPI_Datatype target_datatype, MPI_Op op, MPI_Win win,
+                           MPI_Request* request);
+MPI_METHOD MPI_Rget_accumulate(const void* origin_addr, int origin_count,
+                               MPI_Datatype origin_datatype, void* result_addr, int result_count,
+                               MPI_Datatype result_datatype, int target_rank, MPI_Aint target_disp,
+                               int target_count, MPI_Datatype target_datatype, MPI_Op op,
+                               MPI_Win win, MPI_Request* request);
 
 /* ---- groups (api/mpi_group.cpp, api/mpi_comm.cpp:677) -------------------- */
 MPI_METHOD MPI_Comm_group(MPI_Comm comm, MPI_Group* group);
@@ -544,6 +562,22 @@ MPI_METHOD PMPI_Get_accumulate(const void* origin_addr, int origin_count,
                                MPI_Datatype target_datatype, MPI_Op op, MPI_Win win);
 MPI_METHOD PMPI_Fetch_and_op(const void* origin_addr, void* result_addr, MPI_Datatype datatype,
                              int target_rank, MPI_Aint target_disp, MPI_Op op, MPI_Win win);
+MPI_METHOD PMPI_Rput(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                     int target_rank, MPI_Aint target_disp, int target_count,
+                     MPI_Datatype target_datatype, MPI_Win win, MPI_Request* request);
+MPI_METHOD PMPI_Rget(void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                     int target_rank, MPI_Aint target_disp, int target_count,
+                     MPI_Datatype target_datatype, MPI_Win win, MPI_Request* request);
+MPI_METHOD PMPI_Raccumulate(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                            int target_rank, MPI_Aint target_disp, int target_count,
+                            MPI_Datatype target_datatype, MPI_Op op, MPI_Win win,
+                            MPI_Request* request);
+MPI_METHOD PMPI_Rget_accumulate(const void* origin_addr, int origin_count,
+                                MPI_Datatype origin_datatype, void* result_addr, int result_count,
+                                MPI_Datatype result_datatype, int target_rank,
+                                MPI_Aint target_disp, int target_count,
+                                MPI_Datatype target_datatype, MPI_Op op, MPI_Win win,
+                                MPI_Request* request);
 MPI_METHOD PMPI_Comm_group(MPI_Comm comm, MPI_Group* group);
 MPI_METHOD PMPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm* newcomm);
 MPI_METHOD PMPI_Comm_compare(MPI_Comm comm1, MPI_Comm comm2, int* result);

@@ -1278,11 +1278,7 @@ MSX_EXPORT int MPI_Request_free(MPI_Request* request)
     MSX_REQUIRE_INIT("MPI_Request_free");
     if (!request) { set_error("null request"); return err_return(nullptr, "MPI_Request_free", MPI_ERR_ARG); }
     int rc = request_validate(*request);
-    if (rc == MPI_SUCCESS) {
-        set_error("request 0x%x: invalid kind (a nonblocking collective request cannot be freed)",
-                  (unsigned)*request);
-        rc = MPI_ERR_OTHER;
-    }
+    if (rc == MPI_SUCCESS) rc = request_free(request);
     return err_return(nullptr, "MPI_Request_free", rc);
 }
 
@@ -1322,6 +1318,13 @@ MSX_ALIAS(MPI_Testsome) int PMPI_Testsome(int, MPI_Request[], int*, int[], MPI_S
 MSX_ALIAS(MPI_Waitany) int PMPI_Waitany(int, MPI_Request[], int*, MPI_Status*);
 MSX_ALIAS(MPI_Waitsome) int PMPI_Waitsome(int, MPI_Request[], int*, int[], MPI_Status[]);
 MSX_ALIAS(MPI_Request_free) int PMPI_Request_free(MPI_Request*);
+MSX_ALIAS(MPI_Rput) int PMPI_Rput(const void*, int, MPI_Datatype, int, MPI_Aint, int, MPI_Datatype, MPI_Win,
+                                  MPI_Request*);
+MSX_ALIAS(MPI_Rget) int PMPI_Rget(void*, int, MPI_Datatype, int, MPI_Aint, int, MPI_Datatype, MPI_Win, MPI_Request*);
+MSX_ALIAS(MPI_Raccumulate) int PMPI_Raccumulate(const void*, int, MPI_Datatype, int, MPI_Aint, int, MPI_Datatype,
+                                                MPI_Op, MPI_Win, MPI_Request*);
+MSX_ALIAS(MPI_Rget_accumulate) int PMPI_Rget_accumulate(const void*, int, MPI_Datatype, void*, int, MPI_Datatype, int,
+                                                        MPI_Aint, int, MPI_Datatype, MPI_Op, MPI_Win, MPI_Request*);
 MSX_ALIAS(MPI_Request_get_status) int PMPI_Request_get_status(MPI_Request, int*, MPI_Status*);
 MSX_ALIAS(MPI_Reduce) int PMPI_Reduce(const void*, void*, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
 MSX_ALIAS(MPI_Allreduce) int PMPI_Allreduce(const void*, void*, int, MPI_Datatype, MPI_Op, MPI_Comm);
@@ -2136,6 +2139,126 @@ MSX_EXPORT int MPI_Compare_and_swap(const void* origin_addr, const void* compare
         rc = rma_issue(w, RMA_CAS, target_rank, target_disp, O_REPLACE, origin_addr, 1, datatype, result_addr, 1,
                        datatype, 1, datatype, compare_addr);
     return err_win(w, "MPI_Compare_and_swap", rc);
+}
+
+// ---- request-based RMA (api/mpi_rma.cpp:187 MPI_Rput, 486 MPI_Rget, 813
+// MPI_Raccumulate, 1215 MPI_Rget_accumulate; MPID_Win_R* mpid/win.cpp:1324-1900).
+// The operation is validated and queued exactly as its plain form.  Its request
+// must complete without a synchronisation call, so the target's queue is
+// flushed at once (the reference completes the request when its queued
+// operation has gone out, at the latest at the next flush / unlock) and a
+// complete request is returned.  Passive-target epochs only (MPI-3 11.3.5):
+// in a fence or PSCW epoch the call fails with MPI_ERR_RMA_SYNC.
+namespace {
+int rma_request_pre(RmaWin* w, MPI_Request* request, int target)
+{
+    if (!request) { set_error("**nullptr request"); return MPI_ERR_ARG; }
+    *request = MPI_REQUEST_NULL;
+    if (target != MPI_PROC_NULL && target >= 0 && target < w->comm->size && !w->lock_all &&
+        !w->lock_mode[(size_t)target]) {
+        set_error("request-based RMA outside a passive-target epoch on rank %d (**rmasync)", target);
+        return MPI_ERR_RMA_SYNC;
+    }
+    return MPI_SUCCESS;
+}
+
+int rma_request_post(RmaWin* w, int target, int rc, MPI_Request* request)
+{
+    if (rc == MPI_SUCCESS && target != MPI_PROC_NULL) rc = engine_rma_flush(w, target);
+    if (rc == MPI_SUCCESS) rc = request_completed_rma(request, MPI_SUCCESS);
+    return rc;
+}
+}  // namespace
+
+MSX_EXPORT int MPI_Rput(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype, int target_rank,
+                        MPI_Aint target_disp, int target_count, MPI_Datatype target_datatype, MPI_Win win,
+                        MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Rput");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Rput", rc);
+    rc = rma_request_pre(w, request, target_rank);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = rma_issue(w, RMA_PUT, target_rank, target_disp, O_REPLACE, origin_addr, origin_count, origin_datatype,
+                       nullptr, 0, MPI_DATATYPE_NULL, target_count, target_datatype, nullptr);
+    if (rc == MPI_SUCCESS) rc = rma_request_post(w, target_rank, rc, request);
+    return err_win(w, "MPI_Rput", rc);
+}
+
+MSX_EXPORT int MPI_Rget(void* origin_addr, int origin_count, MPI_Datatype origin_datatype, int target_rank,
+                        MPI_Aint target_disp, int target_count, MPI_Datatype target_datatype, MPI_Win win,
+                        MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Rget");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Rget", rc);
+    rc = rma_request_pre(w, request, target_rank);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = rma_issue(w, RMA_GET, target_rank, target_disp, O_NOOP, nullptr, 0, MPI_DATATYPE_NULL, origin_addr,
+                       origin_count, origin_datatype, target_count, target_datatype, nullptr);
+    if (rc == MPI_SUCCESS) rc = rma_request_post(w, target_rank, rc, request);
+    return err_win(w, "MPI_Rget", rc);
+}
+
+MSX_EXPORT int MPI_Raccumulate(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                               int target_rank, MPI_Aint target_disp, int target_count,
+                               MPI_Datatype target_datatype, MPI_Op op, MPI_Win win, MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Raccumulate");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Raccumulate", rc);
+    OpRef r;
+    rc = rma_request_pre(w, request, target_rank);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = rma_op(op, &r, false);        // MPI_NO_OP: **noopnotallowed
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && origin_count > 0)
+        rc = rma_issue(w, RMA_ACC, target_rank, target_disp, r.opidx, origin_addr, origin_count, origin_datatype,
+                       nullptr, 0, MPI_DATATYPE_NULL, target_count, target_datatype, nullptr);
+    if (rc == MPI_SUCCESS) rc = rma_request_post(w, target_rank, rc, request);
+    return err_win(w, "MPI_Raccumulate", rc);
+}
+
+MSX_EXPORT int MPI_Rget_accumulate(const void* origin_addr, int origin_count, MPI_Datatype origin_datatype,
+                                   void* result_addr, int result_count, MPI_Datatype result_datatype,
+                                   int target_rank, MPI_Aint target_disp, int target_count,
+                                   MPI_Datatype target_datatype, MPI_Op op, MPI_Win win, MPI_Request* request)
+{
+    MSX_REQUIRE_INIT("MPI_Rget_accumulate");
+    RmaWin* w;
+    int rc = v_win(win, &w);
+    if (rc != MPI_SUCCESS) return err_win(nullptr, "MPI_Rget_accumulate", rc);
+    OpRef r;
+    rc = rma_request_pre(w, request, target_rank);
+    if (rc == MPI_SUCCESS) rc = v_op_handle(op, &r);
+    const bool noop = rc == MPI_SUCCESS && r.opidx == O_NOOP;
+    if (rc == MPI_SUCCESS && !noop) rc = v_dtype_any(origin_addr, origin_count, origin_datatype);
+    if (rc == MPI_SUCCESS) rc = v_dtype_any(result_addr, result_count, result_datatype);
+    if (rc == MPI_SUCCESS) rc = v_target(w, target_count, target_datatype, target_rank, target_disp);
+    if (rc == MPI_SUCCESS) rc = rma_op(op, &r, true);
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && result_count > 0) {
+        rc = v_match(result_count, result_datatype, target_count, target_datatype);
+        if (rc == MPI_SUCCESS && !noop) rc = v_match(origin_count, origin_datatype, target_count, target_datatype);
+    }
+    if (rc == MPI_SUCCESS && target_rank != MPI_PROC_NULL && target_count > 0)
+        rc = rma_issue(w, noop ? RMA_GET : RMA_GACC, target_rank, target_disp, r.opidx, origin_addr, origin_count,
+                       origin_datatype, result_addr, result_count, result_datatype, target_count, target_datatype,
+                       nullptr);
+    if (rc == MPI_SUCCESS) rc = rma_request_post(w, target_rank, rc, request);
+    return err_win(w, "MPI_Rget_accumulate", rc);
 }
 
 // ===========================================================================

@@ -283,6 +283,7 @@ int coll_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Dat
 // ---------------------------------------------------------------------------
 struct Request {
     bool live = false;
+    bool rma = false;              // request-based RMA operation (MPI_Rput ... MPI_Rget_accumulate)
     bool done = false;
     int rc = MPI_SUCCESS;
     bool has_fut = false;
@@ -351,6 +352,32 @@ int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req, 
     req_alloc(req, &r);
     r->done = true;
     r->rc = rc;
+    return MPI_SUCCESS;
+}
+
+int request_completed_rma(MPI_Request* req, int rc)
+{
+    Request* r;
+    req_alloc(req, &r);
+    r->rma = true;
+    r->done = true;
+    r->rc = rc;
+    return MPI_SUCCESS;
+}
+
+int request_free(MPI_Request* req)
+{
+    Request* r = req_lookup(*req);
+    if (!r) { set_error("invalid request handle 0x%x", (unsigned)*req); return MPI_ERR_REQUEST; }
+    if (!r->rma) {
+        set_error("request 0x%x: invalid kind (a nonblocking collective request cannot be freed)", (unsigned)*req);
+        return MPI_ERR_OTHER;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_req_mu);
+        r->live = false;
+    }
+    *req = MPI_REQUEST_NULL;
     return MPI_SUCCESS;
 }
 

@@ -89,6 +89,10 @@ int request_start_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t 
 // type in use by a pending operation defers its destruction).
 int request_start_generic(Comm* c, std::function<int()> body, MPI_Request* req,
                           MPI_Datatype hold = MPI_DATATYPE_NULL);
+// A complete request of a request-based RMA call (its operation already
+// flushed); MPI_Request_free releases these, and refuses collective requests.
+int request_completed_rma(MPI_Request* req, int rc);
+int request_free(MPI_Request* req);
 int request_wait(MPI_Request* req, MPI_Status* st);
 int request_test(MPI_Request* req, int* flag, MPI_Status* st);
 // completion helpers of the multi-request calls (api/mpi_completion.cpp)

@@ -808,3 +808,30 @@ FAPI void mpi_compare_and_swap_(void* o, void* c, void* r, const MPI_Fint* dt, c
     *ierr = MPI_Compare_and_swap(o, c, r, *dt, *target, *disp, *win);
 }
 FNAMES(compare_and_swap, COMPARE_AND_SWAP)
+FAPI void mpi_rput_(void* o, const MPI_Fint* ocount, const MPI_Fint* odt, const MPI_Fint* target, const MPI_Aint* disp,
+                    const MPI_Fint* tcount, const MPI_Fint* tdt, const MPI_Fint* win, MPI_Fint* req, MPI_Fint* ierr)
+{
+    *ierr = MPI_Rput(o, *ocount, *odt, *target, *disp, *tcount, *tdt, *win, req);
+}
+FNAMES(rput, RPUT)
+FAPI void mpi_rget_(void* o, const MPI_Fint* ocount, const MPI_Fint* odt, const MPI_Fint* target, const MPI_Aint* disp,
+                    const MPI_Fint* tcount, const MPI_Fint* tdt, const MPI_Fint* win, MPI_Fint* req, MPI_Fint* ierr)
+{
+    *ierr = MPI_Rget(o, *ocount, *odt, *target, *disp, *tcount, *tdt, *win, req);
+}
+FNAMES(rget, RGET)
+FAPI void mpi_raccumulate_(void* o, const MPI_Fint* ocount, const MPI_Fint* odt, const MPI_Fint* target,
+                           const MPI_Aint* disp, const MPI_Fint* tcount, const MPI_Fint* tdt, const MPI_Fint* op,
+                           const MPI_Fint* win, MPI_Fint* req, MPI_Fint* ierr)
+{
+    *ierr = MPI_Raccumulate(o, *ocount, *odt, *target, *disp, *tcount, *tdt, *op, *win, req);
+}
+FNAMES(raccumulate, RACCUMULATE)
+FAPI void mpi_rget_accumulate_(void* o, const MPI_Fint* ocount, const MPI_Fint* odt, void* r, const MPI_Fint* rcount,
+                               const MPI_Fint* rdt, const MPI_Fint* target, const MPI_Aint* disp,
+                               const MPI_Fint* tcount, const MPI_Fint* tdt, const MPI_Fint* op, const MPI_Fint* win,
+                               MPI_Fint* req, MPI_Fint* ierr)
+{
+    *ierr = MPI_Rget_accumulate(o, *ocount, *odt, r, *rcount, *rdt, *target, *disp, *tcount, *tdt, *op, *win, req);
+}
+FNAMES(rget_accumulate, RGET_ACCUMULATE)

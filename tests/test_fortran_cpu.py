@@ -37,7 +37,7 @@ ENTRIES = [
     "group_compare", "group_free",
     "wtick", "query_thread", "is_thread_main", "get_version", "get_processor_name", "comm_create",
     "comm_compare", "comm_test_inter", "comm_remote_size", "comm_remote_group", "intercomm_create",
-    "intercomm_merge",
+    "intercomm_merge", "rput", "rget", "raccumulate", "rget_accumulate",
     "win_post", "win_start", "win_complete", "win_wait", "win_test", "win_get_group",
     "type_size", "type_size_x", "type_contiguous", "type_vector", "type_hvector", "type_create_hvector",
     "type_indexed", "type_hindexed", "type_create_hindexed", "type_create_indexed_block",

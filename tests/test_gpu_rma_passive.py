@@ -177,6 +177,64 @@ L.MPI_Barrier(C.MPI_COMM_WORLD)
 if not (np.all(arr[:p] == 1) and np.all(arr[p:] == 0)):
     fails.append(f"win_allocate contents {arr[:p + 1]}")
 ok(L.MPI_Win_free(ctypes.byref(w2)), "free 2")
+
+# 7. request-based RMA (api/mpi_rma.cpp:187,486,813,1215): MPI_Rget_accumulate
+#    tickets, MPI_Raccumulate (request freed), MPI_Rput / MPI_Rget round trip;
+#    outside a passive-target epoch MPI_ERR_RMA_SYNC
+vp, i32, i64, pr = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int)
+L.MPI_Rput.argtypes = [vp, i32, i32, i32, i64, i32, i32, i32, pr]
+L.MPI_Rget.argtypes = [vp, i32, i32, i32, i64, i32, i32, i32, pr]
+L.MPI_Raccumulate.argtypes = [vp, i32, i32, i32, i64, i32, i32, i32, i32, pr]
+L.MPI_Rget_accumulate.argtypes = [vp, i32, i32, vp, i32, i32, i32, i64, i32, i32, i32, i32, pr]
+M3 = 4096
+if HOSTWIN:
+    hw3 = np.zeros(M3, np.int32); b3 = hw3.ctypes.data
+    read3 = lambda: hw3.copy()
+else:
+    dw3 = torch.zeros(M3, dtype=torch.int32, device="cuda"); torch.cuda.synchronize(); b3 = dw3.data_ptr()
+    read3 = lambda: (torch.cuda.synchronize(), dw3.cpu().numpy())[1]
+w3 = ctypes.c_int()
+ok(L.MPI_Win_create(ctypes.c_void_p(b3), M3 * 4, 4, C.MPI_INFO_NULL, C.MPI_COMM_WORLD, ctypes.byref(w3)), "create 3")
+W3 = w3.value
+req = ctypes.c_int()
+if cls(L.MPI_Raccumulate(one.ctypes.data, 1, C.MPI_INT, 0, 0, 1, C.MPI_INT, C.MPI_SUM, W3, ctypes.byref(req))) \
+        != C.MPI_ERR_RMA_SYNC:
+    fails.append("raccumulate outside an epoch")
+ok(L.MPI_Win_lock_all(0, W3), "lock_all 3")
+t2 = []
+for it in range(10):
+    f = np.zeros(1, np.int32)
+    ok(L.MPI_Rget_accumulate(one.ctypes.data, 1, C.MPI_INT, f.ctypes.data, 1, C.MPI_INT, last, 0, 1, C.MPI_INT,
+                             C.MPI_SUM, W3, ctypes.byref(req)), "rget_accumulate")
+    ok(L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)), "wait rgacc")
+    t2.append(int(f[0]))
+vec = np.arange(256, dtype=np.int32) * (rank + 1)
+for t in range(p):
+    ok(L.MPI_Raccumulate(vec.ctypes.data, 256, C.MPI_INT, t, 256, 256, C.MPI_INT, C.MPI_SUM, W3, ctypes.byref(req)),
+       "raccumulate")
+    ok(L.MPI_Request_free(ctypes.byref(req)), "free rma request")
+pv = np.arange(64, dtype=np.int32) + 100 * rank
+for t in range(p):
+    ok(L.MPI_Rput(pv.ctypes.data, 64, C.MPI_INT, t, 1024 + 64 * rank, 64, C.MPI_INT, W3, ctypes.byref(req)), "rput")
+    ok(L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)), "wait rput")
+bk = np.zeros(64, np.int32)
+ok(L.MPI_Rget(bk.ctypes.data, 64, C.MPI_INT, nxt, 1024 + 64 * rank, 64, C.MPI_INT, W3, ctypes.byref(req)), "rget")
+ok(L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1)), "wait rget")
+if not np.array_equal(bk, pv):
+    fails.append("rput/rget round trip")
+ok(L.MPI_Win_unlock_all(W3), "unlock_all 3")
+L.MPI_Barrier(C.MPI_COMM_WORLD)
+w = read3()
+if rank == last and w[0] != 10 * p:
+    fails.append(f"rget_accumulate total {w[0]} != {10 * p}")
+if not np.array_equal(w[256:512], np.arange(256, dtype=np.int32) * sum(r + 1 for r in range(p))):
+    fails.append("raccumulate region")
+for r in range(p):
+    if not np.array_equal(w[1024 + 64 * r:1024 + 64 * (r + 1)], np.arange(64, dtype=np.int32) + 100 * r):
+        fails.append(f"rput region of rank {r}")
+if len(set(t2)) != 10:
+    fails.append("rget_accumulate tickets repeat")
+ok(L.MPI_Win_free(ctypes.byref(w3)), "free 3")
 print("RESULT", rank, p, len(fails), fails[:6], flush=True)
 L.MPI_Finalize()
 '''
