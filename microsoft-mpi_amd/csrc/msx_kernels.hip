@@ -716,9 +716,23 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     f.n = nflags;
     f.seq = seq;
     for (int i = 0; i < nflags; ++i) f.dst[i] = flags[i];
-    // four 16-byte granules per lane and pass; at most ~2048 pushing workgroups
-    size_t gx = (maxb / 16 + 1023) / 1024;
-    const size_t cap = nseg > 0 ? std::max<size_t>(1, 2048 / (size_t)nseg) : 1;
+    // MSX_PUSH_VECS 16-byte granules per workgroup and pass (default 1024:
+    // four per lane) and at most MSX_PUSH_GRID_CAP pushing workgroups in all
+    // (default 2048).  One granule per lane with up to 16384 workgroups (the
+    // copy kernel's geometry) measured no different on the shared GPU
+    // (scripts/push_cmp.sh, profiles/r02/copy/push_cmp.log).
+    static const size_t per_wg = [] {
+        const char* e = getenv("MSX_PUSH_VECS");
+        const long long v = e ? atoll(e) : 1024;
+        return v >= 256 ? (size_t)v : (size_t)256;
+    }();
+    static const size_t grid_cap = [] {
+        const char* e = getenv("MSX_PUSH_GRID_CAP");
+        const long long v = e ? atoll(e) : 2048;
+        return v >= 1 ? (size_t)v : (size_t)2048;
+    }();
+    size_t gx = (maxb / 16 + per_wg - 1) / per_wg;
+    const size_t cap = nseg > 0 ? std::max<size_t>(1, grid_cap / (size_t)nseg) : 1;
     if (gx < 1) gx = 1;
     if (gx > cap) gx = cap;
     const unsigned total = nseg > 0 ? (unsigned)(gx * (size_t)nseg) : 0u;
