@@ -119,6 +119,76 @@ __global__ __launch_bounds__(BLOCK) void k_combine_host(const T* __restrict__ in
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
 }
 
+// Mutually misaligned operands, both element-aligned (e.g. sub-arrays at
+// different offsets): the vector grid follows `io` (16-byte aligned), and the
+// matching 16 bytes of `in`, which straddle two aligned 16-byte chunks, are
+// loaded as those two chunks and realigned in registers (v_alignbyte), so
+// every load stays aligned and coalesced.  `s` = byte offset of in's vector
+// data from 16-byte alignment (1..15, a multiple of sizeof(T)).  Vector 0 and
+// the last vector are left to the scalar loop: their outer chunk reaches
+// before / past the operand.  Before this path such calls ran element by
+// element: 256 MiB fp32 at 4.9 TB/s, int8 at 1.7 TB/s.
+__device__ __forceinline__ u32x4 realign(const u32x4& A, const u32x4& B, unsigned s)
+{
+    const unsigned d[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    const unsigned r = s & 3;
+    u32x4 o;
+    switch (s >> 2) {
+    case 0:
+        o = u32x4{__builtin_amdgcn_alignbyte(d[1], d[0], r), __builtin_amdgcn_alignbyte(d[2], d[1], r),
+                  __builtin_amdgcn_alignbyte(d[3], d[2], r), __builtin_amdgcn_alignbyte(d[4], d[3], r)};
+        break;
+    case 1:
+        o = u32x4{__builtin_amdgcn_alignbyte(d[2], d[1], r), __builtin_amdgcn_alignbyte(d[3], d[2], r),
+                  __builtin_amdgcn_alignbyte(d[4], d[3], r), __builtin_amdgcn_alignbyte(d[5], d[4], r)};
+        break;
+    case 2:
+        o = u32x4{__builtin_amdgcn_alignbyte(d[3], d[2], r), __builtin_amdgcn_alignbyte(d[4], d[3], r),
+                  __builtin_amdgcn_alignbyte(d[5], d[4], r), __builtin_amdgcn_alignbyte(d[6], d[5], r)};
+        break;
+    default:
+        o = u32x4{__builtin_amdgcn_alignbyte(d[4], d[3], r), __builtin_amdgcn_alignbyte(d[5], d[4], r),
+                  __builtin_amdgcn_alignbyte(d[6], d[5], r), __builtin_amdgcn_alignbyte(d[7], d[6], r)};
+        break;
+    }
+    return o;
+}
+
+template <int OP, class T, class VT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_combine_shift(const T* __restrict__ in, T* __restrict__ io, size_t head,
+                                                         size_t nvec, size_t tail, unsigned s)
+{
+    constexpr size_t EPV = 16 / sizeof(T);
+    const u32x4* __restrict__ ain =
+        reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(in + head) - s);   // aligned
+    u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
+    const size_t bid = (size_t)xcd_tile(blockIdx.x, gridDim.x);
+    const size_t v = 1 + bid * BLOCK + threadIdx.x;
+    const bool live = v + 1 < nvec;
+    // chunk v+1 is the next lane's chunk v: taken with a lane shuffle, loaded
+    // only by the wave's last lane and the last live lane
+    u32x4 a = {0, 0, 0, 0}, y = {0, 0, 0, 0};
+    if (live) {
+        a = ld<true>(ain + v);
+        y = ld<true>(vio + v);
+    }
+    issued_together(a, y);
+    u32x4 b;
+    b.x = __shfl_down(a.x, 1);
+    b.y = __shfl_down(a.y, 1);
+    b.z = __shfl_down(a.z, 1);
+    b.w = __shfl_down(a.w, 1);
+    if (live && ((threadIdx.x & 63) == 63 || v + 2 >= nvec)) b = ld<true>(ain + v + 1);
+    if (live) vio[v] = apply_vec<OP, VT>(y, realign(a, b, s));
+    // scalar: [0, head + EPV) and [head + (nvec - 1) * EPV, head + nvec * EPV + tail)
+    const size_t first = head + EPV, last0 = head + (nvec - 1) * EPV;
+    const size_t nscalar = first + (EPV + tail);
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < nscalar; i += (size_t)gridDim.x * BLOCK) {
+        const size_t e = i < first ? i : last0 + (i - first);
+        io[e] = Fn<OP>::apply(io[e], in[e]);
+    }
+}
+
 // Tuning variant: KT consecutive tiles per workgroup (one contiguous run of
 // KT*BLOCK vectors per operand) instead of one tile per workgroup; UNR = the
 // KT tiles' loads may all be in flight together (else one tile at a time).
@@ -345,10 +415,41 @@ inline void split(const void* in, const void* io, size_t count, size_t& head, si
     head = h; nvec = rest / epv; tail = rest - nvec * epv;
 }
 
+// The realigning path (k_combine_shift): both operands element-aligned but
+// at different offsets from 16-byte alignment, and at least 3 vectors.
+template <class T>
+inline bool split_shift(const void* in, const void* io, size_t count, size_t& head, size_t& nvec, size_t& tail,
+                        unsigned& s)
+{
+    constexpr size_t ES = sizeof(T);
+    const uintptr_t a = (uintptr_t)in, b = (uintptr_t)io;
+    if (ES >= 16 || (16 % ES) != 0 || (a & 15) == (b & 15) || (a % ES) != 0 || (b % ES) != 0) return false;
+    const size_t h = ((16 - (b & 15)) & 15) / ES;
+    if (h >= count) return false;
+    const size_t epv = 16 / ES;
+    const size_t nv = (count - h) / epv;
+    if (nv < 3) return false;
+    head = h;
+    nvec = nv;
+    tail = count - h - nv * epv;
+    s = (unsigned)((a + h * ES) & 15);
+    return true;
+}
+
 template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
 hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
 {
     size_t head, nvec, tail;
+    unsigned sh = 0;
+    if (!cfg.host && cfg.grid_cap == 0 && split_shift<T>(in, io, count, head, nvec, tail, sh)) {
+        size_t grid = (nvec + BLOCK - 1) / BLOCK;
+        const size_t sc = (head + tail + 2 * (16 / sizeof(T)) + BLOCK - 1) / BLOCK;
+        if (grid < sc) grid = sc;
+        if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
+                           static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
+        return hipGetLastError();
+    }
     split<T>(in, io, count, head, nvec, tail);
     const size_t tile = (size_t)BLOCK * UNROLL;
     size_t grid = (nvec + tile - 1) / tile;

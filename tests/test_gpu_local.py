@@ -115,6 +115,43 @@ def test_unaligned_and_misaligned_pointers(L, dt):
             _check_dev(L, op, dt, a, b, off_in, off_io)
 
 
+def test_realigned_operands_every_pair(L):
+    # k_combine_shift: `in` and `inout` element-aligned at different offsets from
+    # 16-byte alignment (every relative shift a type allows), every legal pair,
+    # sizes around the 3-vector threshold and a ragged larger one
+    rng = np.random.default_rng(71)
+    for op, dt in legal_pairs(oracle):
+        kind = KIND[dt]
+        esz = itemsize(kind)
+        if esz >= 16:
+            continue
+        for n in (3 * (16 // esz) - 1, 3 * (16 // esz) + 1, 5003):
+            a, b = gen(kind, op, n, rng), gen(kind, op, n, rng)
+            for off_in, off_io in ((esz, 0), (0, esz), (16 - esz, 2 * esz % 16)):
+                if off_in % 16 == off_io % 16:
+                    continue
+                _check_dev(L, op, dt, a, b, off_in, off_io)
+    # byte data at every byte shift (bitwise ops run on raw bytes)
+    for shift in range(1, 16):
+        a = rng.integers(0, 256, 4099, dtype=np.uint8)
+        b = rng.integers(0, 256, 4099, dtype=np.uint8)
+        _check_dev(L, "MPI_BXOR", "MPI_BYTE", a, b, shift, 0)
+        _check_dev(L, "MPI_SUM", "MPI_INT8_T", a.view(np.int8), b.view(np.int8), 0, shift)
+
+
+def test_realigned_operands_full_size(L):
+    # 256 MiB fp32 SUM with `in` 4 bytes off: bit-exact vs torch (one IEEE add)
+    n = (64 << 20) - 4
+    g = torch.Generator(device="cuda").manual_seed(11)
+    a = torch.rand(n + 4, device="cuda", generator=g)
+    b = torch.rand(n, device="cuda", generator=g)
+    exp = b + a[1:n + 1]
+    torch.cuda.synchronize()
+    assert L.msx_reduce_local_dev(a.data_ptr() + 4, b.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(b.view(torch.int32), exp.view(torch.int32))
+
+
 def test_loc_whole_struct_copy_includes_padding(L):
     # loctype `*this = rhs` (op.cpp:327) copies the whole struct
     rng = np.random.default_rng(9)
