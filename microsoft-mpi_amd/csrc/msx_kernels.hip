@@ -441,7 +441,7 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
 {
     size_t head, nvec, tail;
     unsigned sh = 0;
-    if (!cfg.host && cfg.grid_cap == 0 && split_shift<T>(in, io, count, head, nvec, tail, sh)) {
+    if (cfg.grid_cap == 0 && split_shift<T>(in, io, count, head, nvec, tail, sh)) {
         size_t grid = (nvec + BLOCK - 1) / BLOCK;
         const size_t sc = (head + tail + 2 * (16 / sizeof(T)) + BLOCK - 1) / BLOCK;
         if (grid < sc) grid = sc;
