@@ -327,6 +327,28 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
         gbs = 3 * n * sz.value / ms / 1e6
         out[f"{opn}/{dtn}"] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1),
                                "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    # mutually misaligned operands (k_combine_shift): `in` a few bytes past
+    # 16-byte alignment, `inout` aligned, same 256 MiB
+    for dtn, off in (("MPI_FLOAT", 4), ("MPI_INT8_T", 1)):
+        dt = getattr(C, dtn)
+        esz = L.msx_type_size(dt)
+        n = (nbytes - 16) // esz
+        ts = []
+        for _ in range(3):
+            L.msx_reduce_local_dev(a.data_ptr() + off, b.data_ptr(), n, dt, C.MPI_SUM, sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(10):
+                rc = L.msx_reduce_local_dev(a.data_ptr() + off, b.data_ptr(), n, dt, C.MPI_SUM, sp)
+                if rc:
+                    raise RuntimeError(f"misaligned {dtn}: rc={rc}")
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 10)
+        ms = sorted(ts)[1]
+        gbs = 3 * n * esz / ms / 1e6
+        out[f"MPI_SUM/{dtn}/in+{off}B"] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1),
+                                           "frac": round(gbs / HBM_PEAK_GBS, 4)}
     # the collective combine (k_tree): p = 8 contributions of 32 MiB reduced in
     # the reference's tree order into one output, (p + 1) x 32 MiB of traffic.
     # Sources placed as the engine's window lays out its IN sub-slots (32 MiB
