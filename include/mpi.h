@@ -503,7 +503,7 @@ MPI_METHOD MPI_Unpack(const void* inbuf, int insize, int* position, void* outbuf
                       MPI_Datatype datatype, MPI_Comm comm);
 MPI_METHOD MPI_Pack_size(int incount, MPI_Datatype datatype, MPI_Comm comm, int* size);
 
-/* ---- Fortran handle conversion (mpi.h:6816-6848): handles are already ints - */
+/* ---- Fortran handle conversion (mpi.h:6816-6876): handles are already ints - */
 #define MPI_Comm_c2f(comm)         (MPI_Fint)(comm)
 #define MPI_Comm_f2c(comm)         (MPI_Comm)(comm)
 #define MPI_Type_c2f(datatype)     (MPI_Fint)(datatype)
@@ -514,6 +514,24 @@ MPI_METHOD MPI_Pack_size(int incount, MPI_Datatype datatype, MPI_Comm comm, int*
 #define MPI_Request_f2c(request)   (MPI_Request)(request)
 #define MPI_Win_c2f(win)           (MPI_Fint)(win)
 #define MPI_Win_f2c(win)           (MPI_Win)(win)
+#define MPI_Group_c2f(group)       (MPI_Fint)(group)
+#define MPI_Group_f2c(group)       (MPI_Group)(group)
+#define MPI_Info_c2f(info)         (MPI_Fint)(info)
+#define MPI_Info_f2c(info)         (MPI_Info)(info)
+#define MPI_Errhandler_c2f(errhandler) (MPI_Fint)(errhandler)
+#define MPI_Errhandler_f2c(errhandler) (MPI_Errhandler)(errhandler)
+#define PMPI_Comm_c2f(comm)        (MPI_Fint)(comm)
+#define PMPI_Comm_f2c(comm)        (MPI_Comm)(comm)
+#define PMPI_Type_c2f(datatype)    (MPI_Fint)(datatype)
+#define PMPI_Type_f2c(datatype)    (MPI_Datatype)(datatype)
+#define PMPI_Op_c2f(op)            (MPI_Fint)(op)
+#define PMPI_Op_f2c(op)            (MPI_Op)(op)
+#define PMPI_Request_c2f(request)  (MPI_Fint)(request)
+#define PMPI_Request_f2c(request)  (MPI_Request)(request)
+#define PMPI_Win_c2f(win)          (MPI_Fint)(win)
+#define PMPI_Win_f2c(win)          (MPI_Win)(win)
+#define PMPI_Group_c2f(group)      (MPI_Fint)(group)
+#define PMPI_Group_f2c(group)      (MPI_Group)(group)
 /* The Fortran bindings (mpif.h, include/mpif.h) are exported by the library
    as mpi_<name>_ with the MPI_<NAME>, mpi_<name>, mpi_<name>__ and PMPI_ aliases
    (microsoft-mpi_amd/csrc/msx_fortran.cpp). */
