@@ -660,6 +660,19 @@ hipError_t launch_tree(int opidx, Kind k, const void* const* srcs, int p, void* 
     return launch_tree_spec(opidx, k, t, out, n, s);
 }
 
+// Write-through stores (st_wt) for data that GPU flags announce to peers:
+// the two-step pushes (k_push_wait) and tree results behind result-ready
+// flags.  MSX_WT_STORES=0 keeps plain stores (correct only while the peer
+// windows are mapped uncached on the writer).
+static bool wt_stores()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_WT_STORES");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
 hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t n, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
@@ -721,6 +734,8 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     if (t.done_counter) {
         if (t.done_nflags < 0 || t.done_nflags > 64 || t.done_launches < 1) return hipErrorInvalidValue;
         a.done_counter = t.done_counter;
+        // buffer-store offsets are 32-bit: larger ranges keep plain stores
+        a.wt = (wt_stores() && n * kind_size(k) < ((size_t)1 << 32)) ? 1 : 0;
         a.done_launches = t.done_launches;
         a.done_flags.n = t.done_nflags;
         a.done_flags.seq = t.done_seq;
@@ -837,6 +852,7 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     if (gx < 1) gx = 1;
     if (gx > cap) gx = cap;
     const unsigned total = nseg > 0 ? (unsigned)(gx * (size_t)nseg) : 0u;
+    c.wt = (wt_stores() && maxb < ((size_t)1 << 32)) ? 1 : 0;   // 32-bit buffer offsets
     hipLaunchKernelGGL(k_push_wait, dim3(total + 1), dim3(256), 0, s, c, f, counter, total, sys ? 1 : 0,
                        (unsigned)gx, wait_flags, seq, wait_n, wait_skip, wait_err);
     return hipGetLastError();

@@ -20,6 +20,7 @@ struct CopySegs {
     size_t nbytes[kMaxSegs];
     int n;
     int sys;
+    int wt;    // copy_post_body: write-through stores (st_wt), see there
 };
 
 struct PostFlags {
@@ -41,6 +42,57 @@ __device__ __forceinline__ void stores_done()
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// Write-through stores for data a GPU flag announces to another GPU: relaxed
+// system-scope atomic stores, i.e. global_store_* sc0 sc1, which the L2 passes
+// through to the owner's memory whatever MTYPE the importer maps the peer
+// window with.  Once such a store has completed (stores_done), it is visible
+// at the owner, so the flag protocol does not rest on the windows being
+// mapped uncached on the WRITER (an NC mapping would leave plain stores dirty
+// in this XCD's L2, where only an L2 writeback, ~20x slower per workgroup,
+// could push them out).
+__device__ __forceinline__ void st_wt(u32x4* p, u32x4 v)
+{
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(d, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(d + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// 16-byte write-through stores in bulk: buffer_store_dwordx4 with the same
+// sc0 sc1 policy (aux 17), through a raw buffer resource on a workgroup-
+// uniform base (wt_rsrc) and a byte offset below 4 GiB (the launchers only
+// set `wt` for ranges that satisfy this).  Half the store instructions of
+// st_wt's two 8-byte atomics.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(void* base)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)0xFFFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ void st_wt_at(__amdgpu_buffer_rsrc_t r, size_t off, u32x4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(unsigned)off, 0, 17);
+}
+
+// One element of 1, 2, 4, 8 or 16 bytes, write-through (the scalar tails).
+template <class T>
+__device__ __forceinline__ void st_wt_elem(T* p, const T& v)
+{
+    static_assert(sizeof(T) == 1 || sizeof(T) == 2 || sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16,
+                  "element size");
+    if constexpr (sizeof(T) == 16) {
+        u32x4 w;
+        __builtin_memcpy(&w, &v, 16);
+        st_wt(reinterpret_cast<u32x4*>(p), w);
+    } else {
+        using W = typename std::conditional<sizeof(T) == 1, unsigned char,
+                  typename std::conditional<sizeof(T) == 2, unsigned short,
+                  typename std::conditional<sizeof(T) == 4, unsigned, unsigned long long>::type>::type>::type;
+        W w;
+        __builtin_memcpy(&w, &v, sizeof(T));
+        __hip_atomic_store(reinterpret_cast<W*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // The small-allreduce push (k_push_post, and the first workgroups of a fused
 // k_tree launch): see the comment at k_push_post.
 __device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
@@ -51,24 +103,15 @@ __device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlag
     const size_t nb = c.nbytes[sg];
     const size_t stride = (size_t)gx * 256;
     size_t done = 0;
-    bool plain = false;
     if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
         const size_t nv = nb / 16;
-        for (size_t i = (size_t)bx * 256 + threadIdx.x; i < nv; i += stride) {
-            const u32x4 v = reinterpret_cast<const u32x4*>(src)[i];
-            unsigned long long* d = reinterpret_cast<unsigned long long*>(dst) + 2 * i;
-            __hip_atomic_store(d, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(d + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        for (size_t i = (size_t)bx * 256 + threadIdx.x; i < nv; i += stride)
+            st_wt(reinterpret_cast<u32x4*>(dst) + i, reinterpret_cast<const u32x4*>(src)[i]);
         done = nv * 16;
     }
-    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) {
-        dst[i] = src[i];
-        plain = true;
-    }
-    if (sys || plain) __threadfence_system();          // plain byte stores: write this XCD's L2 back
+    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride)
+        st_wt_elem(dst + i, src[i]);
+    if (sys) __threadfence_system();
     else stores_done();                                 // vmcnt(0): this lane's stores completed
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -102,12 +145,12 @@ __device__ __forceinline__ bool count_done(unsigned* base, unsigned b, unsigned 
     return true;
 }
 
-// Bulk variant for multi-MiB segments (the two-step allreduce's pieces): plain
-// 16-byte stores from a full grid, four loads in flight per lane (as
-// k_copy_segs), then push_post_body's fenced count and flag post.  Plain
-// stores to peer windows rely on the windows' uncached mapping like every
-// other bulk transfer of the engine; `sys` (cached windows) writes the L2
-// back at system scope before counting.
+// Bulk variant for multi-MiB segments (the two-step allreduce's pieces):
+// write-through stores (st_wt) from a full grid, four loads in flight per lane
+// (as k_copy_segs), then push_post_body's fenced count and flag post.  `sys`
+// (cached windows) writes the L2 back at system scope before counting.
+// MSX_WT_STORES=0 (wt == 0) keeps plain 16-byte stores, which rely on the
+// windows' uncached mapping at the writer.
 __device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
                                                unsigned total, int sys, unsigned bx, unsigned gx, int sg)
 {
@@ -121,14 +164,27 @@ __device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlag
         const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
         u32x4* d4 = reinterpret_cast<u32x4*>(dst);
         size_t i = (size_t)bx * 256 + threadIdx.x;
-        for (; i + 3 * stride < nv; i += 4 * stride) {
-            const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
-            d4[i] = a0; d4[i + stride] = a1; d4[i + 2 * stride] = a2; d4[i + 3 * stride] = a3;
+        if (c.wt) {
+            const __amdgpu_buffer_rsrc_t r = wt_rsrc(dst);
+            for (; i + 3 * stride < nv; i += 4 * stride) {
+                const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
+                st_wt_at(r, 16 * i, a0); st_wt_at(r, 16 * (i + stride), a1);
+                st_wt_at(r, 16 * (i + 2 * stride), a2); st_wt_at(r, 16 * (i + 3 * stride), a3);
+            }
+            for (; i < nv; i += stride) st_wt_at(r, 16 * i, s4[i]);
+        } else {
+            for (; i + 3 * stride < nv; i += 4 * stride) {
+                const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
+                d4[i] = a0; d4[i + stride] = a1; d4[i + 2 * stride] = a2; d4[i + 3 * stride] = a3;
+            }
+            for (; i < nv; i += stride) d4[i] = s4[i];
         }
-        for (; i < nv; i += stride) d4[i] = s4[i];
         done = nv * 16;
     }
-    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
+    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) {
+        if (c.wt) st_wt_elem(dst + i, src[i]);
+        else dst[i] = src[i];
+    }
     if (sys) __threadfence_system();
     else stores_done();
     __syncthreads();
@@ -161,6 +217,7 @@ struct TreeArgs {
     unsigned pairmask;
     int chain;
     int sys;   // sources/outputs shared with other GPUs: system-coherent access
+    int wt;    // results announced by done_flags: write-through stores (st_wt)
     const unsigned long long* wait_flags;   // see TreeSpec
     unsigned long long wait_seq;
     int wait_n;
@@ -337,6 +394,19 @@ __device__ __forceinline__ u32x4 tree_vec(const TreeArgs& a, size_t i)
     return v[0];
 }
 
+// Result vector i into `out` and every extra destination; write-through when
+// done_flags will announce it to other GPUs (TreeArgs::wt).
+__device__ __forceinline__ void put_vec(const TreeArgs& a, u32x4* __restrict__ out, size_t i, u32x4 r)
+{
+    if (a.wt) {
+        st_wt_at(wt_rsrc(out), 16 * i, r);
+        for (int e = 0; e < a.nextra; ++e) st_wt_at(wt_rsrc(a.extra[e]), 16 * i, r);
+    } else {
+        out[i] = r;
+        for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
+    }
+}
+
 template <int OP, class VT> struct VecFn {
     __device__ static u32x4 apply(u32x4 io, u32x4 in) { return apply_vec<OP, VT>(io, in); }
 };
@@ -384,8 +454,7 @@ __device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict_
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const u32x4 r = reduce(v[u]);
-                out[i0 + (size_t)u * BLOCK] = r;
-                for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i0 + (size_t)u * BLOCK] = r;
+                put_vec(a, out, i0 + (size_t)u * BLOCK, r);
             }
         } else {
 #pragma unroll
@@ -396,8 +465,7 @@ __device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict_
 #pragma unroll
                     for (int k = 0; k < NL; ++k) v[k] = ld<NT>(src[k] + i);
                     const u32x4 r = reduce(v);
-                    out[i] = r;
-                    for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
+                    put_vec(a, out, i, r);
                 }
             }
         }
@@ -444,8 +512,7 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
                 auto load = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
                 r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
             }
-            reinterpret_cast<u32x4*>(out)[i] = r;
-            for (int e = 0; e < a.nextra; ++e) reinterpret_cast<u32x4*>(a.extra[e])[i] = r;
+            put_vec(a, reinterpret_cast<u32x4*>(out), i, r);
         }
     }
     const size_t first = vec_ok ? nvec * EPV : 0;
@@ -453,8 +520,13 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
     for (size_t s = (size_t)b * BLOCK + threadIdx.x; s < nsc; s += stride) {
         auto load = [&](int k) { return reinterpret_cast<const T*>(a.s[k])[first + s]; };
         const T r = tree_eval<Fn<OP>, T>(a, load);
-        out[first + s] = r;
-        for (int e = 0; e < a.nextra; ++e) static_cast<T*>(a.extra[e])[first + s] = r;
+        if (a.wt) {
+            st_wt_elem(out + first + s, r);
+            for (int e = 0; e < a.nextra; ++e) st_wt_elem(static_cast<T*>(a.extra[e]) + first + s, r);
+        } else {
+            out[first + s] = r;
+            for (int e = 0; e < a.nextra; ++e) static_cast<T*>(a.extra[e])[first + s] = r;
+        }
     }
     if (a.sys) release_system();
     if (a.done_counter) tree_done(a, b, nb);
