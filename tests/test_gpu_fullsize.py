@@ -8,6 +8,8 @@ the ranks sharing this box's one GPU (the 8-GPU node is the driver's):
       selects recursive halving, reduce.cpp:1705), p = 2
   c5  MPI_Iallreduce MPI_BAND MPI_UINT64_T, 512 MiB per rank, overlapped with
       host work before MPI_Wait, p = 2
+  and all three with the configs' own rank count, p = 8 (fp32 SUM checked
+  against the 8-leaf balanced tree of the reference's Rabenseifner order)
 
 Size-independent checks, computed on the GPU by every rank from the other
 ranks' seeds: fp32 SUM is the reference association (x0 + x1) + x2 (IEEE adds
@@ -70,9 +72,18 @@ if CFG == "c3":
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     done("c3 allreduce", L.MPI_Allreduce(x.data_ptr(), y.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, W), t0)
-    exp = gen_f32(0x5EED, n)
-    for r in range(1, p):
-        exp = exp + gen_f32(0x5EED + r, n)        # ((x0 + x1) + x2): the fold's tree for p = 3
+    del x
+    if p & (p - 1) == 0:
+        # power of two: the balanced tree ((x0+x1)+(x2+x3))+((x4+x5)+(x6+x7)), reduce.cpp:3890-4009
+        level = [gen_f32(0x5EED + r, n) for r in range(0, p, 2)]
+        level = [a.add_(gen_f32(0x5EED + 2 * i + 1, n)) for i, a in enumerate(level)]
+        while len(level) > 1:
+            level = [level[i].add_(level[i + 1]) for i in range(0, len(level), 2)]
+        exp = level[0]
+    else:
+        exp = gen_f32(0x5EED, n)
+        for r in range(1, p):
+            exp = exp + gen_f32(0x5EED + r, n)    # ((x0 + x1) + x2): the fold's tree for p = 3
     torch.cuda.synchronize()
     if not torch.equal(y.view(torch.int32), exp.view(torch.int32)):
         fails.append(f"c3: {(y != exp).sum().item()} elements differ")
@@ -128,7 +139,7 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("cfg,p", [("c3", 2), ("c3", 3), ("c4", 2), ("c5", 2)])
+@pytest.mark.parametrize("cfg,p", [("c3", 2), ("c3", 3), ("c4", 2), ("c5", 2), ("c3", 8), ("c4", 8), ("c5", 8)])
 def test_baseline_config_full_size(cfg, p):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -143,7 +154,7 @@ def test_baseline_config_full_size(cfg, p):
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
-    deadline = time.monotonic() + 150
+    deadline = time.monotonic() + (150 if p <= 3 else 220)
     for pr in procs:
         try:
             o, e = pr.communicate(timeout=max(1.0, deadline - time.monotonic()))

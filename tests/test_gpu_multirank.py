@@ -392,7 +392,8 @@ def _free_port():
                                                         (3, 65536, "rccl", None), (8, None, None, None),
                                                         (7, 1 << 20, None, None), (3, None, None, "0"),
                                                         (4, 65536, None, "0"), (3, None, None, "unfused"),
-                                                        (4, None, None, "ts512k"), (6, None, None, None)])
+                                                        (4, None, None, "ts512k"), (6, None, None, None),
+                                                        (3, None, None, "plain_stores")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -410,6 +411,8 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             env["MSX_TRANSPORT"] = transport
         if rd_flags == "unfused":
             env["MSX_FUSED_PUSH"] = "0"             # flag path with a separate push launch
+        elif rd_flags == "plain_stores":
+            env["MSX_WT_STORES"] = "0"              # two-step pushes / results with plain stores
         elif rd_flags == "ts512k":
             env["MSX_TWO_STEP_MAX"] = str(512 << 10)   # two-step and host-barrier Rabenseifner alternate
         elif rd_flags is not None:
