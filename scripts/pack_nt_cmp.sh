@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the datatype pack/unpack kernels with plain (default) vs non-temporal
-# typed-side accesses (MSX_DT_TYPED_NT=1): bench.py's pack table, alternating runs.
+# typed-side accesses (MSX_DT_TYPED_NT=1, a variant since removed: see DESIGN 3b): bench.py pack table.
 cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out/pack_nt
 for i in 0 1; do
