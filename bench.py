@@ -643,7 +643,11 @@ def main():
         dist.barrier()
     # timed region: K back-to-back launches on `stream`, bracketed by HIP
     # events on that stream (kernel time incl. launch gaps) and by the host
-    # clock between barrier + synchronize on both sides (value).
+    # clock between barrier + synchronize on both sides (value).  Each rank's
+    # clock stops at its own final synchronize, before the closing barrier:
+    # the MAX over ranks below covers the slowest rank, and the barrier's own
+    # TCP round trips (gloo, ~0.1-1 ms for 8 processes) stay out of a region
+    # that lasts ~2 ms at K = 20.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -652,9 +656,9 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
