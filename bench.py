@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--coll-scale", type=float, default=1.0, help="size factor for c3-c5")
     ap.add_argument("--no-per-op", action="store_true", help="skip the per-(op, type) roofline table")
     ap.add_argument("--no-pack", action="store_true", help="skip the datatype pack/unpack table")
+    ap.add_argument("--rccl-native-child", metavar="OUT", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -100,32 +101,64 @@ class stdout_to_stderr:
         os.close(self.saved)
 
 
-def rccl_native_allreduce(dist, torch, world, dev, scale):
-    """xGMI reference point: RCCL's own fp32 SUM allreduce (its ring/tree order,
-    NOT the reference's association) on c3's 1 GiB/rank, same GPUs."""
-    try:
-        g = dist.new_group(backend="nccl")
-        n = int((1 << 28) * scale)
-        x = torch.ones(n, device=dev)
-        for _ in range(2):
-            dist.all_reduce(x, group=g)
-        torch.cuda.synchronize()
-        dist.barrier()
-        reps, t0 = 5, time.perf_counter()
-        for _ in range(reps):
-            dist.all_reduce(x, group=g)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / reps
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t[0])
+def rccl_native_child_main(out, scale):
+    """Child-process body of rccl_native_allreduce: its own torch.distributed
+    job (backend "nccl" = RCCL) on this rank's GPU; rank 0 writes the JSON."""
+    import torch
+    import torch.distributed as dist
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    local = int(os.environ["LOCAL_RANK"]) % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+    n = int((1 << 28) * scale)
+    x = torch.ones(n, device="cuda")
+    for _ in range(2):
+        dist.all_reduce(x)
+    torch.cuda.synchronize()
+    dist.barrier()
+    reps, t0 = 5, time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(x)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ok = bool(torch.all(x == float(world) ** (reps + 2)).item())
+    if rank == 0:
         alg = n * 4 / dt / 1e9
-        del x
-        torch.cuda.empty_cache()
-        return {"bytes_per_rank": n * 4, "seconds": round(dt, 5), "algbw_GB_s": round(alg, 2),
-                "busbw_GB_s": round(alg * 2 * (world - 1) / world, 2)}
-    except Exception as e:      # reported, never fatal for the headline line
-        return {"error": repr(e)[:300]}
+        with open(out, "w") as f:
+            json.dump({"bytes_per_rank": n * 4, "seconds": round(dt, 5), "algbw_GB_s": round(alg, 2),
+                       "busbw_GB_s": round(alg * 2 * (world - 1) / world, 2), "correct": ok}, f)
+    dist.destroy_process_group()
+
+
+def rccl_native_allreduce(world, rank, local, scale):
+    """xGMI reference point: RCCL's own fp32 SUM allreduce (its ring/tree order,
+    NOT the reference's association) on c3's 1 GiB/rank, same GPUs.  Runs in a
+    child process per rank with its own rendezvous and a time limit, so an
+    RCCL failure or hang is reported in the JSON line and never stalls it."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"msx_rccl_native_{os.environ.get('MASTER_PORT', '0')}.json")
+    env = dict(os.environ)
+    env.update({"MASTER_PORT": str((int(os.environ.get("MASTER_PORT", "29500")) + 131) % 65536),
+                "RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(local)})
+    try:
+        pr = subprocess.run([sys.executable, os.path.abspath(__file__), "--rccl-native-child", out,
+                             "--coll-scale", str(scale)], env=env, capture_output=True, text=True,
+                            timeout=float(os.environ.get("MSX_RCCL_NATIVE_TIMEOUT", "120")))
+        if pr.returncode != 0:
+            return {"error": f"rank {rank} child rc={pr.returncode}: {pr.stderr[-600:]}"}
+    except subprocess.TimeoutExpired:
+        return {"error": f"rank {rank} child timed out"}
+    if rank == 0:
+        try:
+            with open(out) as f:
+                return json.load(f)
+        except (OSError, ValueError) as e:
+            return {"error": str(e)}
+    return {}
 
 
 def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 1, 256, true, false>"):
@@ -544,6 +577,9 @@ def rma_self_roofline(L, C, torch, dev, n):
 
 def main():
     args = parse()
+    if args.rccl_native_child:
+        rccl_native_child_main(args.rccl_native_child, args.coll_scale)
+        return
     import torch
     import torch.distributed as dist
     import msx
@@ -682,8 +718,12 @@ def main():
         coll = collect("ipc")
         if distinct:
             coll_rccl = collect("rccl")
-            with stdout_to_stderr():
-                rccl_native = rccl_native_allreduce(dist, torch, world, dev, args.coll_scale)
+            mine = rccl_native_allreduce(world, rank, local, args.coll_scale)
+            ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            rccl_native = mine if rank == 0 else None
+            if rank == 0 and not ok.item() and "error" not in rccl_native:
+                rccl_native["error"] = "a non-zero rank's child failed"
 
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
