@@ -33,6 +33,17 @@ hipError_t launch_dt_acc(int opidx, Kind k, const DevLayout& L, int64_t count, c
 namespace {
 
 constexpr int64_t kMaxRuns = (int64_t)1 << 25;     // explicit runs kept per type
+
+// Two-level compact forms (Dtype::rn2); MSX_DT_COMPACT2=0 expands them into
+// explicit run lists as before (A/B and fallback).
+bool compact2_enabled()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_DT_COMPACT2");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
 constexpr int kPairSlots = 5;                       // direct slots 0..4: MPI_FLOAT_INT .. MPI_LONG_DOUBLE_INT
 constexpr unsigned kDirectTypeBits = 0x8c000000u;   // HANDLE_TYPE_DIRECT | MPID_DATATYPE
 
@@ -162,7 +173,7 @@ void destroy(Dtype* t)
 // The single run of a one-run type (either form).
 bool single_run(const Dtype* t, DtRun* r)
 {
-    if (t->rn == 1) { *r = {t->rfirst, t->rlen}; return true; }
+    if (t->rn == 1 && t->rn2 == 1) { *r = {t->rfirst, t->rlen}; return true; }
     if (t->rn == 0 && t->runs.size() == 1) { *r = t->runs[0]; return true; }
     return false;
 }
@@ -174,6 +185,8 @@ void copy_layout(Dtype* t, const Dtype* o)
     t->rfirst = o->rfirst;
     t->rlen = o->rlen;
     t->rstride = o->rstride;
+    t->rn2 = o->rn2;
+    t->rstride2 = o->rstride2;
 }
 
 // Append `nrep` copies of old's runs, copy r at disp0 + r*ext.  A compact old
@@ -184,12 +197,12 @@ int append_copies(std::vector<DtRun>& out, const Dtype* old, int64_t disp0, int6
     std::vector<DtRun> expanded;
     const std::vector<DtRun>* runs = &old->runs;
     if (old->rn) {
-        if (old->rn > kMaxRuns) {
+        if (old->rn > kMaxRuns / old->rn2) {
             set_error("datatype type map exceeds %lld contiguous pieces", (long long)kMaxRuns);
             return MPI_ERR_NO_MEM;
         }
-        expanded.reserve((size_t)old->rn);
-        for (int64_t k = 0; k < old->rn; ++k) push_run(expanded, old->rfirst + k * old->rstride, old->rlen);
+        expanded.reserve((size_t)(old->rn * old->rn2));
+        dtype_for_each_run(old, [&](int64_t d, int64_t l) { push_run(expanded, d, l); });
         runs = &expanded;
     }
     if (nrep <= 0 || runs->empty()) return MPI_SUCCESS;
@@ -292,7 +305,7 @@ int64_t dtype_size(MPI_Datatype h)
     return t ? t->size : -1;
 }
 
-int64_t dtype_nruns(const Dtype* t) { return t->rn ? t->rn : (int64_t)t->runs.size(); }
+int64_t dtype_nruns(const Dtype* t) { return t->rn ? t->rn * t->rn2 : (int64_t)t->runs.size(); }
 
 void dtype_add_ref(MPI_Datatype h)
 {
@@ -341,6 +354,14 @@ int dtype_vector(int count, int blocklen, int64_t stride, bool stride_bytes, MPI
             t->rfirst = r1.disp;
             t->rlen = blen;
             t->rstride = eff;
+        } else if (blocklen == 1 && count > 1 && o->rn > 1 && o->rn2 == 1 && compact2_enabled()) {
+            // one copy per block of a one-level compact type: two levels
+            t->rn = o->rn;
+            t->rfirst = o->rfirst;
+            t->rlen = o->rlen;
+            t->rstride = o->rstride;
+            t->rn2 = count;
+            t->rstride2 = eff;
         } else {
             for (int j = 0; j < count; ++j) {
                 int rc = append_copies(t->runs, o, (int64_t)j * eff, blocklen, a.extent);
@@ -468,6 +489,13 @@ int dtype_struct(int count, const int* blens, const MPI_Aint* disps, const MPI_D
         t = std::make_unique<Dtype>();
         bool found_slb = false, found_sub = false, found_tlb = false, found_tub = false, found_el = false;
         int64_t el_sz = 0, size = 0, tlb = 0, tub = 0, slb = 0, sub = 0, n_el = 0;
+        // One real entry of one copy of a compact type among LB/UB markers
+        // (MPI_Type_create_subarray / darray's closing struct): the layout
+        // stays compact, shifted by the entry's displacement.
+        int n_real = 0, sole = -1;
+        for (int k = 0; k < count; ++k)
+            if (blens[k] != 0 && types[k] != MPI_LB && types[k] != MPI_UB) { ++n_real; sole = k; }
+        const bool keep_compact = n_real == 1 && blens[sole] == 1 && !is_builtin_h(types[sole]) && olds[sole]->rn > 0;
         MPI_Datatype el_type = MPI_DATATYPE_NULL;
         for (i = 0; i < count; ++i) {
             if (blens[i] == 0) continue;
@@ -512,7 +540,10 @@ int dtype_struct(int count, const int* blens, const MPI_Aint* disps, const MPI_D
                 if (!found_tub) { found_tub = true; tub = tu; }
                 else if (tub < tu) tub = tu;
             }
-            if (!marker) {
+            if (!marker && keep_compact) {
+                copy_layout(t.get(), o);
+                t->rfirst += disps[i];
+            } else if (!marker) {
                 const int64_t oext = bi ? o->size : o->extent;
                 int rc = append_copies(t->runs, o, disps[i], blens[i], oext);
                 if (rc != MPI_SUCCESS) return rc;
@@ -907,11 +938,16 @@ int build_dev_layout(Dtype* t)
     if (t->rn) {
         // compact regular form: no run table at all
         al = std::min({al, lowbit_align(t->rfirst), lowbit_align(t->rlen), lowbit_align(t->rstride)});
+        if (t->rn2 > 1) al = std::min(al, lowbit_align(t->rstride2));
         L.align = (int)al;
         L.regular = 1;
         L.first = t->rfirst;
         L.blen = t->rlen;
         L.stride = t->rstride;
+        if (t->rn2 > 1) {
+            L.n1 = t->rn;
+            L.stride2 = t->rstride2;
+        }
         t->dev = L;
         t->dev_ready = true;
         return MPI_SUCCESS;
@@ -986,6 +1022,10 @@ void dtype_serialize(const Dtype* t, std::vector<int64_t>& out)
     out.push_back(t->size);
     out.push_back(t->extent);
     out.push_back((int64_t)t->eltype);
+    if (t->rn && t->rn2 > 1) {   // two-level compact form: flag -2, then first, len, stride, n, stride2, n2
+        out.insert(out.end(), {-2, t->rfirst, t->rlen, t->rstride, t->rn, t->rstride2, t->rn2});
+        return;
+    }
     if (t->rn) {            // compact form: flag -1, then first, len, stride, n
         out.insert(out.end(), {-1, t->rfirst, t->rlen, t->rstride, t->rn});
         return;
@@ -999,6 +1039,25 @@ void dtype_serialize(const Dtype* t, std::vector<int64_t>& out)
 
 Dtype* dtype_from_blob(const int64_t* b, int64_t avail)
 {
+    if (avail >= 10 && b[3] == -2) {
+        const int64_t lim = (int64_t)1 << 40;
+        if (b[5] <= 0 || b[7] <= 0 || b[9] <= 1 || b[7] > lim || b[9] > lim / b[7] || b[7] * b[9] * b[5] != b[0])
+            return nullptr;
+        auto* t = new Dtype();
+        t->size = b[0];
+        t->extent = b[1];
+        t->eltype = (MPI_Datatype)b[2];
+        const TypeInfo* ti = type_info(t->eltype);
+        t->el_size = ti ? ti->size : -1;
+        t->committed = true;
+        t->rfirst = b[4];
+        t->rlen = b[5];
+        t->rstride = b[6];
+        t->rn = b[7];
+        t->rstride2 = b[8];
+        t->rn2 = b[9];
+        return t;
+    }
     if (avail >= 8 && b[3] == -1) {
         if (b[7] <= 0 || b[5] <= 0 || b[7] > ((int64_t)1 << 40) || b[7] * b[5] != b[0]) return nullptr;
         auto* t = new Dtype();
@@ -1045,9 +1104,9 @@ void dt_span(const Dtype* t, int64_t count, int64_t* lo, int64_t* hi)
     if ((t->runs.empty() && !t->rn) || count <= 0) { *lo = *hi = 0; return; }
     int64_t rl = INT64_MAX, rh = INT64_MIN;
     if (t->rn) {
-        const int64_t last = t->rfirst + (t->rn - 1) * t->rstride;
-        rl = std::min(t->rfirst, last);
-        rh = std::max(t->rfirst, last) + t->rlen;
+        const int64_t d1 = (t->rn - 1) * t->rstride, d2 = (t->rn2 - 1) * t->rstride2;
+        rl = t->rfirst + std::min<int64_t>(0, d1) + std::min<int64_t>(0, d2);
+        rh = t->rfirst + std::max<int64_t>(0, d1) + std::max<int64_t>(0, d2) + t->rlen;
     }
     for (const DtRun& r : t->runs) {
         rl = std::min(rl, r.disp);

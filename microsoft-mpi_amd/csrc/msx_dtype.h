@@ -35,9 +35,11 @@ struct DevLayout {
     int64_t size = 0;      // data bytes per instance (sum of run lengths)
     int64_t extent = 0;    // instance stride in bytes
     int64_t nruns = 0;
-    // regular form: run k = [first + k*stride, +blen), k < nruns
+    // regular form: run k = [first + k*stride, +blen), k < nruns; with n1 > 0
+    // (two levels) run k = [first + (k / n1)*stride2 + (k % n1)*stride, +blen)
     int regular = 0;
     int64_t first = 0, blen = 0, stride = 0;
+    int64_t n1 = 0, stride2 = 0;
     // general form: disp[k], poff[k] = packed offset of run k (poff[nruns] = size)
     const int64_t* disp = nullptr;
     const int64_t* poff = nullptr;
@@ -61,7 +63,11 @@ struct Dtype {
     // unmaterialised so huge strided types cost O(1) host memory: run k =
     // [rfirst + k*rstride, +rlen), k < rn; `runs` stays empty while rn > 0 and
     // is expanded only when another constructor needs the explicit list.
+    // Two levels (rn2 > 1: a vector / hvector / contiguous of such a type with
+    // one copy per block, e.g. the planes of a 3-D subarray): run (j, k) =
+    // [rfirst + j*rstride2 + k*rstride, +rlen), j < rn2 outer, k < rn inner.
     int64_t rn = 0, rfirst = 0, rlen = 0, rstride = 0;
+    int64_t rn2 = 1, rstride2 = 0;
     // MPI_Type_get_envelope / get_contents
     int combiner = 1;             // MPI_COMBINER_NAMED
     std::vector<int> ints;
@@ -81,6 +87,17 @@ bool dtype_is_derived(MPI_Datatype h);
 int64_t dtype_size(MPI_Datatype h);
 // Number of contiguous runs of one instance (compact or explicit form).
 int64_t dtype_nruns(const Dtype* t);
+// Visit the runs of one instance in type-map order (any form).
+template <class F>
+void dtype_for_each_run(const Dtype* t, F&& f)
+{
+    if (t->rn) {
+        for (int64_t j = 0; j < t->rn2; ++j)
+            for (int64_t k = 0; k < t->rn; ++k) f(t->rfirst + j * t->rstride2 + k * t->rstride, t->rlen);
+    } else {
+        for (const DtRun& r : t->runs) f(r.disp, r.len);
+    }
+}
 
 // ---- constructors (argument checks are the caller's; return MPI error class)
 // Each creates an uncommitted type and stores its handle in *out.

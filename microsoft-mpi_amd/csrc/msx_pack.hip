@@ -53,6 +53,9 @@ struct CopyArgs {
     int64_t stride;          // bytes
     int64_t gsize, gblen;    // granules
     FastDiv fd_size, fd_blen;
+    // two-level regular layout (n1 > 0): run k at first + (k / n1)*stride2 + (k % n1)*stride
+    int64_t n1, stride2;
+    FastDiv fd_n1;
     // general layout
     const int64_t* disp;
     const int64_t* poff;
@@ -97,6 +100,12 @@ __device__ __forceinline__ int64_t typed_off(const CopyArgs& a, int64_t g)
         if constexpr (NARROW) k = a.fd_blen.div((uint32_t)q);
         else k = q / a.gblen;
         const int64_t off = q - k * a.gblen;
+        if (a.n1) {             // two levels (uniform branch: a kernel argument)
+            int64_t k1;
+            if constexpr (NARROW) k1 = a.fd_n1.div((uint32_t)k);
+            else k1 = k / a.n1;
+            return i * a.extent + a.first + k1 * a.stride2 + (k - k1 * a.n1) * a.stride + off * G;
+        }
         return i * a.extent + a.first + k * a.stride + off * G;
     } else {
         const int64_t qb = q * G;
@@ -154,9 +163,18 @@ __global__ __launch_bounds__(kPackBlock) void k_dt_runs(CopyArgs a)
     // (dispatch order here: XCD-contiguous order measured 10 % slower for this kernel)
     for (int64_t u = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); u < nunits; u += nw) {
         const int64_t i = u / a.nruns, k = u - i * a.nruns;
-        const int64_t po = a.poff[k];
-        const int64_t len = (a.poff[k + 1] - po) / G;
-        T* t = reinterpret_cast<T*>(a.typed + i * a.extent + a.disp[k]);
+        int64_t po, len, disp;
+        if (a.n1) {             // two-level regular layout: run k computed, no tables
+            const int64_t k1 = k / a.n1;
+            po = k * a.gblen * G;
+            len = a.gblen;
+            disp = a.first + k1 * a.stride2 + (k - k1 * a.n1) * a.stride;
+        } else {
+            po = a.poff[k];
+            len = (a.poff[k + 1] - po) / G;
+            disp = a.disp[k];
+        }
+        T* t = reinterpret_cast<T*>(a.typed + i * a.extent + disp);
         T* p = reinterpret_cast<T*>(a.packed + i * a.size + po);
         for (int64_t j0 = lane; j0 < len; j0 += 64 * kUnroll) {
             T v[kUnroll];
@@ -221,10 +239,13 @@ CopyArgs make_args(const DevLayout& L, int64_t count, void* typed, void* packed,
     a.size = L.size;
     a.gsize = L.size / G;
     a.ngran = count * a.gsize;
+    a.nruns = L.nruns;
     if (L.regular) {
         a.first = L.first;
         a.stride = L.stride;
         a.gblen = L.blen / G;
+        a.n1 = L.n1;
+        a.stride2 = L.stride2;
     } else {
         a.disp = L.disp;
         a.poff = L.poff;
@@ -232,6 +253,7 @@ CopyArgs make_args(const DevLayout& L, int64_t count, void* typed, void* packed,
     }
     a.fd_size = FastDiv((uint32_t)(a.gsize < 0xffffffffll ? a.gsize : 1));
     a.fd_blen = FastDiv((uint32_t)(a.gblen > 0 && a.gblen < 0xffffffffll ? a.gblen : 1));
+    a.fd_n1 = FastDiv((uint32_t)(a.n1 > 0 && a.n1 < 0xffffffffll ? a.n1 : 1));
     return a;
 }
 
@@ -244,7 +266,8 @@ hipError_t run_copy(const CopyArgs& a, bool reg, hipStream_t s)
 {
     const bool narrow = a.ngran < (int64_t)0xffffffffll;
     const dim3 block(kPackBlock);
-    if (!reg && a.gsize >= kRunParallelMin * a.nruns) {
+    // long runs: irregular tables, or a two-level regular layout (3-D subarrays)
+    if ((!reg || a.n1) && a.gsize >= kRunParallelMin * a.nruns) {
         const int64_t units = (a.ngran / a.gsize) * a.nruns;
         const int64_t want = (units + kPackBlock / 64 - 1) / (kPackBlock / 64);
         const dim3 grid((unsigned)(want < 8192 ? want : 8192));

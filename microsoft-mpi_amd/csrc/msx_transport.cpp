@@ -994,12 +994,8 @@ int img_store(const Img& m, size_t count, const char* typed_base, void* buf)
         memcpy(packed.data() + p, typed_base + i * t->extent + disp, (size_t)len);
         p += (size_t)len;
     };
-    for (size_t i = 0; i < count; ++i) {
-        if (t->rn)
-            for (int64_t k = 0; k < t->rn; ++k) run((int64_t)i, t->rfirst + k * t->rstride, t->rlen);
-        else
-            for (const DtRun& r : t->runs) run((int64_t)i, r.disp, r.len);
-    }
+    for (size_t i = 0; i < count; ++i)
+        dtype_for_each_run(t, [&](int64_t disp, int64_t len) { run((int64_t)i, disp, len); });
     return dt_unpack_any(t, (int64_t)count, packed.data(), buf);
 }
 

@@ -459,6 +459,36 @@ def test_huge_strided_vector_stays_compact(msxlib):
     assert L.MPI_Type_free(ctypes.byref(t)) == 0 and L.MPI_Type_free(ctypes.byref(u)) == 0
 
 
+def test_vector_of_vector_and_3d_subarray_stay_compact(msxlib):
+    """Two-level compact form: an hvector (one copy per block) of a strided
+    vector keeps (first, length, stride, n, stride2, n2) instead of n * n2
+    explicit runs -- 2^30 runs here, 32x the explicit limit, built and
+    committed at once with the reference's attributes; likewise a 3-D
+    subarray of a 2^40-byte array (its closing LB/UB struct keeps the form)."""
+    import time
+    L = msxlib
+    inner, outer = c_int(), c_int()
+    t0 = time.perf_counter()
+    assert L.MPI_Type_vector(1 << 15, 1, 2, C.MPI_FLOAT, ctypes.byref(inner)) == 0
+    assert L.MPI_Type_create_hvector(1 << 15, 1, 1 << 18, inner.value, ctypes.byref(outer)) == 0
+    assert L.MPI_Type_commit(ctypes.byref(outer)) == 0
+    ext_in = ((1 << 15) - 1) * 8 + 4
+    ext = ((1 << 15) - 1) * (1 << 18) + ext_in
+    assert lib_attrs(L, outer.value) == (4 << 30, 0, ext, 0, ext)
+    sub = c_int()
+    dims, subs, starts = [1 << 12, 1 << 13, 1 << 13], [1 << 11, 1 << 12, 1 << 12], [5, 7, 9]
+    assert L.MPI_Type_create_subarray(3, ibuf(dims), ibuf(subs), ibuf(starts), C.MPI_ORDER_C, C.MPI_FLOAT,
+                                      ctypes.byref(sub)) == 0
+    assert L.MPI_Type_commit(ctypes.byref(sub)) == 0
+    assert time.perf_counter() - t0 < 0.5
+    first = ((5 * (1 << 13) + 7) * (1 << 13) + 9) * 4
+    tl = first
+    tu = first + (((1 << 11) - 1) * (1 << 13) + (1 << 12) - 1) * (1 << 13) * 4 + (1 << 12) * 4
+    assert lib_attrs(L, sub.value) == ((1 << 35) * 4, 0, (1 << 38) * 4, tl, tu - tl)
+    for h in (inner, outer, sub):
+        assert L.MPI_Type_free(ctypes.byref(h)) == 0
+
+
 UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
                       ctypes.POINTER(ctypes.c_int))
 

@@ -290,6 +290,71 @@ def test_compact_vector_beyond_explicit_run_limit(L):
     assert L.MPI_Type_free(ctypes.byref(t)) == 0
 
 
+def test_two_level_compact_beyond_explicit_run_limit(L):
+    """Two-level compact form: an hvector of 2^14 rows, each a vector of 2^13
+    every-other fp32 -- 2^27 runs, 4x the explicit run-list limit -- packs
+    from (first, len, stride, n, stride2, n2) alone: MPI_Pack of a 1 GiB buffer
+    equals torch's x.view(2^14, 2^14)[:, ::2], unpack restores exactly it."""
+    n = 1 << 28
+    x = torch.randn(n, device="cuda")
+    inner, t = c_int(), c_int()
+    assert L.MPI_Type_vector(1 << 13, 1, 2, C.MPI_FLOAT, ctypes.byref(inner)) == 0
+    assert L.MPI_Type_create_hvector(1 << 14, 1, (1 << 14) * 4, inner.value, ctypes.byref(t)) == 0
+    assert L.MPI_Type_commit(ctypes.byref(t)) == 0
+    want = x.view(1 << 14, 1 << 14)[:, ::2].reshape(-1)
+    out = torch.empty(n // 2, device="cuda")
+    torch.cuda.synchronize()
+    pos = c_int(0)
+    assert L.MPI_Pack(x.data_ptr(), 1, t.value, out.data_ptr(), 2 * n, ctypes.byref(pos), C.MPI_COMM_WORLD) == 0, \
+        msx.last_error()
+    torch.cuda.synchronize()
+    assert pos.value == 2 * n
+    bad = (out != want).nonzero().flatten()
+    assert bad.numel() == 0, (bad.numel(), bad[:8].tolist())
+    y = torch.zeros_like(x)
+    torch.cuda.synchronize()
+    pos = c_int(0)
+    assert L.MPI_Unpack(out.data_ptr(), 2 * n, ctypes.byref(pos), y.data_ptr(), 1, t.value, C.MPI_COMM_WORLD) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y[::2], x[::2]) and not y[1::2].any()
+    for h in (inner, t):
+        assert L.MPI_Type_free(ctypes.byref(h)) == 0
+
+
+@pytest.mark.parametrize("order", ["C", "F"])
+def test_subarray_3d_two_level_form_matches_torch(L, order):
+    """3-D subarrays (C and Fortran order) now keep the two-level compact form
+    through their LB/UB struct: pack / unpack against torch slicing, with rows
+    long enough for the run-parallel kernel and short enough for the granule
+    map, device buffers."""
+    for dims, sub, st in (((48, 64, 96), (20, 30, 40), (3, 5, 7)), ((40, 50, 6), (10, 20, 3), (1, 2, 3))):
+        x = torch.randn(*dims, device="cuda")
+        ia = lambda v: (ctypes.c_int * 3)(*v)
+        t = c_int()
+        o = C.MPI_ORDER_C if order == "C" else C.MPI_ORDER_FORTRAN
+        d, s_, st_ = (dims, sub, st) if order == "C" else (dims[::-1], sub[::-1], st[::-1])
+        assert L.MPI_Type_create_subarray(3, ia(d), ia(s_), ia(st_), o, C.MPI_FLOAT, ctypes.byref(t)) == 0
+        assert L.MPI_Type_commit(ctypes.byref(t)) == 0
+        want = x[st[0]:st[0] + sub[0], st[1]:st[1] + sub[1], st[2]:st[2] + sub[2]].reshape(-1)
+        out = torch.empty(want.numel(), device="cuda")
+        torch.cuda.synchronize()
+        pos = c_int(0)
+        assert L.MPI_Pack(x.data_ptr(), 1, t.value, out.data_ptr(), out.numel() * 4, ctypes.byref(pos),
+                          C.MPI_COMM_WORLD) == 0, msx.last_error()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want), (dims, order)
+        y = torch.zeros_like(x)
+        torch.cuda.synchronize()
+        pos = c_int(0)
+        assert L.MPI_Unpack(out.data_ptr(), out.numel() * 4, ctypes.byref(pos), y.data_ptr(), 1, t.value,
+                            C.MPI_COMM_WORLD) == 0
+        torch.cuda.synchronize()
+        m = torch.zeros_like(x, dtype=torch.bool)
+        m[st[0]:st[0] + sub[0], st[1]:st[1] + sub[1], st[2]:st[2] + sub[2]] = True
+        assert torch.equal(y[m], x[m]) and not y[~m].any(), (dims, order)
+        assert L.MPI_Type_free(ctypes.byref(t)) == 0
+
+
 def test_reduce_local_user_op_derived_type_device_buffers(L):
     """User op + derived type on DEVICE buffers: the library stages the type's
     byte span through host memory around the user function; the bytes between
