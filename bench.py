@@ -415,6 +415,13 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
         return {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
     out["tree8/MPI_SUM/MPI_FLOAT"] = entry(time_tree())
+    # HBM bytes per launch from the committed PMC passes (16-B streaming loads:
+    # FETCH_SIZE doubled per the gfx950 calibration), against (p + 1) * 32 MiB
+    raw = pmc_raw("k_tree<3, float, float, 256, false, false, 8, 1, false>")
+    if raw:
+        out["tree8/MPI_SUM/MPI_FLOAT"].update(
+            {"pmc_raw_kib": raw, "traffic": int((2 * raw["FETCH_SIZE"] + raw["WRITE_SIZE"]) * 1024),
+             "bytes_per_launch": (p + 1) * m * 4})
     out["tree8_pow2_stride/MPI_SUM/MPI_FLOAT"] = entry(time_tree(srcs_pow2))
     if tree_sweep:
         for mode, name in ((8, "generic"), (1, "generic_upfront"), (2, "generic_upfront_nt"),
