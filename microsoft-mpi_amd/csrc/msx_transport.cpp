@@ -604,11 +604,40 @@ Leaf leaf_of(int n, int p)
     return l;
 }
 
+// The flat communicators' algorithm switch points (Mpi.SwitchoverSettings
+// [COLL_SWITCHOVER_FLAT], mpid/env.cpp:514-608): MPICH_DEFAULT_*_MSG override
+// the coll.h defaults as env_to_int does (common/mpiutil.cpp:65-91): unset or
+// longer than the 11-character buffer -> default, else _wtoi's value,
+// clamped below at 0.  Read once; every rank must see the same environment,
+// as with the reference.
+namespace {
+uint32_t env_switch(const char* name, int defval)
+{
+    const char* v = getenv(name);
+    if (!v || strlen(v) > 11) return (uint32_t)defval;
+    long long x = strtoll(v, nullptr, 10);           // _wtoi: leading blanks, sign, digits
+    if (x > INT32_MAX) x = INT32_MAX;
+    if (x < 0) x = 0;                                // minval 0
+    return (uint32_t)x;
+}
+struct SwitchPoints {
+    uint32_t allreduce_short = env_switch("MPICH_DEFAULT_ALLREDUCE_SHORT_MSG", 262144);
+    uint32_t reduce_short = env_switch("MPICH_DEFAULT_REDUCE_SHORT_MSG", 65536);
+    uint32_t redscat_long = env_switch("MPICH_DEFAULT_REDSCAT_COMMUTATIVE_LONG_MSG", 524288);
+};
+const SwitchPoints& switch_points()
+{
+    static const SwitchPoints sp;
+    return sp;
+}
+}  // namespace
+
 int allreduce_algo(int p, size_t count, int type_size, bool builtin)
 {
     // reduce.cpp:3884-3888; count*type_size is evaluated in 32 bits.
     const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)type_size);
-    if (nbytes <= 262144u || !builtin || count < (size_t)pof2_floor(p)) return A_RECURSIVE_DOUBLING;
+    if (nbytes <= switch_points().allreduce_short || !builtin || count < (size_t)pof2_floor(p))
+        return A_RECURSIVE_DOUBLING;
     return A_RABENSEIFNER;
 }
 
@@ -616,9 +645,9 @@ int reduce_scatter_algo(int p, size_t total_count, int type_size, bool commutati
 {
     (void)p;
     if (!commutative) return -1;
-    // reduce.cpp:1705: nbytes = (unsigned)(total_count * type_size) wraps at 4 GiB.
+    // reduce.cpp:1705-1709: nbytes = (unsigned)(total_count * type_size) wraps at 4 GiB.
     const uint32_t nbytes = (uint32_t)((uint64_t)total_count * (uint64_t)type_size);
-    return nbytes < 524288u ? A_RS_HALVING : A_RS_PAIRWISE;
+    return nbytes < switch_points().redscat_long ? A_RS_HALVING : A_RS_PAIRWISE;
 }
 
 static int log2i(int v)
@@ -685,9 +714,10 @@ RankTree tree_reduce_scatter(int p, int n)
 
 int reduce_algo(int p, size_t count, int type_size, bool builtin)
 {
-    // reduce.cpp:151: (unsigned)(count*type_size) > reduce_short_msg (64 KiB)
+    // reduce.cpp:151: (unsigned)(count*type_size) > reduce_short_msg (64 KiB by default)
     const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)type_size);
-    return (nbytes > 65536u && builtin && count >= (size_t)pof2_floor(p)) ? A_RABENSEIFNER : A_BINOMIAL;
+    return (nbytes > switch_points().reduce_short && builtin && count >= (size_t)pof2_floor(p)) ? A_RABENSEIFNER
+                                                                                                : A_BINOMIAL;
 }
 
 RankTree tree_reduce_rsag(int p, int n)
@@ -1758,13 +1788,27 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev)
                                                   : (bounce_dst ? engine_bounce(1).dev : w.out(me));
             const bool disjoint = out + count * esz <= mine || mine + count * esz <= out;
-            const bool fuse = want && fused_push() && !sg.src.empty() && disjoint;
+            // Every workgroup of a waiting tree spins until the peers' flags
+            // arrive.  Up to 256 KiB (the default recursive-doubling range) the
+            // grid is small; a larger vector (switch points moved with
+            // MPICH_DEFAULT_*_MSG) gets the two-step pattern instead: ONE
+            // workgroup of the push launch waits, the tree follows on the
+            // stream -- thousands of spinning workgroups per rank starved the
+            // other ranks' pushes on a shared GPU until the 20 s bound.
+            const bool spin_tree = nbytes <= ((size_t)256 << 10);
+            const bool fuse = spin_tree && want && fused_push() && !sg.src.empty() && disjoint;
             unsigned* counter = nullptr;
             if (rc == MPI_SUCCESS && !sg.src.empty()) {
                 counter = tp->push_counter();
                 if (!counter) { set_error("allreduce: push counter allocation failed"); return MPI_ERR_NO_MEM; }
             }
-            if (rc == MPI_SUCCESS && !sg.src.empty() && !fuse) {
+            if (rc == MPI_SUCCESS && !spin_tree) {
+                hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
+                                                fl.data(), (int)fl.size(), seq, sys_fences(),
+                                                counter ? counter + kCountWords : nullptr, w.flags(me),
+                                                want ? p : 0, me, err_dev, s);
+                if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
+            } else if (rc == MPI_SUCCESS && !sg.src.empty() && !fuse) {
                 hipError_t e = launch_push_post(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
                                                 fl.data(), (int)fl.size(), seq, sys_fences(), counter, s);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
@@ -1772,7 +1816,10 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);   // nothing to push
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce arrival flags");
             }
-            if (rc == MPI_SUCCESS && want) {
+            if (rc == MPI_SUCCESS && want && !spin_tree) {
+                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s);   // after the wait, in stream order
+                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
+            } else if (rc == MPI_SUCCESS && want) {
                 TreeWait tw;
                 tw.flags = w.flags(me);
                 tw.seq = seq;

@@ -20,6 +20,19 @@
 
 #include "msx_oracle.h"
 
+/* The flat switch points (mpid/env.cpp:514-608 via env_to_int,
+ * common/mpiutil.cpp:65-91): MPICH_DEFAULT_* override the coll.h defaults;
+ * unset or longer than 11 characters -> default, else the integer, >= 0. */
+static uint32_t switch_point(const char* name, int defval)
+{
+    const char* v = getenv(name);
+    if (!v || strlen(v) > 11) return (uint32_t)defval;
+    long long x = strtoll(v, NULL, 10);
+    if (x > 2147483647LL) x = 2147483647LL;
+    if (x < 0) x = 0;
+    return (uint32_t)x;
+}
+
 static int pof2_floor(int p)
 {
     int v = 1;
@@ -72,7 +85,7 @@ int oracle_allreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
     for (int r = 0; r < p; ++r) if (newrank[r] >= 0) real[newrank[r]] = r;
 
     const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)esz);   /* :3884 */
-    if (nbytes <= 262144u || count < pof2) {
+    if (nbytes <= switch_point("MPICH_DEFAULT_ALLREDUCE_SHORT_MSG", 262144) || count < pof2) {
         /* recursive doubling (:3890-3926): commutative builtin -> Uop(tmp, recvbuf) */
         for (int mask = 1; mask < pof2; mask <<= 1) {
             for (int n = 0; n < pof2; ++n) memcpy(snap[real[n]], rb[real[n]], (size_t)bytes);
@@ -183,7 +196,7 @@ int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcoun
         const void* src = sendbufs[r] != MPI_IN_PLACE ? sendbufs[r] : recvbufs[r];
         memcpy(res[r], src, (size_t)bytes);
     }
-    if (nbytes < 524288u) {
+    if (nbytes < switch_point("MPICH_DEFAULT_REDSCAT_COMMUTATIVE_LONG_MSG", 524288)) {
         /* recursive halving (:917-1219) */
         const int pof2 = pof2_floor(p), rem = p - pof2;
         int* newrank = (int*)calloc((size_t)p, sizeof(int));
@@ -298,7 +311,7 @@ int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
     }
     const int pof2 = pof2_floor(p), rem = p - pof2;
     const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)esz);   /* :151 */
-    if (nbytes > 65536u && count >= pof2) {
+    if (nbytes > switch_point("MPICH_DEFAULT_REDUCE_SHORT_MSG", 65536) && count >= pof2) {
         int* real = (int*)calloc((size_t)pof2, sizeof(int));
         for (int r = 0; r < p; ++r) {
             if (r < 2 * rem) {

@@ -193,6 +193,73 @@ def test_algorithm_gates_follow_reference_32bit_arithmetic():
     assert algo(2, 8, 16384, 4) == 4 and algo(2, 8, 16385, 4) == 1
 
 
+SWITCH_WORKER = r'''
+import os, sys
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd")); sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np
+import msx, oracle
+from test_collectives_cpu import (algo, engine_allreduce_result, engine_reduce_result,
+                                  engine_reduce_scatter_result, _data)
+C = msx.C
+print("GATES", algo(0, 8, 64, 4), algo(0, 8, 70001, 4), algo(1, 8, 40, 4), algo(2, 8, 30000, 4), flush=True)
+bad = []
+for p in (3, 4, 8):
+    for count in (13, 70001):
+        xs = _data(p, count, C.MPI_SUM, 5 * p + count % 7)
+        rb = [np.zeros(count, np.float32) for _ in range(p)]
+        assert oracle.allreduce(C.MPI_SUM, C.MPI_FLOAT, xs, rb) == 0
+        for r in range(p):
+            if not np.array_equal(engine_allreduce_result(xs, C.MPI_SUM, C.MPI_FLOAT, r).view(np.uint32),
+                                  rb[r].view(np.uint32)):
+                bad.append(("allreduce", p, count, r))
+        for root in (0, p - 1):
+            exp = np.zeros(count, np.float32)
+            assert oracle.reduce(C.MPI_SUM, C.MPI_FLOAT, root, xs, exp) == 0
+            if not np.array_equal(engine_reduce_result(xs, C.MPI_SUM, C.MPI_FLOAT, root).view(np.uint32),
+                                  exp.view(np.uint32)):
+                bad.append(("reduce", p, count, root))
+    for per in (5, 9000):
+        counts = [per + (i % 3) for i in range(p)]
+        xs = _data(p, sum(counts), C.MPI_SUM, 3 * p + per)
+        rb = [np.zeros(c, np.float32) for c in counts]
+        assert oracle.reduce_scatter(C.MPI_SUM, C.MPI_FLOAT, counts, xs, rb) == 0
+        for r in range(p):
+            if not np.array_equal(engine_reduce_scatter_result(xs, counts, C.MPI_SUM, C.MPI_FLOAT, r).view(np.uint32),
+                                  rb[r].view(np.uint32)):
+                bad.append(("reduce_scatter", p, per, r))
+print("BAD", bad, flush=True)
+'''
+
+
+@pytest.mark.parametrize("env,gates", [
+    # every switch point at 0: Rabenseifner from 8 floats on, pairwise reduce_scatter
+    ({"MPICH_DEFAULT_ALLREDUCE_SHORT_MSG": "0", "MPICH_DEFAULT_REDUCE_SHORT_MSG": "0",
+      "MPICH_DEFAULT_REDSCAT_COMMUTATIVE_LONG_MSG": "0"}, "1 1 3 1"),
+    # huge: recursive doubling / binomial / recursive halving at every size
+    ({"MPICH_DEFAULT_ALLREDUCE_SHORT_MSG": "2147483647", "MPICH_DEFAULT_REDUCE_SHORT_MSG": "999999999",
+      "MPICH_DEFAULT_REDSCAT_COMMUTATIVE_LONG_MSG": "2000000000"}, "0 0 2 4"),
+    # negative -> clamped to 0 (env_to_int's minval); 12 characters -> ignored (default);
+    # 100 B: a 160-B reduce_scatter is already pairwise
+    ({"MPICH_DEFAULT_ALLREDUCE_SHORT_MSG": "-5", "MPICH_DEFAULT_REDUCE_SHORT_MSG": "000000065536",
+      "MPICH_DEFAULT_REDSCAT_COMMUTATIVE_LONG_MSG": "100"}, "1 1 3 1"),
+])
+def test_switch_points_follow_the_reference_environment(env, gates):
+    """MPICH_DEFAULT_{ALLREDUCE,REDUCE}_SHORT_MSG / _REDSCAT_COMMUTATIVE_LONG_MSG
+    move the flat algorithm switch points like mpid/env.cpp:514-608 (env_to_int:
+    unset or over 11 characters -> default, clamped at 0); engine schedules and
+    the oracle's step-by-step simulation (which reads the same variables) stay
+    bit-identical on both sides of every moved gate."""
+    e = dict(os.environ)
+    e.update(env)
+    pr = subprocess.run([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(SWITCH_WORKER)],
+                        capture_output=True, text=True, env=e, timeout=300)
+    assert pr.returncode == 0, pr.stderr[-2000:]
+    out = dict(l.split(" ", 1) for l in pr.stdout.splitlines() if l[:4] in ("GATE", "BAD "))
+    assert out["GATES"] == gates, out
+    assert out["BAD"] == "[]", out
+
+
 # ---------------------------------------------------------------------------
 # world_size 2 over gloo
 # ---------------------------------------------------------------------------

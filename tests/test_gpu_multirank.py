@@ -393,7 +393,8 @@ def _free_port():
                                                         (7, 1 << 20, None, None), (3, None, None, "0"),
                                                         (4, 65536, None, "0"), (3, None, None, "unfused"),
                                                         (4, None, None, "ts512k"), (6, None, None, None),
-                                                        (3, None, None, "plain_stores")])
+                                                        (3, None, None, "plain_stores"), (4, None, None, "switch0"),
+                                                        (3, None, None, "switch0"), (5, None, None, "switchmax")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -411,6 +412,14 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             env["MSX_TRANSPORT"] = transport
         if rd_flags == "unfused":
             env["MSX_FUSED_PUSH"] = "0"             # flag path with a separate push launch
+        elif rd_flags in ("switch0", "switchmax"):
+            # the reference's flat switch points moved (mpid/env.cpp:514-608): at 0
+            # every allreduce of >= pof2 elements is Rabenseifner (blocks of a few
+            # elements) and every reduce_scatter pairwise; the oracle simulation
+            # in the worker reads the same variables
+            v = "0" if rd_flags == "switch0" else "2147483647"
+            for k in ("ALLREDUCE_SHORT_MSG", "REDUCE_SHORT_MSG", "REDSCAT_COMMUTATIVE_LONG_MSG"):
+                env["MPICH_DEFAULT_" + k] = v
         elif rd_flags == "plain_stores":
             env["MSX_WT_STORES"] = "0"              # two-step pushes / results with plain stores
         elif rd_flags == "ts512k":
