@@ -394,7 +394,9 @@ def _free_port():
                                                         (4, 65536, None, "0"), (3, None, None, "unfused"),
                                                         (4, None, None, "ts512k"), (6, None, None, None),
                                                         (3, None, None, "plain_stores"), (4, None, None, "switch0"),
-                                                        (3, None, None, "switch0"), (5, None, None, "switchmax")])
+                                                        (3, None, None, "switch0"), (5, None, None, "switchmax"),
+                                                        (5, 65536, None, "switch0"), (7, None, None, "switchmax"),
+                                                        (8, None, None, "switch0")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
