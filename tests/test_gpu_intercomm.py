@@ -164,8 +164,8 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("chunk", [None, 1 << 20])
-def test_intercommunicator_reductions_five_ranks(chunk):
+@pytest.mark.parametrize("chunk,switch", [(None, None), (1 << 20, None), (None, "0"), (None, "2147483647")])
+def test_intercommunicator_reductions_five_ranks(chunk, switch):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -178,6 +178,9 @@ def test_intercommunicator_reductions_five_ranks(chunk):
                     "MSX_BOOTSTRAP_TIMEOUT": "180"})
         if chunk:
             env["MSX_CHUNK_BYTES"] = str(chunk)     # transfers across the groups take many chunks
+        if switch is not None:                      # moved flat switch points (the oracle reads them too)
+            for k in ("ALLREDUCE_SHORT_MSG", "REDUCE_SHORT_MSG", "REDSCAT_COMMUTATIVE_LONG_MSG"):
+                env["MPICH_DEFAULT_" + k] = switch
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []

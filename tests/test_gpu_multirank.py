@@ -396,7 +396,7 @@ def _free_port():
                                                         (3, None, None, "plain_stores"), (4, None, None, "switch0"),
                                                         (3, None, None, "switch0"), (5, None, None, "switchmax"),
                                                         (5, 65536, None, "switch0"), (7, None, None, "switchmax"),
-                                                        (8, None, None, "switch0")])
+                                                        (8, None, None, "switch0"), (3, None, None, "staged")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -422,6 +422,10 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             v = "0" if rd_flags == "switch0" else "2147483647"
             for k in ("ALLREDUCE_SHORT_MSG", "REDUCE_SHORT_MSG", "REDSCAT_COMMUTATIVE_LONG_MSG"):
                 env["MPICH_DEFAULT_" + k] = v
+        elif rd_flags == "staged":
+            # host buffers staged through HBM: no call-scoped pinning, no bounce buffers
+            env["MSX_HOST_PIN_MIN"] = str(1 << 40)
+            env["MSX_HOST_BOUNCE_MAX"] = "0"
         elif rd_flags == "plain_stores":
             env["MSX_WT_STORES"] = "0"              # two-step pushes / results with plain stores
         elif rd_flags == "ts512k":
