@@ -132,8 +132,8 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("p", [1, 2, 3])
-def test_user_op_collectives_on_derived_type(p):
+@pytest.mark.parametrize("p,switch", [(1, None), (2, None), (3, None), (3, "0")])
+def test_user_op_collectives_on_derived_type(p, switch):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -144,6 +144,9 @@ def test_user_op_collectives_on_derived_type(p):
         env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
                     "MSX_BOOTSTRAP_TIMEOUT": "180"})
+        if switch is not None:    # moved flat switch points (the oracle in the worker reads them too)
+            for k in ("ALLREDUCE_SHORT_MSG", "REDUCE_SHORT_MSG", "REDSCAT_COMMUTATIVE_LONG_MSG"):
+                env["MPICH_DEFAULT_" + k] = switch
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []

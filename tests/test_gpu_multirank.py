@@ -396,7 +396,8 @@ def _free_port():
                                                         (3, None, None, "plain_stores"), (4, None, None, "switch0"),
                                                         (3, None, None, "switch0"), (5, None, None, "switchmax"),
                                                         (5, 65536, None, "switch0"), (7, None, None, "switchmax"),
-                                                        (8, None, None, "switch0"), (3, None, None, "staged")])
+                                                        (8, None, None, "switch0"), (3, None, None, "staged"),
+                                                        (4, 1 << 20, None, "cached")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -422,6 +423,10 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             v = "0" if rd_flags == "switch0" else "2147483647"
             for k in ("ALLREDUCE_SHORT_MSG", "REDUCE_SHORT_MSG", "REDSCAT_COMMUTATIVE_LONG_MSG"):
                 env["MPICH_DEFAULT_" + k] = v
+        elif rd_flags == "cached":
+            # the documented fallback: cached windows, every engine kernel with
+            # system-scope acquire / release fences
+            env["MSX_WINDOW_CACHED"] = "1"
         elif rd_flags == "staged":
             # host buffers staged through HBM: no call-scoped pinning, no bounce buffers
             env["MSX_HOST_PIN_MIN"] = str(1 << 40)
