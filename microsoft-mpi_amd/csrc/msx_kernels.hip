@@ -723,6 +723,7 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         a.flags.n = t.push_nflags;
         a.flags.seq = t.push_seq;
         for (int i = 0; i < t.push_nflags; ++i) a.flags.dst[i] = t.push_flags[i];
+        if (maxb >= ((size_t)1 << 32)) return hipErrorInvalidValue;   // 32-bit write-through offsets
         size_t gx = (maxb / 16 + 255) / 256;          // as launch_push_post
         if (gx < 1) gx = 1;
         if (gx > 16) gx = 16;
@@ -799,6 +800,7 @@ hipError_t launch_push_post(const void* const* src, void* const* dst, const size
         c.nbytes[i] = nbytes[i];
         if (nbytes[i] > maxb) maxb = nbytes[i];
     }
+    if (maxb >= ((size_t)1 << 32)) return hipErrorInvalidValue;   // 32-bit write-through offsets
     PostFlags f{};
     for (int i = 0; i < nflags; ++i) f.dst[i] = flags[i];
     f.n = nflags;

@@ -104,9 +104,12 @@ __device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlag
     const size_t stride = (size_t)gx * 256;
     size_t done = 0;
     if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        // 16-byte write-through buffer stores (segments stay far below 4 GiB:
+        // at most half an IN sub-slot)
         const size_t nv = nb / 16;
+        const __amdgpu_buffer_rsrc_t r = wt_rsrc(dst);
         for (size_t i = (size_t)bx * 256 + threadIdx.x; i < nv; i += stride)
-            st_wt(reinterpret_cast<u32x4*>(dst) + i, reinterpret_cast<const u32x4*>(src)[i]);
+            st_wt_at(r, 16 * i, reinterpret_cast<const u32x4*>(src)[i]);
         done = nv * 16;
     }
     for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride)
