@@ -181,6 +181,68 @@ def main(out_path, scale):
     log(f"c3 host done {res.get('c3_host_pageable_allreduce_sum_f32', res.get('c3_host_error'))}")
     del hsend, hrecv, hexp
 
+    # ---- c4 / c5 on host memory (the host variant of every GPU
+    # config), at bounded sizes: a 512 MiB send buffer per rank for the
+    # reduce_scatter MAX fp64, a 256 MiB uint64 vector for the Iallreduce BAND
+    per_h = int((64 << 20) * scale) // p
+    tot_h = per_h * p
+    jh = np.arange(tot_h, dtype=np.int64)
+    hs4 = ((jh * 2654435761 + rank * 40503) % 1000003).astype(np.float64)
+    blk = jh[rank * per_h:(rank + 1) * per_h]
+    he4 = np.full(per_h, -1.0)
+    for r in range(p):
+        he4 = np.maximum(he4, ((blk * 2654435761 + r * 40503) % 1000003).astype(np.float64))
+    del jh, blk
+    hr4 = np.empty(per_h, np.float64)
+    hcounts = (ctypes.c_int * p)(*([per_h] * p))
+    ts = []
+    for it in range(3):
+        barrier()
+        t0 = time.perf_counter()
+        rc = L.MPI_Reduce_scatter(hs4.ctypes.data, hr4.ctypes.data, hcounts, C.MPI_DOUBLE, C.MPI_MAX,
+                                  C.MPI_COMM_WORLD)
+        ts.append(time.perf_counter() - t0)
+        if rc:
+            res["c4_host_error"] = f"rc={rc} {msx.last_error()}"
+            break
+    if "c4_host_error" not in res:
+        t = sorted(ts[1:])[len(ts[1:]) // 2]
+        res["c4_host_pageable_reduce_scatter_max_f64"] = {
+            "bytes_per_rank": tot_h * 8, "seconds": round(t, 5),
+            "busbw_GB_s": round(tot_h * 8 / t / 1e9 * (p - 1) / p, 2),
+            "correct": bool(np.array_equal(hr4, he4))}
+    log(f"c4 host done {res.get('c4_host_pageable_reduce_scatter_max_f64', res.get('c4_host_error'))}")
+    del hs4, hr4, he4
+    n5 = int((32 << 20) * scale)
+    k5 = np.arange(n5, dtype=np.uint64)
+    bit = lambda r: np.left_shift(np.uint64(1), (k5 * np.uint64(7) + np.uint64(13 * r)) % np.uint64(64))
+    hs5 = ~bit(rank)                                     # every rank clears one bit per element
+    he5 = np.full(n5, np.uint64(0xFFFFFFFFFFFFFFFF))
+    for r in range(p):
+        he5 &= ~bit(r)
+    del k5
+    hr5 = np.empty_like(hs5)
+    ts = []
+    for it in range(3):
+        barrier()
+        req = ctypes.c_int()
+        t0 = time.perf_counter()
+        rc = L.MPI_Iallreduce(hs5.ctypes.data, hr5.ctypes.data, n5, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD,
+                              ctypes.byref(req))
+        rc = rc or L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1))
+        ts.append(time.perf_counter() - t0)
+        if rc:
+            res["c5_host_error"] = f"rc={rc} {msx.last_error()}"
+            break
+    if "c5_host_error" not in res:
+        t = sorted(ts[1:])[len(ts[1:]) // 2]
+        res["c5_host_pageable_iallreduce_band_u64"] = {
+            "bytes_per_rank": n5 * 8, "seconds": round(t, 5),
+            "busbw_GB_s": round(n5 * 8 / t / 1e9 * 2 * (p - 1) / p, 2),
+            "correct": bool(np.array_equal(hr5, he5))}
+    log(f"c5 host done {res.get('c5_host_pageable_iallreduce_band_u64', res.get('c5_host_error'))}")
+    del hs5, hr5, he5
+
     # ---- c4: reduce_scatter MAX fp64, 4 GiB per rank sendbuf ----------------
     per = int((512 << 20) * scale) // p                  # recvcount per rank (c4: 2^29 / p)
     tot = per * p
