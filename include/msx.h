@@ -129,6 +129,14 @@ int msx_schedule_tree(int which, int p, int n, int* src32, int* P, unsigned* pai
 /* which = 0 allreduce, 1 reduce_scatter, 2 reduce: 0 recursive doubling,
  * 1 Rabenseifner, 2 recursive halving, 3 pairwise, 4 binomial */
 int msx_schedule_algo(int which, int p, int64_t count, int type_size);
+/* the same with the gate size taken from `dt`: MPI_Type_size (blocking calls,
+ * reduce_scatter) or the extent (nbc = 1: the NBC task lists of
+ * MPI_Iallreduce / MPI_Ireduce, reduce.cpp:4717,4881,6701,6740) */
+int msx_schedule_algo_dt(int which, int p, int64_t count, MPI_Datatype dt, int nbc);
+/* MPI_Ireduce's Rabenseifner tree of newrank n over root-relative ranks
+ * (IreduceBuildScatterGatherTaskList, reduce.cpp:6267-6670) */
+int msx_schedule_ireduce_tree(int p, int n, int root, int* src32, int* P, unsigned* pairmask,
+                              int* chain);
 int msx_schedule_newrank(int rank, int p);
 int msx_schedule_block(int p, int64_t count, int n, int64_t* start, int64_t* len);
 

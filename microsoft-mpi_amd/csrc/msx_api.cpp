@@ -769,11 +769,12 @@ int v_reduce(Comm* c, const void* sendbuf, void* recvbuf, int count, MPI_Datatyp
     return rc;
 }
 
-int run_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t n, MPI_Datatype datatype, const OpRef& r, int root)
+int run_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t n, MPI_Datatype datatype, const OpRef& r, int root,
+               bool nbc)
 {
     if (n == 0) return MPI_SUCCESS;
     return c->inter ? engine_inter_reduce(c, sendbuf, recvbuf, n, datatype, r, root)
-                    : coll_reduce(c, sendbuf, recvbuf, n, datatype, r, root);
+                    : coll_reduce(c, sendbuf, recvbuf, n, datatype, r, root, nbc);
 }
 
 int run_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* counts, MPI_Datatype datatype,
@@ -797,7 +798,7 @@ MSX_EXPORT int MPI_Allreduce(const void* sendbuf, void* recvbuf, int count, MPI_
     if (rc == MPI_SUCCESS && count > 0) rc = v_allreduce_bufs(c, sendbuf, recvbuf, count, datatype);
     if (rc == MPI_SUCCESS && count > 0)
         rc = c->inter ? engine_inter_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r)
-                      : coll_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r);
+                      : coll_allreduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, force_async());
     return err_return(c, "MPI_Allreduce", rc);
 }
 
@@ -810,7 +811,7 @@ MSX_EXPORT int MPI_Reduce(const void* sendbuf, void* recvbuf, int count, MPI_Dat
     bool skip = false;
     int rc = v_comm(comm, &c);
     if (rc == MPI_SUCCESS) rc = v_reduce(c, sendbuf, recvbuf, count, datatype, op, root, &r, &skip);
-    if (rc == MPI_SUCCESS && !skip) rc = run_reduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, root);
+    if (rc == MPI_SUCCESS && !skip) rc = run_reduce(c, sendbuf, recvbuf, (size_t)count, datatype, r, root, force_async());
     return err_return(c, "MPI_Reduce", rc);
 }
 
@@ -973,7 +974,7 @@ MSX_EXPORT int MPI_Ireduce(const void* sendbuf, void* recvbuf, int count, MPI_Da
     if (rc == MPI_SUCCESS) rc = v_reduce(c, sendbuf, recvbuf, count, datatype, op, root, &r, &skip);
     if (rc == MPI_SUCCESS) {
         const size_t n = skip ? 0 : (size_t)count;
-        rc = request_start_generic(c, [=] { return run_reduce(c, sendbuf, recvbuf, n, datatype, r, root); },
+        rc = request_start_generic(c, [=] { return run_reduce(c, sendbuf, recvbuf, n, datatype, r, root, true); },
                                    request, datatype);
     }
     return err_return(c, "MPI_Ireduce", rc);
@@ -2421,6 +2422,30 @@ MSX_EXPORT int msx_schedule_algo(int which, int p, int64_t count, int type_size)
     if (which == 0) return allreduce_algo(p, (size_t)count, type_size, true);
     if (which == 2) return reduce_algo(p, (size_t)count, type_size, true);
     return reduce_scatter_algo(p, (size_t)count, type_size, true);
+}
+
+// The same, with the gate's bytes per element taken from the datatype as the
+// reference does: MPI_Type_size for the blocking calls and every reduce_scatter,
+// the extent for the NBC task lists of MPI_Iallreduce / MPI_Ireduce (nbc = 1).
+MSX_EXPORT int msx_schedule_algo_dt(int which, int p, int64_t count, MPI_Datatype dt, int nbc)
+{
+    if (!dtype_lookup(dt)) return -1;
+    const int gate = gate_type_size(dt, which != 1 && nbc != 0);
+    return msx_schedule_algo(which, p, count, gate);
+}
+
+// MPI_Ireduce's Rabenseifner tree of newrank n for `root` (root-relative ranks,
+// reduce.cpp:6267-6670); same reporting as msx_schedule_tree
+MSX_EXPORT int msx_schedule_ireduce_tree(int p, int n, int root, int* src32, int* P, unsigned* pairmask,
+                                         int* chain)
+{
+    if (p < 1 || p > 16 || root < 0 || root >= p || !src32 || !P || !pairmask || !chain) return MPI_ERR_ARG;
+    const RankTree t = tree_ireduce_rsag(p, n, root);
+    for (int i = 0; i < 32; ++i) src32[i] = t.src[i];
+    *P = t.P;
+    *pairmask = t.pairmask;
+    *chain = 0;
+    return MPI_SUCCESS;
 }
 
 // newrank of `rank`, and the allreduce block owned by newrank n

@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <strings.h>
 #include <vector>
 
 #include "msx_runtime.h"
@@ -238,23 +239,36 @@ int coll_barrier(Comm* c)
 }
 
 int coll_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                   const OpRef& op)
+                   const OpRef& op, bool nbc)
 {
     if (c->size == 1) {
         if (sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
         return local_copy(sendbuf, recvbuf, count, dt);
     }
-    return engine_allreduce(c, sendbuf, recvbuf, count, dt, op);
+    return engine_allreduce(c, sendbuf, recvbuf, count, dt, op, nbc);
 }
 
 int coll_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                const OpRef& op, int root)
+                const OpRef& op, int root, bool nbc)
 {
     if (c->size == 1) {
         if (sendbuf == MPI_IN_PLACE) return MPI_SUCCESS;
         return local_copy(sendbuf, recvbuf, count, dt);
     }
-    return engine_reduce(c, sendbuf, recvbuf, count, dt, op, root);
+    return engine_reduce(c, sendbuf, recvbuf, count, dt, op, root, nbc);
+}
+
+bool force_async()
+{
+    // env_is_on (common/mpiutil.cpp:9-61): a 5-wchar buffer, so values of
+    // five or more characters read as unset (the default, off)
+    static const bool on = [] {
+        const char* v = getenv("MSMPI_FORCE_ASYNC_WORKFLOW");
+        if (!v || strlen(v) > 4) return false;
+        if (strcmp(v, "1") == 0) return true;
+        return strcasecmp(v, "on") == 0 || strcasecmp(v, "yes") == 0 || strcasecmp(v, "true") == 0;
+    }();
+    return on;
 }
 
 int coll_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
@@ -385,7 +399,7 @@ int request_start_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t 
                             MPI_Datatype dt, const OpRef& op, MPI_Request* req)
 {
     return request_start_generic(
-        c, [=] { return count ? coll_allreduce(c, sendbuf, recvbuf, count, dt, op) : MPI_SUCCESS; },
+        c, [=] { return count ? coll_allreduce(c, sendbuf, recvbuf, count, dt, op, true) : MPI_SUCCESS; },
         req, dt);
 }
 

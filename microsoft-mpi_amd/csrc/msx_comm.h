@@ -52,6 +52,12 @@ struct OpRef {
     bool commutative = true;
 };
 
+// MSMPI_FORCE_ASYNC_WORKFLOW (mpid/env.cpp:1381-1384, read at MPI_Init with
+// env_is_on: "1", or "on" / "yes" / "true" in any case, at most 4
+// characters): blocking MPI_Reduce / MPI_Allreduce / MPI_Reduce_scatter[_block]
+// run the NBC builders and wait (api/mpi_reduce.cpp:129,508,903,1317).
+bool force_async();
+
 // Process state (init/finalize, world bootstrap).
 bool is_initialized();
 bool is_finalized();
@@ -61,10 +67,12 @@ Comm* world();
 
 // Reduction collectives over `comm` (arguments already validated).
 // `kind` is the element class of `dt` (K_NONE for user ops on non-reducible types).
+// nbc: follow the reference's NBC task list (MPI_Iallreduce / MPI_Ireduce,
+// or the blocking call under MSMPI_FORCE_ASYNC_WORKFLOW, force_async()).
 int coll_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                   const OpRef& op);
+                   const OpRef& op, bool nbc = false);
 int coll_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                const OpRef& op, int root);
+                const OpRef& op, int root, bool nbc = false);
 int coll_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
                         MPI_Datatype dt, const OpRef& op);
 int coll_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,

@@ -720,6 +720,15 @@ int reduce_algo(int p, size_t count, int type_size, bool builtin)
                                                                                                 : A_BINOMIAL;
 }
 
+int gate_type_size(MPI_Datatype dt, bool nbc)
+{
+    if (dtype_is_derived(dt)) {            // user ops only; the builtin gates never see one
+        const Dtype* t = dtype_lookup(dt);
+        return t ? (int)(nbc ? t->extent : t->size) : 0;
+    }
+    return nbc ? type_size(dt) : (int)dtype_size(dt);
+}
+
 RankTree tree_reduce_rsag(int p, int n)
 {
     // MPI_Reduce folds the ODD rank into the even one below it (reduce.cpp:
@@ -738,6 +747,18 @@ RankTree tree_reduce_rsag(int p, int n)
             t.src[2 * k] = m + rem;
         }
     }
+    return t;
+}
+
+RankTree tree_ireduce_rsag(int p, int n, int root)
+{
+    // IreduceBuildScatterGatherTaskList (reduce.cpp:6267-6670) runs the same
+    // fold and recursive halving over ranks RELATIVE TO THE ROOT: peer =
+    // RankAdd(TrimmedToOriginalRankEven(rem, s ^ offset), root) (:6471), the
+    // even relative rank combining Uop(tmp = x_{rel+1}, recvbuf) (:6403-6411).
+    RankTree t = tree_reduce_rsag(p, n);
+    for (int i = 0; i < 32; ++i)
+        if (t.src[i] >= 0) t.src[i] = (t.src[i] + root) % p;
     return t;
 }
 
@@ -1506,7 +1527,7 @@ struct P2p {
 };
 
 int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf, size_t count,
-                   MPI_Datatype dt, const OpRef& op, int root)
+                   MPI_Datatype dt, const OpRef& op, int root, bool nbc)
 {
     Transport* tp = c->tp;
     const int p = c->size, me = c->rank;
@@ -1518,8 +1539,8 @@ int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf,
     char* dst = static_cast<char*>(recvbuf);
     const bool want = (root < 0 || root == me);
     const bool is_reduce = root >= 0;
-    const int algo = is_reduce ? reduce_algo(p, count, (int)esz, true)
-                               : allreduce_algo(p, count, (int)esz, true);
+    const int gate = gate_type_size(dt, nbc);
+    const int algo = is_reduce ? reduce_algo(p, count, gate, true) : allreduce_algo(p, count, gate, true);
     const BufInfo bs = classify(src), bd = classify(dst);
     size_t qmax = (chunk_bytes() / (size_t)p) / esz;
     qmax -= qmax % 16;
@@ -1586,7 +1607,8 @@ int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf,
             allreduce_block(p, count, j, &bst, &bl);
             const size_t e1 = std::min(phi, bst + bl - o);
             const int owner = allreduce_block_owner(p, j);
-            const RankTree t = is_reduce ? tree_reduce_rsag(p, owner) : tree_allreduce(p, owner);
+            const RankTree t = !is_reduce ? tree_allreduce(p, owner)
+                                          : (nbc ? tree_ireduce_rsag(p, owner, root) : tree_reduce_rsag(p, owner));
             rc = run_rank_tree(op.opidx, k, t, srcs, esz, e0 - plo, e1 - e0, outp + e0 * esz, s);
             e0 = e1;
         }
@@ -1621,7 +1643,7 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
     hipStream_t s = tp->stream();
     size_t qe = (chunk_bytes() / (size_t)p) / esz;
     qe -= qe % 16;
-    const int algo = reduce_scatter_algo(p, total, (int)esz, op.commutative);
+    const int algo = reduce_scatter_algo(p, total, gate_type_size(dt, false), op.commutative);
     const int n = newrank_of(me, p);
     const RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
                                                : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
@@ -1671,7 +1693,7 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
 
 // root < 0: allreduce; root >= 0: only `root` receives the result (MPI_Reduce).
 int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                 const OpRef& op, int root = -1)
+                 const OpRef& op, int root = -1, bool nbc = false)
 {
     // user functions are host code: no GPU needed on this path
     if (op.opidx == O_NULL) return host_user_allreduce(c, sendbuf, recvbuf, count, dt, op);
@@ -1680,7 +1702,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
 
     Transport* tp = c->tp;
     if (rccl_requested())
-        if (ncclComm_t rcomm = rccl_comm(tp)) return rccl_allreduce(rcomm, c, sendbuf, recvbuf, count, dt, op, root);
+        if (ncclComm_t rcomm = rccl_comm(tp)) return rccl_allreduce(rcomm, c, sendbuf, recvbuf, count, dt, op, root, nbc);
     const int p = c->size, me = c->rank;
     const TypeInfo* ti = type_info(dt);
     const Kind k = ti->kind;
@@ -1690,8 +1712,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     char* dst = static_cast<char*>(recvbuf);
     const bool want = (root < 0 || root == me);          // this rank receives the result
     const bool is_reduce = root >= 0;
-    const int algo = is_reduce ? reduce_algo(p, count, (int)esz, true)
-                               : allreduce_algo(p, count, (int)esz, true);
+    const int gate = gate_type_size(dt, nbc);
+    const int algo = is_reduce ? reduce_algo(p, count, gate, true) : allreduce_algo(p, count, gate, true);
     // A recursive-doubling (or binomial) call that fits half a sub-slot runs
     // barrier-free at its end: it uses the IN half `rd_parity`, alternating per
     // call.  Pushing into a peer's half P again (two calls later) happens only
@@ -1970,7 +1992,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         }
         for (size_t i = 0; i < ranges.size() && rc == MPI_SUCCESS; ++i) {
             const Range& g = ranges[i];
-            const RankTree t = is_reduce ? tree_reduce_rsag(p, g.owner) : tree_allreduce(p, g.owner);
+            const RankTree t = !is_reduce ? tree_allreduce(p, g.owner)
+                                          : (nbc ? tree_ireduce_rsag(p, g.owner, root) : tree_reduce_rsag(p, g.owner));
             std::vector<char*> extra;
             for (size_t d = 1; d < dests.size(); ++d) extra.push_back(w.out(dests[d]) + obase + g.e0 * esz);
             TreeWait tw;
@@ -2045,7 +2068,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             allreduce_block(p, count, j, &bst, &bl);
             const size_t e1 = std::min(phi, bst + bl - o);
             const int owner = allreduce_block_owner(p, j);
-            const RankTree t = is_reduce ? tree_reduce_rsag(p, owner) : tree_allreduce(p, owner);
+            const RankTree t = !is_reduce ? tree_allreduce(p, owner)
+                                          : (nbc ? tree_ireduce_rsag(p, owner, root) : tree_reduce_rsag(p, owner));
             std::vector<char*> extra;
             for (size_t d = 1; d < dests.size(); ++d) extra.push_back(w.out(dests[d]) + e0 * esz);
             rc = run_rank_tree(op.opidx, k, t, subs, esz, e0 - plo, e1 - e0, w.out(dests[0]) + e0 * esz, s, extra);
@@ -2104,8 +2128,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
             // function, reduce.cpp:917-1334
             std::vector<char> all((size_t)p * mf.bytes);
             if ((rc = c->tp->allgather(full.data(), mf.bytes, all.data())) != MPI_SUCCESS) return rc;
-            const int gate_esz = mf.t ? (int)mf.t->size : (int)esz;
-            const int algo = reduce_scatter_algo(p, total, gate_esz, true);
+            const int algo = reduce_scatter_algo(p, total, gate_type_size(dt, false), true);
             const int n = newrank_of(me, p);
             const RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
                                                        : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
@@ -2147,7 +2170,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
     size_t qe = w.Q / esz;
     qe -= qe % 16;
     if (qe == 0) { set_error("reduce_scatter: window too small"); return MPI_ERR_INTERN; }
-    const int algo = reduce_scatter_algo(p, total, (int)esz, op.commutative);
+    const int algo = reduce_scatter_algo(p, total, gate_type_size(dt, false), op.commutative);
     const int n = newrank_of(me, p);
     const RankTree t = (algo == A_RS_PAIRWISE) ? tree_pairwise(p, me)
                                                : tree_reduce_scatter(p, n >= 0 ? n : newrank_of(me + 1, p));
@@ -2268,9 +2291,9 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
 
 // ---- public engine entry points --------------------------------------------
 int engine_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                     const OpRef& op)
+                     const OpRef& op, bool nbc)
 {
-    return worker().run([=] { return do_allreduce(c, sendbuf, recvbuf, count, dt, op); });
+    return worker().run([=] { return do_allreduce(c, sendbuf, recvbuf, count, dt, op, -1, nbc); });
 }
 
 int engine_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
@@ -2321,13 +2344,13 @@ int host_user_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, 
 }  // namespace
 
 int engine_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                  const OpRef& op, int root)
+                  const OpRef& op, int root, bool nbc)
 {
     // Builtin ops: the reference's binomial / Rabenseifner trees (do_allreduce
     // in reduce mode); user ops: host_user_reduce.
     return worker().run([=]() -> int {
         if (op.opidx == O_NULL) return host_user_reduce(c, sendbuf, recvbuf, count, dt, op, root);
-        return do_allreduce(c, sendbuf, recvbuf, count, dt, op, root);
+        return do_allreduce(c, sendbuf, recvbuf, count, dt, op, root, nbc);
     });
 }
 

@@ -130,14 +130,25 @@ RankTree tree_reduce_scatter(int p, int n);
 RankTree tree_pairwise(int p, int r);
 //   reduce, Rabenseifner: leaves y_k = leafR(n ^ k), leafR = even-first fold
 RankTree tree_reduce_rsag(int p, int n);
+//   MPI_Ireduce, Rabenseifner: tree_reduce_rsag over root-relative ranks
+RankTree tree_ireduce_rsag(int p, int n, int root);
 //   reduce, binomial:     leaves x_{(k + root) % p}, k < p, of a nextpow2(p) tree
 RankTree tree_reduce_binomial(int p, int root);
+// Bytes per element the algorithm gates multiply the count by: the blocking
+// calls use MPI_Type_size (reduce.cpp:151, :1705, :3821), the NBC task lists
+// of MPI_Iallreduce / MPI_Ireduce the extent (:4712-4717, :6695-6701; 16 vs
+// 12 for MPI_DOUBLE_INT, 8 vs 6 for MPI_SHORT_INT); MPI_Ireduce_scatter uses
+// the size again (:3201).
+int gate_type_size(MPI_Datatype dt, bool nbc);
 
 // ---- engine entry points (msx_comm.cpp routes size > 1 here) ---------------
+// nbc: the schedule of the reference's NBC task list (MPI_Iallreduce /
+// MPI_Ireduce, or a blocking call under MSMPI_FORCE_ASYNC_WORKFLOW): the
+// extent gate and, for MPI_Ireduce's Rabenseifner, root-relative ranks.
 int engine_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                     const OpRef& op);
+                     const OpRef& op, bool nbc = false);
 int engine_reduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
-                  const OpRef& op, int root);
+                  const OpRef& op, int root, bool nbc = false);
 int engine_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* recvcounts,
                           MPI_Datatype dt, const OpRef& op);
 int engine_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,

@@ -47,6 +47,12 @@ def lib():
     L.oracle_reduce.argtypes = [i, i, i, i, i64, ctypes.POINTER(p), p]
     L.oracle_scan.restype = i
     L.oracle_scan.argtypes = [i, i, i, i64, i, ctypes.POINTER(p), ctypes.POINTER(p)]
+    L.oracle_type_size.restype = i
+    L.oracle_type_size.argtypes = [i]
+    L.oracle_iallreduce.restype = i
+    L.oracle_iallreduce.argtypes = [i, i, i, i64, ctypes.POINTER(p), ctypes.POINTER(p)]
+    L.oracle_ireduce.restype = i
+    L.oracle_ireduce.argtypes = [i, i, i, i, i64, ctypes.POINTER(p), p]
     L.oracle_reduce_scatter.restype = i
     L.oracle_reduce_scatter.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(p), ctypes.POINTER(p)]
     _lib = L
@@ -78,6 +84,27 @@ def allreduce(op, dt, sendbufs, recvbufs):
     S = (ctypes.c_void_p * p)(*[_addr(b) for b in sendbufs])
     R = (ctypes.c_void_p * p)(*[_addr(b) for b in recvbufs])
     return lib().oracle_allreduce(op, dt, p, sendbufs[0].size, S, R)
+
+
+def type_size(dt):
+    """MPI_Type_size of a reducible predefined type (12 for MPI_DOUBLE_INT)."""
+    return lib().oracle_type_size(dt)
+
+
+def iallreduce(op, dt, sendbufs, recvbufs):
+    """MPI_Iallreduce's NBC task list (extent gate, reduce.cpp:4699-4982)."""
+    p = len(sendbufs)
+    S = (ctypes.c_void_p * p)(*[_addr(b) for b in sendbufs])
+    R = (ctypes.c_void_p * p)(*[_addr(b) for b in recvbufs])
+    return lib().oracle_iallreduce(op, dt, p, sendbufs[0].size, S, R)
+
+
+def ireduce(op, dt, root, sendbufs, recvbuf):
+    """MPI_Ireduce's NBC task list (extent gate, root-relative Rabenseifner,
+    reduce.cpp:6005-6768)."""
+    p = len(sendbufs)
+    S = (ctypes.c_void_p * p)(*[_addr(b) for b in sendbufs])
+    return lib().oracle_ireduce(op, dt, p, root, sendbufs[0].size, S, _addr(recvbuf))
 
 
 def reduce_scatter(op, dt, recvcounts, sendbufs, recvbufs):

@@ -100,6 +100,20 @@ int oracle_kind_size(int kind)
     }
 }
 
+/* MPI_Type_size of a reducible predefined type.  The pair types are built by
+ * SetTypeCharacteristics<T1,T2> (mpid/datatype.cpp:1282-1293): size =
+ * sizeof(T1) + sizeof(T2), extent = sizeof(struct {T1 a; T2 b;}).  So
+ * DOUBLE_INT / LONG_DOUBLE_INT carry 12 data bytes in a 16-byte extent and
+ * SHORT_INT 6 in 8; every other type has size == extent == oracle_kind_size. */
+int oracle_type_size(MPI_Datatype dt)
+{
+    switch (oracle_kind_of(dt)) {
+    case ORK_LOC_SI: return (int)(sizeof(int16_t) + sizeof(int32_t));
+    case ORK_LOC_DI: return (int)(sizeof(double) + sizeof(int32_t));
+    default: return oracle_kind_size(oracle_kind_of(dt));
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* legality (op.cpp:739-1883, USE_STRICT_MPI undefined)                      */
 /* ------------------------------------------------------------------------ */

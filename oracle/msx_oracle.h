@@ -34,8 +34,12 @@ enum oracle_kind {
 
 /* datatype handle -> element class (ORK_NONE if not reducible) */
 int oracle_kind_of(MPI_Datatype dt);
-/* bytes per element of a kind (sizeof the C struct, padding included) */
+/* bytes per element of a kind (sizeof the C struct, padding included): the
+ * datatype's EXTENT */
 int oracle_kind_size(int kind);
+/* MPI_Type_size (data bytes; 12 for MPI_DOUBLE_INT, 6 for MPI_SHORT_INT,
+ * datatype.cpp:1282-1293) */
+int oracle_type_size(MPI_Datatype dt);
 /* MPIR_Op_<op>_check_dtype (op.cpp:739-1883): MPI_SUCCESS or MPI_ERR_OP */
 int oracle_op_check(MPI_Op op, MPI_Datatype dt);
 /* MPIR_Op_<op>(in, inout, &len, &dt) (op.cpp:703-1795) with a 64-bit count.
@@ -60,6 +64,25 @@ int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
                   const void* const* sendbufs, void* recvbuf_root);
 int oracle_scan(MPI_Op op, MPI_Datatype dt, int p, int64_t count, int exclusive,
                 const void* const* sendbufs, void* const* recvbufs);
+/* The non-blocking forms as the reference builds their NBC task lists (also
+ * what MSMPI_FORCE_ASYNC_WORKFLOW runs for the blocking calls):
+ *  - MPI_Iallreduce, IallreduceBuildTaskList (reduce.cpp:4699-4982): the
+ *    blocking butterfly, but the Rabenseifner gate reads the EXTENT,
+ *    (unsigned)(extent*count) > short_msg (:4717, :4791, :4881), where the
+ *    blocking call reads MPI_Type_size (:3884);
+ *  - MPI_Ireduce, IreduceBuildTaskList (:6676-6768): the same extent gate
+ *    (:6740), and IreduceBuildScatterGatherTaskList (:6267-6670) runs the
+ *    recursive halving over ranks RELATIVE TO THE ROOT (odd relative ranks
+ *    fold into relativeRank-1, TrimmedToOriginalRankEven, peers at
+ *    root + relative rank), where the blocking Rabenseifner uses absolute
+ *    ranks (:174-300).  The binomial task list (:6005-6198) equals the
+ *    blocking binomial tree.
+ *  - MPI_Ireduce_scatter[_block] (:3176-3257) gate on MPI_Type_size like the
+ *    blocking call and build the same trees, so oracle_reduce_scatter serves. */
+int oracle_iallreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
+                      const void* const* sendbufs, void* const* recvbufs);
+int oracle_ireduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
+                   const void* const* sendbufs, void* recvbuf_root);
 
 #ifdef __cplusplus
 }

@@ -47,8 +47,11 @@ static int combine(MPI_Op op, MPI_Datatype dt, const void* in, void* inout, int6
     return n > 0 ? oracle_reduce_local(op, dt, in, inout, n) : 0;
 }
 
-int oracle_allreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
-                     const void* const* sendbufs, void* const* recvbufs)
+/* gate_size: bytes per element the algorithm gate multiplies count by --
+ * MPI_Type_size for the blocking call (reduce.cpp:3821,3884), the extent for
+ * the NBC task list (:4712-4717,4881). */
+static int allreduce_sim(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
+                         const void* const* sendbufs, void* const* recvbufs, int64_t gate_size)
 {
     if (oracle_op_check(op, dt) != MPI_SUCCESS) return MPI_ERR_OP;
     if (p < 1) return MPI_ERR_ARG;
@@ -84,7 +87,7 @@ int oracle_allreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
     int* real = (int*)calloc((size_t)pof2, sizeof(int));
     for (int r = 0; r < p; ++r) if (newrank[r] >= 0) real[newrank[r]] = r;
 
-    const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)esz);   /* :3884 */
+    const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)gate_size);   /* :3884 / :4881 */
     if (nbytes <= switch_point("MPICH_DEFAULT_ALLREDUCE_SHORT_MSG", 262144) || count < pof2) {
         /* recursive doubling (:3890-3926): commutative builtin -> Uop(tmp, recvbuf) */
         for (int mask = 1; mask < pof2; mask <<= 1) {
@@ -174,6 +177,24 @@ int oracle_allreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
     return rc ? MPI_ERR_OP : MPI_SUCCESS;
 }
 
+int oracle_allreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
+                     const void* const* sendbufs, void* const* recvbufs)
+{
+    return allreduce_sim(op, dt, p, count, sendbufs, recvbufs, oracle_type_size(dt));
+}
+
+/* IallreduceBuildTaskList (reduce.cpp:4699-4982): fold, recursive doubling
+ * (IallreduceBuildRecursiveDoublingTaskList :4601-4693) or reduce-scatter +
+ * allgather (IallreduceBuildReduceScatterAllGatherTaskList :4346-4595) with
+ * the blocking call's peers, index arithmetic and -- builtin ops being
+ * commutative -- NbcTask::ExecuteReduce's Uop(recv, reduce) roles
+ * (tasks.cpp:680-686); only the gate differs: fullExtent = extent * count. */
+int oracle_iallreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
+                      const void* const* sendbufs, void* const* recvbufs)
+{
+    return allreduce_sim(op, dt, p, count, sendbufs, recvbufs, oracle_kind_size(oracle_kind_of(dt)));
+}
+
 int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcounts,
                           const void* const* sendbufs, void* const* recvbufs)
 {
@@ -185,7 +206,9 @@ int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcoun
     int rc = MPI_SUCCESS;
     if (total == 0) { free(disps); return MPI_SUCCESS; }
     const int64_t bytes = total * esz;
-    const uint32_t nbytes = (uint32_t)((uint64_t)total * (uint64_t)esz);   /* :1705 */
+    /* :1705 nbytes = (unsigned)(total_count * type_size); the NBC builder
+     * gates on the same product, cbBuffer (:3201) */
+    const uint32_t nbytes = (uint32_t)((uint64_t)total * (uint64_t)oracle_type_size(dt));
     char** res = (char**)calloc((size_t)p, sizeof(char*));
     char** tmp = (char**)calloc((size_t)p, sizeof(char*));
     char** snap = (char**)calloc((size_t)p, sizeof(char*));
@@ -291,8 +314,8 @@ int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcoun
  * that only moves data (:330-450): root's block j is the value its owner
  * computed.  Binomial (otherwise, :489-537): relative ranks to root, node
  * relrank receives from relrank|mask and combines Uop(tmp=received, recvbuf). */
-int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
-                  const void* const* sendbufs, void* recvbuf_root)
+static int reduce_sim(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
+                      const void* const* sendbufs, void* recvbuf_root, int64_t gate_size, int relative)
 {
     if (oracle_op_check(op, dt) != MPI_SUCCESS) return MPI_ERR_OP;
     if (p < 1 || root < 0 || root >= p) return MPI_ERR_ARG;
@@ -310,20 +333,27 @@ int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
         memcpy(rb[r], sendbufs[r], (size_t)bytes);
     }
     const int pof2 = pof2_floor(p), rem = p - pof2;
-    const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)esz);   /* :151 */
+    const uint32_t nbytes = (uint32_t)((uint64_t)count * (uint64_t)gate_size);   /* :151 / :6740 */
+    /* absolute rank of (relative) rank q: the blocking call works on absolute
+     * ranks, the NBC scatter-gather on ranks relative to the root (:6309,
+     * :6471 RankAdd(TrimmedToOriginalRankEven(rem, peer), root)) */
+    const int base = relative ? root : 0;
+#define ABS_RANK(q) (((q) + base) % p)
     if (nbytes > switch_point("MPICH_DEFAULT_REDUCE_SHORT_MSG", 65536) && count >= pof2) {
         int* real = (int*)calloc((size_t)pof2, sizeof(int));
-        for (int r = 0; r < p; ++r) {
-            if (r < 2 * rem) {
-                if ((r & 1) == 0) {                 /* even: receive from r+1 and combine */
-                    memcpy(tmp[r], rb[r + 1], (size_t)bytes);
+        for (int q = 0; q < p; ++q) {
+            const int r = ABS_RANK(q);
+            if (q < 2 * rem) {
+                if ((q & 1) == 0) {                 /* even: receive from q+1 and combine (:190-203, :6386-6420) */
+                    memcpy(tmp[r], rb[ABS_RANK(q + 1)], (size_t)bytes);
                     rc |= combine(op, dt, tmp[r], rb[r], count);
-                    real[r / 2] = r;
+                    real[q / 2] = r;
                 }
             } else {
-                real[r - rem] = r;
+                real[q - rem] = r;
             }
         }
+#undef ABS_RANK
         const int64_t reduceSize = count / pof2, endSize = count % pof2;
         int *send_idx = calloc((size_t)pof2, sizeof(int)), *recv_idx = calloc((size_t)pof2, sizeof(int));
         int *last_idx = calloc((size_t)pof2, sizeof(int)), *idx_shift = calloc((size_t)pof2, sizeof(int));
@@ -390,6 +420,26 @@ int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
     for (int r = 0; r < p; ++r) { free(rb[r]); free(tmp[r]); free(snap[r]); }
     free(rb); free(tmp); free(snap);
     return rc ? MPI_ERR_OP : MPI_SUCCESS;
+}
+
+int oracle_reduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
+                  const void* const* sendbufs, void* recvbuf_root)
+{
+    return reduce_sim(op, dt, p, root, count, sendbufs, recvbuf_root, oracle_type_size(dt), 0);
+}
+
+/* IreduceBuildTaskList (reduce.cpp:6676-6768): extent gate (:6701, :6740);
+ * IreduceBuildScatterGatherTaskList over root-relative ranks, the even
+ * relative rank combining Uop(tmp = x_{rel+1}, recvbuf) (:6403-6411,
+ * rightOrder false, commutative builtin -> tasks.cpp:680-686), recursive
+ * halving with ascending offsets keeping the lower half (:6461-6559), gather
+ * by translated rank (:6570-6664: scatter rank s holds chunk bitrev(s));
+ * IreduceBuildBinomialTaskList (:6005-6198): children rank+1, +2, +4 ...
+ * combined in that order, Uop(tmp, recvbuf) -- the blocking binomial tree. */
+int oracle_ireduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
+                   const void* const* sendbufs, void* recvbuf_root)
+{
+    return reduce_sim(op, dt, p, root, count, sendbufs, recvbuf_root, oracle_kind_size(oracle_kind_of(dt)), 1);
 }
 
 /* MPI_Scan / MPI_Exscan as the reference runs them: the NBC task lists of

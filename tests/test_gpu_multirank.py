@@ -222,7 +222,7 @@ else: check("host scan pinned", hs, es[rank])
 cnt = 30001
 xr = inputs("MPI_SUM", "MPI_FLOAT", cnt, 6000)
 er = raw(np.zeros_like(xr[0]))
-assert oracle.reduce(C.MPI_SUM, C.MPI_FLOAT, p - 1, xr, er) == 0
+assert oracle.ireduce(C.MPI_SUM, C.MPI_FLOAT, p - 1, xr, er) == 0      # NBC task list: root-relative ranks
 per = 5003
 xs_b = inputs("MPI_MAX", "MPI_DOUBLE", per * p, 6001)
 es_b = [raw(np.zeros(per, xs_b[0].dtype)) for _ in range(p)]
