@@ -70,14 +70,43 @@ def run_collectives_child(world, rank, local, scale, transport="ipc"):
                 "MSX_BOOTSTRAP_PORT": str((int(os.environ.get("MASTER_PORT", "29500")) + off) % 65536),
                 "MSX_BOOTSTRAP_TIMEOUT": "90",
                 "MSX_BENCH_LOG": os.environ.get("MSX_BENCH_LOG", os.devnull)})
+    mine = f"{out}.rank{rank}"
+    for path in (out, mine):
+        if os.path.exists(path):
+            os.remove(path)
+
+    def child_error(what, stderr):
+        """The child's own structured error (bench_collectives.fail), else the
+        library's MSX_STUCK reports (rank, phase, peer of a blocked step)."""
+        try:
+            with open(mine) as f:
+                err = json.load(f).get("error")
+            if err:
+                return err
+        except (OSError, ValueError):
+            pass
+        stuck = []
+        for line in (stderr or "").splitlines():
+            if line.startswith("MSX_STUCK "):
+                try:
+                    stuck.append(json.loads(line[len("MSX_STUCK "):]))
+                except ValueError:
+                    pass
+        err = {"rank": rank, "text": f"child {what}: {(stderr or '')[-400:]}"}
+        if stuck:
+            err.update({"kind": "stuck", "phase": stuck[-1].get("phase"), "peer": stuck[-1].get("peer"),
+                        "stuck": stuck[-4:]})
+        return err
+
     try:
         pr = subprocess.run([sys.executable, os.path.join(REPO, "bench_collectives.py"), out, str(scale)],
                             env=env, capture_output=True, text=True,
                             timeout=float(os.environ.get("MSX_COLL_TIMEOUT", "150" if transport == "ipc" else "120")))
         if pr.returncode != 0:
-            return {"error": f"rank {rank} child rc={pr.returncode}: {pr.stderr[-600:]}"}
+            return {"error": child_error(f"rc={pr.returncode}", pr.stderr)}
     except subprocess.TimeoutExpired as e:
-        return {"error": f"rank {rank} child timed out: {str(e.stderr)[-600:] if e.stderr else ''}"}
+        se = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else e.stderr
+        return {"error": child_error("timed out", se)}
     if rank == 0:
         try:
             with open(out) as f:
@@ -206,7 +235,50 @@ def pmc_raw(kernel_substr):
     return out
 
 
+def host_cpu_info():
+    """CPU model, sockets, NUMA nodes and the cores this job may use
+    (recorded next to the CPU baseline)."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["cores_allowed"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        models, sockets = set(), set()
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                if k.strip() == "model name":
+                    models.add(v.strip())
+                elif k.strip() == "physical id":
+                    sockets.add(v.strip())
+        info["model"] = " / ".join(sorted(models)) or None
+        info["sockets"] = len(sockets) or None
+    except OSError:
+        pass
+    info["numa_nodes"] = len(glob.glob("/sys/devices/system/node/node[0-9]*")) or None
+    return info
+
+
+def _median_rate(fn, bytes_per_call, seconds, min_iters=20, warmup=3):
+    """3 warm-up calls, then at least `min_iters` timed calls
+    (and at least `seconds` of them); returns (median seconds per call, calls)."""
+    for _ in range(warmup):
+        fn()
+    ts, t_end = [], time.perf_counter() + seconds
+    while len(ts) < min_iters or time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], len(ts)
+
+
 def cpu_baseline(seconds, elems):
+    """The oracle's Op<float>::Sum (the C restatement of op.cpp:42-52) on this
+    box's host: one thread (what one MS-MPI rank runs) and every core allotted
+    to the job (elements sharded), median of >= 20 calls after 3 warm-ups over
+    the full 2 x 256 MiB operands (>> LLC)."""
     import numpy as np
     import oracle
     import msx
@@ -215,36 +287,21 @@ def cpu_baseline(seconds, elems):
     rng = np.random.default_rng(0x5EED)
     a = rng.uniform(-1, 1, n).astype(np.float32)
     b = rng.uniform(-1, 1, n).astype(np.float32)
-    oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b)      # warm-up / page-in
-    calls, t0 = 0, time.perf_counter()
-    while True:
-        oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b)
-        calls += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    gib = calls * n * BYTES_PER_ELEM / el / 2**30
-    out = {"value": round(gib, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-           "sample": f"{calls} calls of oracle Op<float>::Sum over 2 x {n * 4 >> 20} MiB host buffers "
-                     f"({el:.1f} s, 1 thread = one MS-MPI rank)",
-           "payload_GiB_s": round(calls * n * 4 / el / 2**30, 3)}
+    t1, k1 = _median_rate(lambda: oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b), n * BYTES_PER_ELEM, seconds)
+    cpu = host_cpu_info()
+    out = {"value": round(n * BYTES_PER_ELEM / t1 / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+           "sample": f"median of {k1} calls (after 3 warm-ups) of oracle Op<float>::Sum over 2 x {n * 4 >> 20} MiB "
+                     f"host buffers, 1 thread = one MS-MPI rank",
+           "payload_GiB_s": round(n * 4 / t1 / 2**30, 3), "ms_per_call": round(t1 * 1e3, 3), "cpu": cpu}
     # every host core of this job, elements sharded across
     # threads (the box allots 16 cores to a one-GPU job)
-    try:
-        cores = min(16, len(os.sched_getaffinity(0)))
-    except AttributeError:
-        cores = min(16, os.cpu_count() or 1)
+    cores = min(16, cpu.get("cores_allowed") or os.cpu_count() or 1)
     if cores > 1:
-        oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=cores)
-        calls, t0 = 0, time.perf_counter()
-        while True:
-            oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=cores)
-            calls += 1
-            el = time.perf_counter() - t0
-            if el >= seconds / 3:
-                break
-        out["all_cores"] = {"value": round(calls * n * BYTES_PER_ELEM / el / 2**30, 3), "unit": "GiB/s",
-                            "cores": cores, "sample": f"{calls} calls, {el:.1f} s, {cores} threads"}
+        tN, kN = _median_rate(lambda: oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=cores),
+                              n * BYTES_PER_ELEM, seconds / 3)
+        out["all_cores"] = {"value": round(n * BYTES_PER_ELEM / tN / 2**30, 3), "unit": "GiB/s", "cores": cores,
+                            "payload_GiB_s": round(n * 4 / tN / 2**30, 3), "ms_per_call": round(tN * 1e3, 3),
+                            "sample": f"median of {kN} calls after 3 warm-ups, {cores} threads"}
     return out
 
 
@@ -269,7 +326,10 @@ def cpu_baseline_collectives(p=8, seconds_each=2.0):
     recursive-halving reduce_scatter), p ranks simulated in lock step on ONE
     core with memcpy as the transport: the combine + copy work of a p-rank
     MS-MPI job, serialised.  Bounded samples (SURVEY.md §8(d) CPU baseline for
-    c3-c5): 16 MiB per rank for c3 / c5, a 64 MiB sendbuf per rank for c4.
+    c3-c5): 16 MiB per rank for c3 / c5, a 64 MiB sendbuf per rank for c4 --
+    with the simulator's per-rank scratch, 0.5-1 GiB of host memory per call,
+    far above the LLC, so the memory-bound rate does not depend on the size;
+    median of >= 20 calls after 3 warm-ups.
     busBW uses the same formulas as the GPU numbers (S/t·2(p-1)/p, S/t·(p-1)/p)."""
     import numpy as np
     import oracle
@@ -278,14 +338,7 @@ def cpu_baseline_collectives(p=8, seconds_each=2.0):
     rng = np.random.default_rng(0x5EED)
 
     def timed(fn):
-        fn()
-        calls, t0 = 0, time.perf_counter()
-        while True:
-            fn()
-            calls += 1
-            el = time.perf_counter() - t0
-            if el >= seconds_each:
-                return el / calls, calls
+        return _median_rate(fn, 0, seconds_each)
 
     out = {"ranks_simulated": p, "cores": 1, "kind": "port"}
     n = 1 << 22
@@ -582,11 +635,54 @@ def rma_self_roofline(L, C, torch, dev, n):
             "frac": round(gbs / HBM_PEAK_GBS, 4), "correct": correct}
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    script (one per GPU: LOCAL_RANK = rank; on a box with fewer GPUs they share
+    them round-robin), the way `torch.distributed.run --nproc-per-node N` would,
+    before this process touches any GPU.  Rank 0 prints the JSON line; the exit
+    status is the first failing rank's.  A rank that fails takes the others
+    down after a grace period, so nothing waits for gloo's 30-minute timeout."""
+    import signal
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(args.gpus),
+                    "LOCAL_WORLD_SIZE": str(args.gpus), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc, failed_at = 0, None
+    while any(pr.poll() is None for pr in procs):
+        bad = [pr for pr in procs if pr.poll() not in (None, 0)]
+        if bad and failed_at is None:
+            failed_at = time.time()
+            rc = bad[0].returncode
+        if failed_at is not None and time.time() - failed_at > 60:
+            for pr in procs:
+                if pr.poll() is None:
+                    os.killpg(pr.pid, signal.SIGKILL)
+        time.sleep(0.2)
+    for pr in procs:
+        if pr.returncode and not rc:
+            rc = pr.returncode
+    return rc
+
+
 def main():
     args = parse()
     if args.rccl_native_child:
         rccl_native_child_main(args.rccl_native_child, args.coll_scale)
         return
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: the launcher and the flag disagree")
     import torch
     import torch.distributed as dist
     import msx
@@ -705,7 +801,11 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+    kern_all = [kern_ms]
     if world > 1:
+        parts = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, t)
+        kern_all = [float(x[1]) for x in parts]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms_max = float(t[0]), float(t[1])
 
@@ -716,11 +816,13 @@ def main():
     if world > 1 and not args.no_collectives:
         def collect(transport):
             mine = run_collectives_child(world, rank, local, args.coll_scale, transport)
-            ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            errs = [None] * world
+            dist.all_gather_object(errs, mine.get("error"))      # every rank's structured error
             res = mine if rank == 0 else None
-            if rank == 0 and not ok.item() and "error" not in res:
-                res["error"] = "a non-zero rank's child failed"
+            if rank == 0 and any(e is not None for e in errs):
+                res["errors"] = [dict(e, rank=r) if isinstance(e, dict) else {"rank": r, "text": e}
+                                 for r, e in enumerate(errs) if e is not None]
+                res.setdefault("error", res["errors"][0])
             return res
         coll = collect("ipc")
         if distinct:
@@ -802,10 +904,29 @@ def main():
                          "bytes_per_launch": n * BYTES_PER_ELEM,
                          "kernel_us_mean": round(kern_ms * 1e3, 2),
                          "timing": "HIP events around the K launches on the launch stream / K",
-                         "kernel_us_mean_max_rank": round(kern_ms_max * 1e3, 2)},
+                         "kernel_us_mean_max_rank": round(kern_ms_max * 1e3, 2),
+                         "kernel_us_mean_per_rank": [round(k * 1e3, 2) for k in kern_all]},
         }
         if host is not None:
             out["host_path"] = host
+        def summarize(c):
+            """c3-c5 of one data plane at a glance: correct, busBW, fractions."""
+            if not c:
+                return None
+            sm = {}
+            for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4"),
+                             ("c5_iallreduce_band_u64", "c5")):
+                v = c.get(key)
+                if v:
+                    sm[tag] = {k: v.get(k) for k in ("correct", "busbw_GB_s", "busbw_frac_measured_links",
+                                                      "busbw_frac_xgmi") if k in v}
+            if c.get("peer_write_probe"):
+                sm["measured_links_GB_s_per_gpu"] = c["peer_write_probe"].get("outbound_GB_s_per_gpu")
+            if "error" in c:
+                sm["error"] = c["error"]
+            return sm
+        if coll is not None or coll_rccl is not None:
+            out["collectives_summary"] = {"ipc": summarize(coll), "rccl": summarize(coll_rccl)}
         if coll is not None:
             out["collectives"] = coll
         if coll_rccl is not None:

@@ -19,6 +19,7 @@ path in argv[1].
 import ctypes
 import json
 import os
+import re
 import sys
 import time
 
@@ -52,8 +53,33 @@ def main(out_path, scale):
 
     log(f"init ok p={p} scale={scale}")
 
+    def fail(config, rc):
+        """Fail fast with a structured error: which config, and -- parsed from
+        the library's timeout text (flag_timeout / ShmBarrier / Hub in
+        msx_transport.cpp) -- which rank waited in which phase for which peer.
+        Every rank writes <out>.rank<r>; the parent gathers them into its JSON
+        line.  No MPI_Finalize: the peers may be gone."""
+        text = msx.last_error()
+        err = {"config": config, "rank": rank, "rc": rc, "text": text}
+        m = re.search(r"(flag timeout|wait timeout|ipc error): op=(\S+) rank=(-?\d+) phase=(\S+) peer=(-?\d+)", text)
+        if m:
+            err.update({"kind": m.group(1), "op": m.group(2), "phase": m.group(4), "peer": int(m.group(5))})
+        res["error"] = err
+        log(f"FAILED {err}")
+        for path in ([out_path] if rank == 0 else []) + [f"{out_path}.rank{rank}"]:
+            with open(path, "w") as f:
+                json.dump(res, f)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(3)
+
+    def check(config, rc):
+        if rc:
+            fail(config, rc)
+        return rc
+
     def barrier():
-        L.MPI_Barrier(C.MPI_COMM_WORLD)
+        check("barrier", L.MPI_Barrier(C.MPI_COMM_WORLD))
 
     # ---- c3: allreduce SUM fp32, 1 GiB per rank ------------------------------
     n = int((256 << 20) * scale)
@@ -90,7 +116,7 @@ def main(out_path, scale):
         times.append(time.perf_counter() - t0)
         log(f"c3 iter {it} rc={rc} {times[-1]:.4f}s")
         if rc:
-            res["c3_error"] = f"rc={rc} {msx.last_error()}"
+            fail("c3", rc)
             break
     if "c3_error" not in res:
         t = sorted(times[1:])[len(times[1:]) // 2]
@@ -120,7 +146,8 @@ def main(out_path, scale):
             a, want = torch.ones(m, device=dev), torch.full((m,), float(p), device=dev)
         b = torch.empty_like(a)
         torch.cuda.synchronize()
-        L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+        check(f"allreduce_curve_{nbytes}",
+              L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD))
         # back-to-back calls after one barrier, averaged (the OSU latency
         # method: no barrier wake-up skew inside the timed calls)
         iters = 50 if nbytes <= (4 << 20) else 10
@@ -129,7 +156,8 @@ def main(out_path, scale):
             barrier()
             t0 = time.perf_counter()
             for _ in range(iters):
-                L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+                check(f"allreduce_curve_{nbytes}",
+                      L.MPI_Allreduce(a.data_ptr(), b.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD))
             ts.append((time.perf_counter() - t0) / iters)
         t = sorted(ts)[1]
         curve[str(nbytes)] = {"us": round(t * 1e6, 1), "busbw_GB_s": round(nbytes / t / 1e9 * 2 * (p - 1) / p, 2),
@@ -144,7 +172,8 @@ def main(out_path, scale):
         barrier()
         t0 = time.perf_counter()
         for _ in range(50):
-            L.MPI_Reduce(a.data_ptr(), out.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, 0, C.MPI_COMM_WORLD)
+            check("reduce_4096B", L.MPI_Reduce(a.data_ptr(), out.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM, 0,
+                                               C.MPI_COMM_WORLD))
         ts.append((time.perf_counter() - t0) / 50)
     res["reduce_4096B_root0_us"] = {"us": round(sorted(ts)[1] * 1e6, 1),
                                      "correct": bool(torch.all(out == p).item()) if rank == 0 else None}
@@ -170,7 +199,7 @@ def main(out_path, scale):
         rc = L.MPI_Allreduce(hsend.ctypes.data, hrecv.ctypes.data, nh, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
         ts.append(time.perf_counter() - t0)
         if rc:
-            res["c3_host_error"] = f"rc={rc} {msx.last_error()}"
+            fail("c3_host", rc)
             break
     if "c3_host_error" not in res:
         t = sorted(ts[1:])[len(ts[1:]) // 2]
@@ -203,7 +232,7 @@ def main(out_path, scale):
                                   C.MPI_COMM_WORLD)
         ts.append(time.perf_counter() - t0)
         if rc:
-            res["c4_host_error"] = f"rc={rc} {msx.last_error()}"
+            fail("c4_host", rc)
             break
     if "c4_host_error" not in res:
         t = sorted(ts[1:])[len(ts[1:]) // 2]
@@ -232,7 +261,7 @@ def main(out_path, scale):
         rc = rc or L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1))
         ts.append(time.perf_counter() - t0)
         if rc:
-            res["c5_host_error"] = f"rc={rc} {msx.last_error()}"
+            fail("c5_host", rc)
             break
     if "c5_host_error" not in res:
         t = sorted(ts[1:])[len(ts[1:]) // 2]
@@ -266,7 +295,7 @@ def main(out_path, scale):
         times.append(time.perf_counter() - t0)
         log(f"c4 iter {it} rc={rc} {times[-1]:.4f}s")
         if rc:
-            res["c4_error"] = f"rc={rc} {msx.last_error()}"
+            fail("c4", rc)
             break
     if "c4_error" not in res:
         t = sorted(times[1:])[len(times[1:]) // 2]
@@ -305,7 +334,8 @@ def main(out_path, scale):
     for _ in range(2):
         barrier()
         t0 = time.perf_counter()
-        rc |= L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD)
+        rc = check("c5_blocking", L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND,
+                                                  C.MPI_COMM_WORLD))
         t_comm = min(t_comm, time.perf_counter() - t0)
     # size the host loop to about the communication time, so the overlap is
     # measurable: efficiency = hidden time / min(t_comm, t_host), 1 = perfect
@@ -328,7 +358,7 @@ def main(out_path, scale):
     t_total = time.perf_counter() - t0
     log(f"c5 done rc={rc},{rc2},{rc3} comm={t_comm:.4f} host={t_host:.4f} total={t_total:.4f}")
     if rc or rc2 or rc3:
-        res["c5_error"] = f"rc={rc},{rc2},{rc3} {msx.last_error()}"
+        fail("c5", rc or rc2 or rc3)
     else:
         S = n * 8
         res["c5_iallreduce_band_u64"] = {
@@ -368,7 +398,7 @@ def main(out_path, scale):
     t, rc = timed(lambda: L.MPI_Reduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, 0,
                                        C.MPI_COMM_WORLD))
     if rc:
-        res["reduce_error"] = f"rc={rc} {msx.last_error()}"
+        fail("reduce", rc)
     else:
         S = n * 4
         res["reduce_sum_f32_root0"] = {"bytes_per_rank": S, "seconds": round(t, 5),
@@ -387,7 +417,7 @@ def main(out_path, scale):
     t, rc = timed(lambda: L.MPI_Scan(send2.data_ptr(), out.data_ptr(), m, C.MPI_FLOAT, C.MPI_SUM,
                                      C.MPI_COMM_WORLD))
     if rc:
-        res["scan_error"] = f"rc={rc} {msx.last_error()}"
+        fail("scan", rc)
     else:
         res["scan_sum_f32"] = {"bytes_per_rank": m * 4, "seconds": round(t, 5),
                                "GB_s_per_rank": round(m * 4 / t / 1e9, 2), "correct": bool(torch.equal(out, pre))}
@@ -417,7 +447,7 @@ def main(out_path, scale):
             if rc:
                 break
     if rc:
-        res["rma_error"] = f"rc={rc} {msx.last_error()}"
+        fail("rma", rc)
     else:
         t = sorted(ts[1:])[len(ts[1:]) // 2]
         src_rank = (rank - 1) % p
@@ -446,7 +476,7 @@ def main(out_path, scale):
         for key, fn in (("rma_accumulate_sum_f32_lock", passive), ("rma_accumulate_sum_f32_pscw", pscw)):
             t, rc = timed(fn)
             if rc:
-                res[key] = {"error": f"rc={rc} {msx.last_error()}"}
+                fail(key, rc)
                 break
             barrier()
             done += (3 + 1) * (src_rank + 1)

@@ -60,7 +60,34 @@ extern "C" {
 #define MPI_ERR_SIZE        51
 #define MPI_ERR_DISP        52
 #define MPI_ERR_ASSERT      53
+/* classes of the MPI-2 subsystems outside the reduction path (I/O, dynamic
+ * processes, attributes): values as the reference header, so code that names
+ * them compiles unchanged */
+#define MPI_ERR_ACCESS      20
+#define MPI_ERR_AMODE       21
+#define MPI_ERR_BAD_FILE    22
+#define MPI_ERR_CONVERSION  23
+#define MPI_ERR_DUP_DATAREP 24
+#define MPI_ERR_FILE_EXISTS 25
+#define MPI_ERR_FILE_IN_USE 26
+#define MPI_ERR_FILE        27
+#define MPI_ERR_INFO_KEY    29
+#define MPI_ERR_INFO_VALUE  30
+#define MPI_ERR_INFO_NOKEY  31
+#define MPI_ERR_IO          32
+#define MPI_ERR_NAME        33
+#define MPI_ERR_NO_SPACE    36
+#define MPI_ERR_NO_SUCH_FILE 37
+#define MPI_ERR_PORT        38
+#define MPI_ERR_QUOTA       39
+#define MPI_ERR_READ_ONLY   40
+#define MPI_ERR_SERVICE     41
+#define MPI_ERR_SPAWN       42
+#define MPI_ERR_UNSUPPORTED_DATAREP 43
+#define MPI_ERR_UNSUPPORTED_OPERATION 44
+#define MPI_ERR_KEYVAL      48
 #define MPI_ERR_LASTCODE    0x3fffffff
+#define MPICH_ERR_LAST_CLASS 53
 
 #define MPI_MAX_ERROR_STRING 512
 #define MPI_MAX_PROCESSOR_NAME 128

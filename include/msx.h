@@ -63,6 +63,37 @@ int msx_op_check(MPI_Op op, MPI_Datatype datatype);
 /* element size in bytes of a predefined datatype (-1 if unknown) */
 int msx_type_size(MPI_Datatype datatype);
 
+/* The builtin op table, MPIR_Op_table (src/mpi/msmpi/mpid/op.cpp:618-622),
+ * entries MPIR_Op_<op> (op.cpp:703-1923): the MPI_User_function shape that
+ * MPID_Uop_call (include/op.h:171-174), the NBC reduce tasks (tasks.cpp:667,
+ * 680), RMA accumulate (win.cpp:1435) and the Fortran proxy (mpif.cpp:963-976)
+ * call.  Blocking: `inout` holds the result on return; operands may be device
+ * memory (the gfx950 kernels run on it) or host memory (offloaded like
+ * MPI_Reduce_local).  *len <= 0 does nothing.  An unsupported (op, datatype)
+ * pair leaves inout untouched and sets the calling thread's op_errno to
+ * MPI_ERR_OP (op.cpp:1791); a GPU failure also lands there.
+ * msx_op_table(op) returns the entry of MPI_MAX .. MPI_NO_OP (NULL for any
+ * other handle). */
+void msx_op_max(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_min(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_sum(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_prod(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_land(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_band(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_lor(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_bor(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_lxor(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_bxor(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_minloc(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_maxloc(void* in, void* inout, int* len, MPI_Datatype* dt);
+void msx_op_replace(void* in, void* inout, int* len, MPI_Datatype* dt);   /* MPIR_Op_replace op.cpp:1886 */
+void msx_op_noop(void* in, void* inout, int* len, MPI_Datatype* dt);      /* MPIR_Op_noop op.cpp:1906 */
+MPI_User_function* msx_op_table(MPI_Op op);
+/* op_errno of the calling thread (Mpi.CallState->op_errno,
+ * include/MpiCallState.h:13) and its reset (reduce.cpp:97, 3794) */
+int msx_op_errno(void);
+void msx_op_errno_reset(void);
+
 /* inout[i] = inout[i] (op) in[i], i in [0,count); device pointers,
  * stream-ordered (returns after the launch, not after completion). */
 int msx_reduce_local_dev(const void* in, void* inout, int64_t count,

@@ -2295,6 +2295,79 @@ MSX_EXPORT int msx_op_check(MPI_Op op, MPI_Datatype dt)
 
 MSX_EXPORT int msx_type_size(MPI_Datatype dt) { return type_size(dt); }
 
+// ---- the builtin op table (MPIR_Op_table, mpid/op.cpp:618-622, :703-1923) ----
+// Each entry has the MPI_User_function shape the reference's internal callers
+// bind to: NBC reduce tasks (mpid/tasks.cpp:667,680), RMA accumulate
+// (mpid/win.cpp:1435, packethandling.cpp:2938,3046), the Fortran proxy
+// (fortran/mpif.cpp:963-976) and MPID_Uop_call (include/op.h:171-174).  Like
+// MPIR_Op_<op> they validate nothing up front: `*len` <= 0 does nothing (the
+// reference loops `while(--len >= 0)`), and a datatype outside the op's table
+// leaves inout untouched and sets the calling thread's op_errno to MPI_ERR_OP
+// (op.cpp:732,...,1791; Mpi.CallState->op_errno, include/MpiCallState.h:13).
+// Device operands (or pinned / pageable host memory, offloaded like
+// MPI_Reduce_local) are combined by the gfx950 kernels; the call returns with
+// the result in `inout`.  A failure of the GPU path also lands in op_errno.
+namespace {
+thread_local int t_op_errno = 0;
+
+void op_entry(int opidx, void* in, void* inout, int* len, MPI_Datatype* dt)
+{
+    if (!len || !dt || *len <= 0) return;
+    if (op_check_dtype(opidx, *dt) != MPI_SUCCESS) {
+        set_error("**opundefined: builtin op %d on datatype 0x%x", opidx, *dt);
+        t_op_errno = MPI_ERR_OP;
+        return;
+    }
+    const int rc = reduce_local_any(opidx, type_info(*dt)->kind, in, inout, (size_t)*len);
+    if (rc != MPI_SUCCESS) t_op_errno = rc;
+}
+}  // namespace
+
+#define MSX_OP_ENTRY(fn, idx) \
+    MSX_EXPORT void fn(void* in, void* inout, int* len, MPI_Datatype* dt) { op_entry(idx, in, inout, len, dt); }
+MSX_OP_ENTRY(msx_op_max, O_MAX)
+MSX_OP_ENTRY(msx_op_min, O_MIN)
+MSX_OP_ENTRY(msx_op_sum, O_SUM)
+MSX_OP_ENTRY(msx_op_prod, O_PROD)
+MSX_OP_ENTRY(msx_op_land, O_LAND)
+MSX_OP_ENTRY(msx_op_band, O_BAND)
+MSX_OP_ENTRY(msx_op_lor, O_LOR)
+MSX_OP_ENTRY(msx_op_bor, O_BOR)
+MSX_OP_ENTRY(msx_op_lxor, O_LXOR)
+MSX_OP_ENTRY(msx_op_bxor, O_BXOR)
+MSX_OP_ENTRY(msx_op_minloc, O_MINLOC)
+MSX_OP_ENTRY(msx_op_maxloc, O_MAXLOC)
+#undef MSX_OP_ENTRY
+
+// MPIR_Op_replace (op.cpp:1886-1903): MPIR_Localcopy(in -> inout), any datatype
+MSX_EXPORT void msx_op_replace(void* in, void* inout, int* len, MPI_Datatype* dt)
+{
+    if (!len || !dt || *len <= 0) return;
+    const int rc = local_copy(in, inout, (size_t)*len, *dt);
+    if (rc != MPI_SUCCESS) t_op_errno = rc;
+}
+
+// MPIR_Op_noop (op.cpp:1906-1923)
+MSX_EXPORT void msx_op_noop(void*, void*, int*, MPI_Datatype*) {}
+
+// MPIR_Op_table[op % 16 - 1]: the entry of a builtin op handle
+// (MPI_MAX .. MPI_NO_OP, 0x58000001 .. 0x5800000e), NULL for anything else.
+MSX_EXPORT MPI_User_function* msx_op_table(MPI_Op op)
+{
+    static MPI_User_function* const kTable[] = {
+        msx_op_max, msx_op_min, msx_op_sum, msx_op_prod, msx_op_land, msx_op_band, msx_op_lor,
+        msx_op_bor, msx_op_lxor, msx_op_bxor, msx_op_minloc, msx_op_maxloc, msx_op_replace, msx_op_noop};
+    static_assert(sizeof(kTable) / sizeof(kTable[0]) == O_NOOP, "one entry per builtin op");
+    const int idx = op & 0xff;
+    if ((op & ~0xff) != (MPI_MAX & ~0xff) || idx < O_MAX || idx > O_NOOP) return nullptr;
+    return kTable[idx - 1];
+}
+
+// Mpi.CallState->op_errno of the calling thread: read it, and clear it before
+// a sequence of calls (the collectives do `op_errno = 0`, reduce.cpp:97,3794).
+MSX_EXPORT int msx_op_errno(void) { return t_op_errno; }
+MSX_EXPORT void msx_op_errno_reset(void) { t_op_errno = 0; }
+
 MSX_EXPORT int msx_reduce_local_dev(const void* in, void* inout, int64_t count, MPI_Datatype dt,
                                     MPI_Op op, void* stream)
 {

@@ -100,6 +100,7 @@ int world_init()
     (void)ensure_device();
     g_world.rank = rank;
     g_world.size = size;
+    set_diag_rank(rank);
     g_world.lpid.resize((size_t)size);
     for (int r = 0; r < size; ++r) g_world.lpid[(size_t)r] = r;
     g_self.lpid.assign(1, rank);

@@ -59,12 +59,14 @@ struct TreeSpec {
     // GPU-side arrival wait (barrier-free small allreduce): before reading,
     // every workgroup waits until wait_flags[r] >= wait_seq for all r < wait_n,
     // r != wait_skip (flags posted by peers with launch_post_flags); after
-    // ~20 s without them it stores 1 to *wait_err (host-visible) and exits.
+    // flag_wait_seconds() without them it stores wait_tag * 65536 + 1 + r (r =
+    // the first peer missing) to *wait_err (host-visible) and exits.
     const unsigned long long* wait_flags = nullptr;
     unsigned long long wait_seq = 0;
     int wait_n = 0;
     int wait_skip = -1;
     int* wait_err = nullptr;
+    int wait_tag = 1;
     // Fused push (the barrier-free small allreduce in one launch): extra
     // workgroups copy push_n[i] bytes push_src[i] -> push_dst[i] with
     // system-coherent stores and, once all of them completed, store push_seq
@@ -105,14 +107,19 @@ hipError_t launch_push_post(const void* const* src, void* const* dst, const size
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
                             unsigned* counter, hipStream_t s);
 
-// launch_push_post's push and flags (nseg may be 0: wait only), plus ONE
-// workgroup that waits until wait_flags[r] >= seq for r < wait_n, r !=
-// wait_skip (~20 s bound, then 1 -> *wait_err).  Launches after it on `s`
-// read what the flags announce.
+// launch_push_post's push and flags (nseg may be 0: the flags are then
+// posted by the waiting workgroup itself), plus ONE workgroup that waits until
+// wait_flags[r] >= seq for r < wait_n, r != wait_skip (flag_wait_seconds()
+// bound, then wait_tag * 65536 + 1 + r -> *wait_err).  Launches after it on
+// `s` read what the flags announce.
 hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
                             unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,
-                            int* wait_err, hipStream_t s);
+                            int* wait_err, hipStream_t s, int wait_tag = 1);
+// Bound of every GPU flag wait: MSX_FLAG_TIMEOUT_MS (default 20000), in
+// s_memrealtime ticks and in seconds.
+unsigned long long flag_wait_ticks();
+double flag_wait_seconds();
 
 // Copy nseg independent byte ranges in one launch (one grid row per segment),
 // used to pull allgather blocks from every peer concurrently.

@@ -376,14 +376,19 @@ __global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsi
 // what the flags announce.
 __global__ __launch_bounds__(256) void k_push_wait(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
                                                    int sys, unsigned gx, const unsigned long long* wflags,
-                                                   unsigned long long wseq, int wn, int wskip, int* werr)
+                                                   unsigned long long wseq, int wn, int wskip, int* werr,
+                                                   unsigned long long wticks, int wtag)
 {
     const unsigned b = blockIdx.x;
     if (b < total) {
         copy_post_body(c, f, counter, total, sys, b / (unsigned)c.n, gx, (int)(b % (unsigned)c.n));
         return;
     }
-    (void)wait_flags_body(wflags, wseq, wn, wskip, werr);
+    // flags without data (no push workgroups): nothing to order them after,
+    // so the waiting workgroup posts them before it waits
+    if (total == 0 && threadIdx.x < (unsigned)f.n)
+        __hip_atomic_store(f.dst[threadIdx.x], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    (void)wait_flags_body(wflags, wseq, wn, wskip, werr, wticks, wtag);
 }
 
 }  // namespace dev
@@ -708,6 +713,8 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     a.wait_n = t.wait_n;
     a.wait_skip = t.wait_skip;
     a.wait_err = t.wait_err;
+    a.wait_ticks = flag_wait_ticks();
+    a.wait_tag = t.wait_tag;
     if (t.wait_flags && (!t.wait_err || t.wait_n < 0)) return hipErrorInvalidValue;
     if (t.push_nseg > 0) {
         if (t.push_nseg > kMaxSegs || t.push_nflags < 0 || t.push_nflags > 64 || !t.push_counter)
@@ -813,10 +820,23 @@ hipError_t launch_push_post(const void* const* src, void* const* dst, const size
     return hipGetLastError();
 }
 
+unsigned long long flag_wait_ticks()
+{
+    static const unsigned long long t = [] {
+        const char* e = getenv("MSX_FLAG_TIMEOUT_MS");
+        long long ms = e ? atoll(e) : 20000;
+        if (ms < 1) ms = 1;
+        return (unsigned long long)ms * 100000ull;          // s_memrealtime: 100 MHz
+    }();
+    return t;
+}
+
+double flag_wait_seconds() { return (double)flag_wait_ticks() / 1e8; }
+
 hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
                             unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,
-                            int* wait_err, hipStream_t s)
+                            int* wait_err, hipStream_t s, int wait_tag)
 {
     if (nseg < 0 || nseg > kMaxSegs || nflags < 0 || nflags > 64 || !wait_flags || !wait_err ||
         (nseg > 0 && !counter))
@@ -856,7 +876,7 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     const unsigned total = nseg > 0 ? (unsigned)(gx * (size_t)nseg) : 0u;
     c.wt = (wt_stores() && maxb < ((size_t)1 << 32)) ? 1 : 0;   // 32-bit buffer offsets
     hipLaunchKernelGGL(k_push_wait, dim3(total + 1), dim3(256), 0, s, c, f, counter, total, sys ? 1 : 0,
-                       (unsigned)gx, wait_flags, seq, wait_n, wait_skip, wait_err);
+                       (unsigned)gx, wait_flags, seq, wait_n, wait_skip, wait_err, flag_wait_ticks(), wait_tag);
     return hipGetLastError();
 }
 

@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <thread>
 #include <time.h>
 #include <unistd.h>
 #include <utility>
@@ -66,6 +67,77 @@ void set_error(const char* fmt, ...)
 }
 
 const char* last_error() { return g_err; }
+
+// ---- stuck-phase reporter ----------------------------------------------------
+// Host steps that can block on another process or GPU (IPC handle opens, the
+// bootstrap exchange, stream synchronisations) run inside a PhaseScope.  A
+// watchdog thread prints one line per step that exceeds MSX_STUCK_REPORT_S
+// (default 30 s; the bench children are killed at 120-150 s):
+//   MSX_STUCK {"rank":R,"phase":"...","peer":Q,"seconds":T}
+// so a hang on a multi-GPU node names the rank, the step and the peer in the
+// parent's JSON instead of surfacing as a bare timeout.
+namespace {
+constexpr int kPhaseSlots = 64;
+struct PhaseSlot {
+    std::atomic<int> used{0};
+    const char* phase = nullptr;
+    int peer = -1;
+    double t0 = 0;
+    bool reported = false;
+};
+PhaseSlot g_phase[kPhaseSlots];
+std::atomic<int> g_diag_rank{0};
+std::once_flag g_watch_once;
+
+double mono_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+void watchdog()
+{
+    const char* e = getenv("MSX_STUCK_REPORT_S");
+    const double limit = e ? atof(e) : 30.0;
+    for (;;) {
+        usleep(250 * 1000);
+        const double now = mono_s();
+        for (PhaseSlot& sl : g_phase) {
+            if (sl.used.load(std::memory_order_acquire) != 2 || sl.reported || now - sl.t0 < limit) continue;
+            sl.reported = true;
+            fprintf(stderr, "MSX_STUCK {\"rank\":%d,\"phase\":\"%s\",\"peer\":%d,\"seconds\":%.1f}\n",
+                    g_diag_rank.load(), sl.phase ? sl.phase : "?", sl.peer, now - sl.t0);
+            fflush(stderr);
+        }
+    }
+}
+}  // namespace
+
+void set_diag_rank(int r) { g_diag_rank.store(r); }
+
+PhaseScope::PhaseScope(const char* phase, int peer)
+{
+    std::call_once(g_watch_once, [] { std::thread(watchdog).detach(); });
+    for (int i = 0; i < kPhaseSlots; ++i) {
+        int z = 0;
+        if (g_phase[i].used.compare_exchange_strong(z, 1, std::memory_order_acq_rel)) {
+            PhaseSlot& sl = g_phase[i];
+            sl.phase = phase;
+            sl.peer = peer;
+            sl.t0 = mono_s();
+            sl.reported = false;
+            sl.used.store(2, std::memory_order_release);
+            slot_ = i;
+            return;
+        }
+    }
+}
+
+PhaseScope::~PhaseScope()
+{
+    if (slot_ >= 0) g_phase[slot_].used.store(0, std::memory_order_release);
+}
 
 void trace(const char* fmt, ...)
 {

@@ -29,6 +29,20 @@ void trace(const char* fmt, ...);
 void set_error(const char* fmt, ...);
 const char* last_error();
 
+// A host step that may block on another process or GPU; a watchdog thread
+// prints `MSX_STUCK {"rank":..,"phase":..,"peer":..,"seconds":..}` on stderr
+// once the step exceeds MSX_STUCK_REPORT_S (default 30 s).
+class PhaseScope {
+public:
+    PhaseScope(const char* phase, int peer = -1);
+    ~PhaseScope();
+    PhaseScope(const PhaseScope&) = delete;
+    PhaseScope& operator=(const PhaseScope&) = delete;
+private:
+    int slot_ = -1;
+};
+void set_diag_rank(int rank);   // the rank named in MSX_STUCK lines
+
 // Device bring-up.  Returns MPI_SUCCESS or MPI_ERR_OTHER (no usable GPU).
 int ensure_device();
 int current_device();

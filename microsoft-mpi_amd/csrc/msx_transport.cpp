@@ -181,16 +181,23 @@ public:
     {
         std::lock_guard<std::mutex> g(mu_);
         char* out = static_cast<char*>(all);
+        auto fail = [&](int peer, const char* phase) {
+            const std::string why = last_error();
+            set_error("wait timeout: op=hub_allgather rank=%d phase=%s peer=%d limit_s=%.1f (%s)", rank_, phase, peer,
+                      timeout_, why.c_str());
+            return MPI_ERR_OTHER;
+        };
         if (rank_ == 0) {
             memcpy(out, mine, n);
             for (int r = 1; r < size_; ++r)
-                if (io_all(fd_[r], out + (size_t)r * n, n, false, timeout_) != MPI_SUCCESS) return MPI_ERR_OTHER;
+                if (io_all(fd_[r], out + (size_t)r * n, n, false, timeout_) != MPI_SUCCESS) return fail(r, "gather");
             for (int r = 1; r < size_; ++r)
-                if (io_all(fd_[r], out, (size_t)size_ * n, true, timeout_) != MPI_SUCCESS) return MPI_ERR_OTHER;
+                if (io_all(fd_[r], out, (size_t)size_ * n, true, timeout_) != MPI_SUCCESS) return fail(r, "scatter");
             return MPI_SUCCESS;
         }
-        if (io_all(fd_[0], const_cast<void*>(mine), n, true, timeout_) != MPI_SUCCESS) return MPI_ERR_OTHER;
-        return io_all(fd_[0], out, (size_t)size_ * n, false, timeout_);
+        if (io_all(fd_[0], const_cast<void*>(mine), n, true, timeout_) != MPI_SUCCESS) return fail(0, "send");
+        if (io_all(fd_[0], out, (size_t)size_ * n, false, timeout_) != MPI_SUCCESS) return fail(0, "receive");
+        return MPI_SUCCESS;
     }
 
 private:
@@ -212,14 +219,18 @@ struct ShmBar {
     // per rank: sequence number of the last barrier-free call it has finished
     // (its tree has read its IN half), see do_allreduce
     std::atomic<uint64_t> done[kDoneSlots];
+    // per rank: 1 + the generation of the barrier it last entered (timeouts
+    // name the ranks that never arrived)
+    std::atomic<uint32_t> at[kDoneSlots];
 };
-static_assert(sizeof(ShmBar) <= 4096, "one page");
+constexpr size_t kShmBarBytes = 8192;
+static_assert(sizeof(ShmBar) <= kShmBarBytes, "two pages");
 
 class ShmBarrier {
 public:
     ~ShmBarrier()
     {
-        if (bar_) munmap(bar_, 4096);
+        if (bar_) munmap(bar_, kShmBarBytes);
     }
 
     // Collective over the hub.  Returns false (and stays unused) when shared
@@ -227,6 +238,7 @@ public:
     bool init(Hub& hub, int rank, int size, double timeout_s)
     {
         size_ = size;
+        rank_ = rank;
         timeout_ = timeout_s;
         char name[64] = {0};
         int fd = -1;
@@ -234,7 +246,7 @@ public:
             // created and sized before anyone learns the name
             snprintf(name, sizeof(name), "/msx_bar_%d_%ld", (int)getpid(), (long)(now_s() * 1e6));
             fd = shm_open(name, O_CREAT | O_RDWR, 0600);
-            if (fd < 0 || ftruncate(fd, 4096) != 0) name[0] = 0;
+            if (fd < 0 || ftruncate(fd, kShmBarBytes) != 0) name[0] = 0;
         }
         std::vector<char> all((size_t)size * sizeof(name));
         if (hub.allgather(name, sizeof(name), all.data()) != MPI_SUCCESS) {
@@ -246,7 +258,7 @@ public:
         if (ok && rank != 0) fd = shm_open(name, O_RDWR, 0600);
         std::vector<int> oks((size_t)size);
         void* m = MAP_FAILED;
-        if (ok && fd >= 0) m = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (ok && fd >= 0) m = mmap(nullptr, kShmBarBytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         if (fd >= 0) close(fd);
         int mine = (m != MAP_FAILED) ? 1 : 0;
         if (hub.allgather(&mine, sizeof(int), oks.data()) != MPI_SUCCESS) mine = 0;
@@ -254,7 +266,7 @@ public:
         for (int v : oks) all_ok = all_ok && v;
         if (rank == 0) shm_unlink(name);
         if (!all_ok) {
-            if (m != MAP_FAILED) munmap(m, 4096);
+            if (m != MAP_FAILED) munmap(m, kShmBarBytes);
             trace("shm barrier unavailable; hub barrier in use");
             return false;
         }
@@ -269,7 +281,11 @@ public:
     {
         const double t_end = now_s() + timeout_;
         for (int spin = 0; bar_->done[rank].load(std::memory_order_acquire) < v; ++spin) {
-            if (now_s() > t_end) { set_error("rank %d did not finish its previous call", rank); return MPI_ERR_OTHER; }
+            if (now_s() > t_end) {
+                set_error("wait timeout: op=flag_call rank=%d phase=previous_call_done peer=%d seq=%llu limit_s=%.1f",
+                          rank_, rank, (unsigned long long)v, timeout_);
+                return MPI_ERR_OTHER;
+            }
             if (spin > 2000) sched_yield();
         }
         return MPI_SUCCESS;
@@ -278,6 +294,7 @@ public:
     int wait()
     {
         const uint32_t g = bar_->gen.load(std::memory_order_acquire);
+        if (size_ <= kDoneSlots) bar_->at[rank_].store(g + 1, std::memory_order_relaxed);
         if (bar_->count.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)size_) {
             bar_->count.store(0, std::memory_order_relaxed);
             bar_->gen.store(g + 1, std::memory_order_release);
@@ -290,7 +307,15 @@ public:
             if (bar_->gen.load(std::memory_order_acquire) != g) return MPI_SUCCESS;
         const double t_end = now_s() + timeout_;
         while (bar_->gen.load(std::memory_order_acquire) == g) {
-            if (now_s() > t_end) { set_error("barrier: timed out"); return MPI_ERR_OTHER; }
+            if (now_s() > t_end) {
+                // the first rank that has not entered this barrier
+                int missing = -1;
+                for (int r = 0; r < size_ && r < kDoneSlots && missing < 0; ++r)
+                    if (bar_->at[r].load(std::memory_order_relaxed) != g + 1) missing = r;
+                set_error("wait timeout: op=barrier rank=%d phase=host_barrier peer=%d seq=%u limit_s=%.1f", rank_,
+                          missing, g, timeout_);
+                return MPI_ERR_OTHER;
+            }
             struct timespec ts = {0, 100 * 1000 * 1000};
             syscall(SYS_futex, reinterpret_cast<uint32_t*>(&bar_->gen), FUTEX_WAIT, g, &ts, nullptr, 0);
         }
@@ -300,6 +325,7 @@ public:
 private:
     ShmBar* bar_ = nullptr;
     int size_ = 1;
+    int rank_ = 0;
     double timeout_ = 600.0;
 };
 
@@ -380,7 +406,10 @@ public:
         size_t asz = 0;
         hipError_t e = hipMemGetAddressRange(&base, &asz, const_cast<void*>(ptr));
         trace("map_peers: ptr=%p base=%p size=%zu rc=%d", ptr, base, asz, (int)e);
-        if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, base);
+        if (e == hipSuccess) {
+            PhaseScope ph("ipc_get_handle");
+            e = hipIpcGetMemHandle(&mine.h, base);
+        }
         trace("map_peers: handle rc=%d", (int)e);
         if (e == hipSuccess) {
             mine.ok = 1;
@@ -390,7 +419,11 @@ public:
             set_error("rank %d: buffer %p cannot be shared over IPC (%s)", rank, ptr, hipGetErrorString(e));
         }
         std::vector<IpcRec> all((size_t)size);
-        int rc = hub_.allgather(&mine, sizeof(mine), all.data());
+        int rc;
+        {
+            PhaseScope ph("ipc_handle_exchange");
+            rc = hub_.allgather(&mine, sizeof(mine), all.data());
+        }
         trace("map_peers: exchanged rc=%d", rc);
         if (rc != MPI_SUCCESS) return rc;
         out.assign((size_t)size, nullptr);
@@ -406,9 +439,16 @@ public:
             if (it != opened_.end()) {
                 pbase = it->second;
             } else {
-                e = hipIpcOpenMemHandle(&pbase, all[r].h, hipIpcMemLazyEnablePeerAccess);
+                {
+                    PhaseScope ph("ipc_open", r);
+                    e = hipIpcOpenMemHandle(&pbase, all[r].h, hipIpcMemLazyEnablePeerAccess);
+                }
                 trace("map_peers: opened rank %d handle -> %p rc=%d", r, pbase, (int)e);
-                if (e != hipSuccess) return hip_fail(e, "hipIpcOpenMemHandle");
+                if (e != hipSuccess) {
+                    hip_fail(e, "hipIpcOpenMemHandle");
+                    set_error("ipc error: op=map_peers rank=%d phase=ipc_open peer=%d (%s)", rank, r, hipGetErrorString(e));
+                    return MPI_ERR_OTHER;
+                }
                 opened_[key] = pbase;
             }
             out[r] = static_cast<char*>(pbase) + all[r].offset;
@@ -893,8 +933,40 @@ Worker& worker()
     return w;
 }
 
+// A GPU flag wait ran out of time: the kernel stored tag * 65536 + 1 + r
+// into the pinned word (r = the first flag index still missing; for the
+// collectives' per-rank flags, the peer's rank).  One structured line, the
+// text of msx_last_error(), which bench_collectives.py parses into its JSON.
+int flag_timeout(const char* op, int me, int word, unsigned long long seq, bool index_is_rank = true)
+{
+    const int tag = word >> 16, idx = (word & 0xffff) - 1;
+    const char* phase = tag == 2 ? "result" : "arrival";
+    set_error("flag timeout: op=%s rank=%d phase=%s peer=%d seq=%llu limit_s=%.1f", op, me, phase,
+              index_is_rank ? idx : -1, seq, flag_wait_seconds());
+    trace("%s", last_error());
+    return MPI_ERR_OTHER;
+}
+
+// Fault injection for the timeout diagnostics (tests only):
+// MSX_FAULT_DROP_FLAGS=<rank>:<seq> -- that rank does not post its arrival
+// flags of flag-synchronised call <seq>, so its peers' waits run out.
+bool fault_drop_flags(int me, unsigned long long seq)
+{
+    static const std::pair<int, unsigned long long> f = [] {
+        const char* e = getenv("MSX_FAULT_DROP_FLAGS");
+        int r = -1;
+        unsigned long long q = 0;
+        if (e && sscanf(e, "%d:%llu", &r, &q) != 2) r = -1;
+        return std::make_pair(r, q);
+    }();
+    if (f.first != me || f.second != seq) return false;
+    trace("fault injection: rank %d drops the arrival flags of call %llu", me, seq);
+    return true;
+}
+
 int sync_stream(hipStream_t s, const char* what)
 {
+    PhaseScope ph(what);
     hipError_t e = hipStreamSynchronize(s);
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
 }
@@ -1793,7 +1865,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 if (r != me && (root < 0 || r == root)) {
                     if (seq > 2) rc = tp->wait_done(r, seq - 2);
                     sg.add(mine, w.sub(r, me) + half, count * esz);
-                    fl.push_back(w.flags(r) + me);
+                    if (!fault_drop_flags(me, seq)) fl.push_back(w.flags(r) + me);
                 }
             subs[(size_t)me] = const_cast<char*>(mine);
             int* err_host = nullptr;
@@ -1861,10 +1933,9 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             const int rs = sync_stream(s, "allreduce tree");
             if (rc == MPI_SUCCESS) rc = rs;
             if (rc == MPI_SUCCESS && bounce_dst) memcpy(dst, engine_bounce(1).host, nbytes);
-            if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
-                set_error("allreduce: a peer's contribution did not arrive within 20 s");
-                rc = MPI_ERR_OTHER;
-            }
+            if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
+                rc = flag_timeout(root < 0 ? "allreduce" : "reduce", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE),
+                                  seq);
             tp->post_done(seq);                   // this rank's tree no longer reads the half
             tp->rd_parity ^= 1;
             tp->window_open = true;
@@ -1946,7 +2017,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             if (seq > 2) rc = tp->wait_done(r, seq - 2);
             if (hi_of(r) > lo_of(r)) {
                 sg.add(mine + lo_of(r) * esz, w.sub(r, me) + half, (hi_of(r) - lo_of(r)) * esz);
-                fl.push_back(w.flags(r) + me);
+                if (!fault_drop_flags(me, seq)) fl.push_back(w.flags(r) + me);
             }
         }
         std::vector<int> dests;
@@ -2007,17 +2078,15 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         if (rc == MPI_SUCCESS && want) {
             // step 2: every peer's result in my OUT half, then into recvbuf
             hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq, false, nullptr,
-                                            w.flags(me) + kResultFlags, p, me, err_dev, s);
+                                            w.flags(me) + kResultFlags, p, me, err_dev, s, 2);
             if (e != hipSuccess) rc = hip_fail(e, "allreduce result wait");
             char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : dst;
             if (rc == MPI_SUCCESS) rc = copy_async(out, w.out(me) + obase, len * esz, s);
         }
         const int rs = sync_stream(s, "allreduce two-step");
         if (rc == MPI_SUCCESS) rc = rs;
-        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
-            set_error("allreduce: a peer's piece or result did not arrive within 20 s");
-            rc = MPI_ERR_OTHER;
-        }
+        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
+            rc = flag_timeout(root < 0 ? "allreduce" : "reduce", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), seq);
         tp->post_done(seq);
         tp->rd_parity ^= 1;
         tp->window_open = true;
@@ -2206,7 +2275,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
             if (rc == MPI_SUCCESS && seq > 2) rc = tp->wait_done(r, seq - 2);
             if (cnt && rc == MPI_SUCCESS) {
                 sg.add(v, w.sub(r, me) + half, cnt * esz);
-                fl.push_back(w.flags(r) + me);
+                if (!fault_drop_flags(me, seq)) fl.push_back(w.flags(r) + me);
             }
         }
         int* err_host = nullptr;
@@ -2229,10 +2298,8 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
         }
         const int rs = sync_stream(s, "reduce_scatter one-step");
         if (rc == MPI_SUCCESS) rc = rs;
-        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
-            set_error("reduce_scatter: a peer's block did not arrive within 20 s");
-            rc = MPI_ERR_OTHER;
-        }
+        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
+            rc = flag_timeout("reduce_scatter", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), seq);
         tp->post_done(seq);
         tp->rd_parity ^= 1;
         tp->window_open = true;
@@ -2626,10 +2693,8 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
             rc = copy_async(dst_dev ? static_cast<void*>(outv) : recvbuf, cur_r, bytes, s);
         const int rs = sync_stream(s, "scan");
         if (rc == MPI_SUCCESS) rc = rs;
-        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
-            set_error("scan: a peer's partial did not arrive within 20 s");
-            rc = MPI_ERR_OTHER;
-        }
+        if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
+            rc = flag_timeout("scan", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), seq, false);
         tp->post_done(seq);
         tp->rd_parity ^= 1;
         tp->window_open = true;
@@ -3720,10 +3785,8 @@ int p2p_finish(Comm* u, int rc, int* err_host)
 {
     const int rs = sync_stream(u->tp->stream(), "intercommunicator transfer");
     if (rc == MPI_SUCCESS) rc = rs;
-    if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE)) {
-        set_error("intercommunicator: the peer's data did not arrive within 20 s");
-        rc = MPI_ERR_OTHER;
-    }
+    if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
+        rc = flag_timeout("intercomm_p2p", u->rank, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), 0, false);
     return rc;
 }
 

@@ -226,6 +226,8 @@ struct TreeArgs {
     int wait_n;
     int wait_skip;
     int* wait_err;
+    unsigned long long wait_ticks;   // bound of the wait in s_memrealtime ticks (100 MHz)
+    int wait_tag;                    // phase code reported with a timeout
     // fused push (barrier-free small allreduce): the first npush workgroups
     // copy this rank's contribution into the peers' IN halves and post the
     // arrival flags (push_post_body) instead of evaluating the tree
@@ -269,10 +271,12 @@ __device__ __forceinline__ void tree_done(const TreeArgs& a, unsigned b, unsigne
 // Arrival wait of the barrier-free small allreduce: thread 0 of every
 // workgroup polls the peers' flags (uncached window memory, system-scope
 // loads) until each reaches the call's sequence number.  Bounded: after
-// ~20 s (s_memrealtime runs at 100 MHz) it reports through *wait_err and the
-// workgroup exits, so a missing peer can never leave a wave running.
+// `ticks` of s_memrealtime (100 MHz; MSX_FLAG_TIMEOUT_MS, default 20 s) it
+// reports through *wait_err -- tag * 65536 + 1 + the first peer whose flag is
+// missing, so the host can name the phase and the peer -- and the workgroup
+// exits, so a missing peer can never leave a wave running.
 __device__ __forceinline__ bool wait_flags_body(const unsigned long long* flags, unsigned long long seq, int n,
-                                                int skip, int* err)
+                                                int skip, int* err, unsigned long long ticks, int tag)
 {
     __shared__ int ok;
     if (threadIdx.x == 0) {
@@ -281,8 +285,8 @@ __device__ __forceinline__ bool wait_flags_body(const unsigned long long* flags,
         for (int r = 0; r < n && good; ++r) {
             if (r == skip) continue;
             while (__hip_atomic_load(flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
-                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                    __hip_atomic_store(err, tag * 65536 + 1 + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     good = 0;
                     break;
                 }
@@ -303,7 +307,7 @@ __device__ __forceinline__ bool wait_flags_body(const unsigned long long* flags,
 
 __device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
 {
-    return wait_flags_body(a.wait_flags, a.wait_seq, a.wait_n, a.wait_skip, a.wait_err);
+    return wait_flags_body(a.wait_flags, a.wait_seq, a.wait_n, a.wait_skip, a.wait_err, a.wait_ticks, a.wait_tag);
 }
 
 // Start-of-kernel system acquire: invalidate this CU's L1 and the XCD's L2

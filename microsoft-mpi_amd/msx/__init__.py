@@ -194,7 +194,7 @@ def exported_symbols():
         with open(os.path.join(INCLUDE_DIR, h)) as f:
             txt = f.read()
         names.update(re.findall(
-            r"(?:MPI_METHOD|double MPIAPI|const char\*|int)\s+((?:P?MPI|msx)_\w+)\s*\(", txt))
+            r"(?:MPI_METHOD|double MPIAPI|const char\*|int|void|MPI_User_function\*)\s+((?:P?MPI|msx)_\w+)\s*\(", txt))
     return sorted(names)
 
 

@@ -44,6 +44,48 @@ def test_handle_values_match_msmpi_abi():
             assert L.msx_type_size(h(name)) == (hv >> 8) & 0xFF, name
 
 
+# Constants of the reference header that name subsystems outside the reduction
+# path (MPI-IO, point-to-point / buffered sends, attributes and window
+# attributes, dynamic processes, matched probes): not declared by include/mpi.h.
+_OUT_OF_PATH_CONSTANTS = {
+    "MPI_APPNUM", "MPI_BSEND_OVERHEAD", "MPI_DISPLACEMENT_CURRENT", "MPI_FILE_NULL", "MPI_HOST", "MPI_IO",
+    "MPI_KEYVAL_INVALID", "MPI_LASTUSEDCODE", "MPI_MAX_DATAREP_STRING", "MPI_MAX_INFO_KEY", "MPI_MAX_INFO_VAL",
+    "MPI_MAX_LIBRARY_VERSION_STRING", "MPI_MAX_OBJECT_NAME", "MPI_MAX_PORT_NAME", "MPI_MESSAGE_NO_PROC",
+    "MPI_MESSAGE_NULL", "MPI_MODE_APPEND", "MPI_MODE_CREATE", "MPI_MODE_DELETE_ON_CLOSE", "MPI_MODE_EXCL",
+    "MPI_MODE_RDONLY", "MPI_MODE_RDWR", "MPI_MODE_SEQUENTIAL", "MPI_MODE_UNIQUE_OPEN", "MPI_MODE_WRONLY",
+    "MPI_SEEK_CUR", "MPI_SEEK_END", "MPI_SEEK_SET", "MPI_TAG_UB", "MPI_TYPECLASS_COMPLEX", "MPI_TYPECLASS_INTEGER",
+    "MPI_TYPECLASS_REAL", "MPI_UNIVERSE_SIZE", "MPI_WIN_BASE", "MPI_WIN_CREATE_FLAVOR", "MPI_WIN_DISP_UNIT",
+    "MPI_WIN_FLAVOR_ALLOCATE", "MPI_WIN_FLAVOR_CREATE", "MPI_WIN_FLAVOR_DYNAMIC", "MPI_WIN_FLAVOR_SHARED",
+    "MPI_WIN_MODEL", "MPI_WIN_SEPARATE", "MPI_WIN_SIZE", "MPI_WIN_UNIFIED", "MPI_WTIME_IS_GLOBAL",
+    "MSMPI_BSEND_OVERHEAD_V1", "MSMPI_BSEND_OVERHEAD_V2", "MSMPI_MODE_HIDDEN", "MSMPI_VER"}
+
+
+def test_header_constants_match_the_reference_header():
+    """Every integer constant of include/mpi.h that the reference's
+    src/include/mpi.h also defines has the reference's value (x64 branch), and
+    every reference constant is declared except the out-of-path list above.
+    The reference values are the data fixture tests/golden/mpi_h_constants.json
+    (229 constants), made by tests/golden/gen_mpi_h_constants.py from the
+    reference header in the survey container."""
+    import json
+    sys.path.insert(0, os.path.join(msx.REPO_ROOT, "tests", "golden"))
+    import gen_mpi_h_constants as gen
+    with open(os.path.join(msx.REPO_ROOT, "tests", "golden", "mpi_h_constants.json")) as f:
+        ref = json.load(f)["constants"]
+    with open(os.path.join(msx.REPO_ROOT, "include", "mpi.h")) as f:
+        ours = gen.parse(f.read(), defined={"_WIN64", "MSMPI_NO_SAL"})
+    shared = sorted(set(ref) & set(ours))
+    assert len(shared) >= 180
+    wrong = [(k, hex(ref[k]), hex(ours[k])) for k in shared if ref[k] != ours[k]]
+    assert not wrong, wrong
+    missing = sorted(set(ref) - set(ours) - _OUT_OF_PATH_CONSTANTS)
+    assert not missing, missing
+    # and the values the library itself reports (msx.C is read from the same header)
+    for k in shared:
+        if hasattr(C, k):
+            assert getattr(C, k) & 0xFFFFFFFF == ref[k] & 0xFFFFFFFF, k
+
+
 def test_type_sizes_llp64():
     L = msx.lib()
     assert L.msx_type_size(C.MPI_LONG) == 4 and L.msx_type_size(C.MPI_UNSIGNED_LONG) == 4
@@ -126,6 +168,46 @@ def test_no_gpu_fails_loudly_not_silently(msxlib):
     assert (b == 1).all()    # nothing computed on the CPU
     assert msxlib.msx_reduce_local_dev(a.ctypes.data, b.ctypes.data, 8, C.MPI_FLOAT, C.MPI_SUM,
                                        None) == C.MPI_ERR_OTHER
+
+
+def test_op_table_entries_without_gpu(msxlib):
+    """msx_op_table / msx_op_<op> (the MPIR_Op_table replacement, op.cpp:618-622,
+    703-1923): lookups, the MPI_User_function shape, op_errno semantics
+    (illegal pair -> MPI_ERR_OP with inout untouched, op.cpp:1791; len <= 0 does
+    nothing), and on a GPU-less host a loud MPI_ERR_OTHER instead of a CPU result."""
+    L = msxlib
+    UF = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+    L.msx_op_table.restype = ctypes.c_void_p
+    L.msx_op_table.argtypes = [ctypes.c_int]
+    names = ["max", "min", "sum", "prod", "land", "band", "lor", "bor", "lxor", "bxor", "minloc", "maxloc",
+             "replace", "noop"]
+    for k, nm in enumerate(names):
+        assert L.msx_op_table(0x58000001 + k) == ctypes.cast(getattr(L, "msx_op_" + nm), ctypes.c_void_p).value, nm
+    for bad in (C.MPI_OP_NULL, 0x5800000F, 0x58000000, 0x58000103, C.MPI_FLOAT):
+        assert L.msx_op_table(bad) is None, hex(bad)
+    L.msx_op_errno.restype = ctypes.c_int
+    a = np.arange(8, dtype=np.uint8)
+    b = np.full(8, 5, dtype=np.uint8)
+    n, dt = ctypes.c_int(8), ctypes.c_int(C.MPI_BYTE)
+    fsum = UF(L.msx_op_table(C.MPI_SUM))
+    L.msx_op_errno_reset()
+    fsum(a.ctypes.data, b.ctypes.data, ctypes.byref(n), ctypes.byref(dt))     # SUM on MPI_BYTE
+    assert L.msx_op_errno() == C.MPI_ERR_OP and (b == 5).all()
+    L.msx_op_errno_reset()
+    z = ctypes.c_int(0)
+    fsum(a.ctypes.data, b.ctypes.data, ctypes.byref(z), ctypes.byref(ctypes.c_int(C.MPI_INT)))
+    assert L.msx_op_errno() == 0 and (b == 5).all()
+    # noop / replace (host memcpy, no GPU needed)
+    fr = UF(L.msx_op_table(C.MPI_REPLACE))
+    fr(a.ctypes.data, b.ctypes.data, ctypes.byref(n), ctypes.byref(dt))
+    assert L.msx_op_errno() == 0 and (b == a).all()
+    if L.msx_device_count() == 0:
+        x = np.ones(8, np.float32)
+        y = np.full(8, 2, np.float32)
+        fsum(x.ctypes.data, y.ctypes.data, ctypes.byref(n), ctypes.byref(ctypes.c_int(C.MPI_FLOAT)))
+        assert L.msx_op_errno() == C.MPI_ERR_OTHER and (y == 2).all()
+        assert "no usable MI355X" in msx.last_error()
 
 
 class _Status(ctypes.Structure):

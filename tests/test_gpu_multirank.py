@@ -456,3 +456,44 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
         # RCCL needs one GPU per rank: ranks sharing a GPU keep the IPC engine
         n_dev = torch.cuda.device_count()
         assert used == ["rccl" if transport == "rccl" and n_dev >= p else "ipc"], used
+
+
+# One rank per GPU -- the deployment the north star names.  The one-GPU box
+# skips these; on a node with >= 2 visible GPUs they execute the cross-GPU data
+# paths that the shared-GPU cases above cannot: IPC windows opened on another
+# device (xGMI remote writes, system-scope write-through, peer flag polls) and
+# the RCCL send/recv plane, each checked bit for bit against the oracle.
+@pytest.mark.parametrize("transport", ["ipc", "rccl"])
+def test_collectives_one_rank_per_gpu(transport):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n_dev = torch.cuda.device_count()
+    if n_dev < 2:
+        pytest.skip("needs >= 2 GPUs (one rank per GPU)")
+    p = min(n_dev, 4)
+    port = _free_port()
+    procs = []
+    for r in range(p):
+        env = dict(os.environ)
+        env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": str(r),
+                    "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
+                    "MSX_BOOTSTRAP_TIMEOUT": "180", "MSX_TRANSPORT": transport,
+                    "MSX_FLAG_TIMEOUT_MS": "60000"})
+        procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    results = []
+    for pr in procs:
+        try:
+            o, e = pr.communicate(timeout=400)
+        except subprocess.TimeoutExpired:
+            pr.kill()
+            o, e = pr.communicate()
+        results.append((pr.returncode, o, e))
+    for rc, o, e in results:
+        assert rc == 0, (o + e)[-3000:]
+        line = [l for l in o.splitlines() if l.startswith("RESULT")]
+        assert line, (o + e)[-3000:]
+        assert line[0].split()[3] == "0", line[0]
+        used = [l.split()[1] for l in o.splitlines() if l.startswith("TRANSPORT")]
+        assert used == [transport], used
