@@ -540,7 +540,14 @@ def pack_roofline(L, C, torch, dev, stream):
         torch.cuda.synchronize()
         if rc or not torch.equal(packed, want.view(-1).view(torch.uint8)):
             raise RuntimeError(f"pack parity failed for {name}: rc={rc}")
-        res = {"packed_bytes": nb, "algorithmic_bytes_per_call": 2 * nb}
+        # HBM moves whole 32-B sectors: a gapped typed side touches more bytes
+        # than it carries (scripts/gap_probe.py: a bare 16-of-32-B store kernel
+        # reports WRITE_SIZE = 2x its data too), so each entry also reports
+        # packed bytes + the typed side's touched 32-B sectors
+        typed_sectors = {"vector_16B_blocks_stride32B": 2 * nb, "double_int_records_12of16B": nb * 16 // 12,
+                         "subarray3d_fp32_rows1536B": nb}[name]
+        res = {"packed_bytes": nb, "algorithmic_bytes_per_call": 2 * nb,
+               "touched_sector_bytes_per_call": nb + typed_sectors}
         for label, fn, a, b in (("pack", L.msx_pack_dev, typed, packed), ("unpack", L.msx_unpack_dev, packed, typed)):
             ts = []
             for _ in range(3):
@@ -554,7 +561,9 @@ def pack_roofline(L, C, torch, dev, stream):
                 ts.append(e0.elapsed_time(e1) / 10)
             ms = sorted(ts)[1]
             gbs = 2 * nb / ms / 1e6
+            sec = res["touched_sector_bytes_per_call"] / ms / 1e6
             res[label] = {"us": round(ms * 1e3, 1), "GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                          "sector_GB_s": round(sec, 1), "frac_sector": round(sec / HBM_PEAK_GBS, 4),
                           "kernel": KERNEL_OF[name][label]}
             res[label]["pmc_raw_kib"] = pmc_raw(KERNEL_OF[name][label])
         out[name] = res
@@ -579,7 +588,8 @@ def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
         a.random_(0, 256)
         b.random_(0, 256)
     out = {}
-    for mode, name, streams in ((0, "read2", 2), (3, "read1", 1), (1, "write1", 1), (2, "copy_r1w1", 2)):
+    for mode, name, streams in ((0, "read2", 2), (3, "read1", 1), (1, "write1", 1), (2, "copy_r1w1", 2),
+                                (6, "write_16of32B", 0.5), (7, "read_16of32B", 0.5)):
         ts = []
         for _ in range(3):
             for _ in range(2):

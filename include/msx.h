@@ -127,11 +127,16 @@ int msx_tune_variant_count(void);
  * the combines); grid_cap 0 = default. */
 int msx_tune_tree(int mode, int grid_cap);
 const char* msx_tune_variant_name(int variant);
+/* realigning combine for mutually misaligned operands: the cross-lane move of
+ * the `in` chunks, 0 = DPP wave shift (default), 1 = ds_bpermute, 2 = DPP on
+ * the earlier wave grid skewed by one vector (measurement) */
+int msx_tune_shift(int mode);
 /* HBM ceiling probe (measurement only): the default combine's launch geometry
  * with another stream mix over `bytes` per stream (16-B aligned device
  * pointers): mode 0 reads a and b, 1 writes b, 2 copies a -> b, 3 reads a;
  * 4 copies a -> b with the engine's segment-copy kernel (k_copy_segs), 5 with
- * hipMemcpyAsync.
+ * hipMemcpyAsync; 6 writes 16 B of every 32 B of b (gapped store), 7 reads
+ * 16 B of every 32 B of a (gapped load).
  * Stream-ordered; b's contents are unspecified afterwards. */
 int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream);
 /* device allocation for measurements: uncached = the engine windows' memory

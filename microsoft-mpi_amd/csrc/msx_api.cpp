@@ -2413,6 +2413,11 @@ MSX_EXPORT int msx_tune_set(int variant, int grid_cap)
     return MPI_SUCCESS;
 }
 
+MSX_EXPORT int msx_tune_shift(int mode)
+{
+    return shift_tune_set(mode) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
+}
+
 MSX_EXPORT int msx_tune_tree(int mode, int grid_cap)
 {
     return tree_tune_set(mode, grid_cap) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
@@ -2420,7 +2425,7 @@ MSX_EXPORT int msx_tune_tree(int mode, int grid_cap)
 
 MSX_EXPORT int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream)
 {
-    if (mode < 0 || mode > 5 || bytes < 0 || !b || (mode != 1 && !a)) return MPI_ERR_ARG;
+    if (mode < 0 || mode > 7 || bytes < 0 || !b || (mode != 1 && mode != 6 && !a)) return MPI_ERR_ARG;
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
     hipError_t e = launch_probe(mode, a, b, (size_t)bytes, static_cast<hipStream_t>(stream));

@@ -133,6 +133,8 @@ hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size
 // grid_cap 0 = default cap.  Returns 0, or -1 for an invalid setting.
 struct TreeTune { int mode = 0; int grid_cap = 0; };
 int tree_tune_set(int mode, int grid_cap);
+// realigning combine (mutually misaligned operands): 0 = DPP lane shift, 1 = ds_bpermute
+int shift_tune_set(int mode);
 
 // HBM ceiling probe (measurement only, see k_probe): mode 0 reads a and b,
 // 1 writes b, 2 copies a -> b, 3 reads a; `bytes` per stream, 16-B aligned.

@@ -154,7 +154,17 @@ __device__ __forceinline__ u32x4 realign(const u32x4& A, const u32x4& B, unsigne
     return o;
 }
 
-template <int OP, class T, class VT, int BLOCK>
+// Lane i takes lane i+1's word: DPP wave_shl:1 (a VALU operand modifier on
+// the GFX9 family, dpp_ctrl 0x130) or a ds_bpermute through the LDS crossbar
+// (__shfl_down).  Lane 63 gets 0 either way; it loads its own next chunk.
+template <bool DPP>
+__device__ __forceinline__ unsigned from_next_lane(unsigned x)
+{
+    if constexpr (DPP) return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
+    else return __shfl_down(x, 1);
+}
+
+template <int OP, class T, class VT, int BLOCK, bool DPP, bool SKEW = false>
 __global__ __launch_bounds__(BLOCK) void k_combine_shift(const T* __restrict__ in, T* __restrict__ io, size_t head,
                                                          size_t nvec, size_t tail, unsigned s)
 {
@@ -163,22 +173,32 @@ __global__ __launch_bounds__(BLOCK) void k_combine_shift(const T* __restrict__ i
         reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(in + head) - s);   // aligned
     u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
     const size_t bid = (size_t)xcd_tile(blockIdx.x, gridDim.x);
-    const size_t v = 1 + bid * BLOCK + threadIdx.x;
-    const bool live = v + 1 < nvec;
+    // vector v of lane tid: wave spans start on 1-KiB boundaries of `io`'s
+    // vector grid (vector 0 is left idle, not shifted to lane 0: a grid that
+    // started at vector 1 made every wave straddle one more 128-B line per
+    // operand, -12 % at 256 MiB)
+    const size_t v = bid * BLOCK + threadIdx.x + (SKEW ? 1 : 0);   // SKEW: the old grid (measurement)
+    const bool live = v >= 1 && v + 1 < nvec;
     // chunk v+1 is the next lane's chunk v: taken with a lane shuffle, loaded
     // only by the wave's last lane and the last live lane
-    u32x4 a = {0, 0, 0, 0}, y = {0, 0, 0, 0};
+    // The extra chunk of those lanes is loaded together with the other two
+    // operands, not after the shuffle: issued behind the wait for `a` it added
+    // a second memory round trip to every wave (0.79 of the aligned rate).
+    const bool own_next = live && ((threadIdx.x & 63) == 63 || v + 2 >= nvec);
+    u32x4 a = {0, 0, 0, 0}, y = {0, 0, 0, 0}, nx = {0, 0, 0, 0};
     if (live) {
         a = ld<true>(ain + v);
         y = ld<true>(vio + v);
     }
-    issued_together(a, y);
+    if (own_next) nx = ld<true>(ain + v + 1);
+    asm volatile("" : "+v"(a), "+v"(y), "+v"(nx));
+    __builtin_amdgcn_sched_barrier(0);
     u32x4 b;
-    b.x = __shfl_down(a.x, 1);
-    b.y = __shfl_down(a.y, 1);
-    b.z = __shfl_down(a.z, 1);
-    b.w = __shfl_down(a.w, 1);
-    if (live && ((threadIdx.x & 63) == 63 || v + 2 >= nvec)) b = ld<true>(ain + v + 1);
+    b.x = from_next_lane<DPP>(a.x);
+    b.y = from_next_lane<DPP>(a.y);
+    b.z = from_next_lane<DPP>(a.z);
+    b.w = from_next_lane<DPP>(a.w);
+    if (own_next) b = nx;
     if (live) vio[v] = apply_vec<OP, VT>(y, realign(a, b, s));
     // scalar: [0, head + EPV) and [head + (nvec - 1) * EPV, head + nvec * EPV + tail)
     const size_t first = head + EPV, last0 = head + (nvec - 1) * EPV;
@@ -259,6 +279,13 @@ __global__ __launch_bounds__(256) void k_probe(const u32x4* __restrict__ a, u32x
         b[i] = u32x4{key, key ^ (unsigned)i, key, (unsigned)(i >> 32)};
     } else if constexpr (MODE == 2) {
         b[i] = ld<true>(a + i);
+    } else if constexpr (MODE == 6) {
+        // gapped store: 16 B of every 32 B (the 16-B-block vector's unpack)
+        b[2 * i] = u32x4{key, key ^ (unsigned)i, key, (unsigned)(i >> 32)};
+    } else if constexpr (MODE == 7) {
+        // gapped load: 16 B of every 32 B (the same vector's pack)
+        const u32x4 x = ld<true>(a + 2 * i);
+        if ((x.x ^ x.y ^ x.z ^ x.w) == key) b[i] = x;
     } else {
         const u32x4 x = ld<true>(a + i);
         if ((x.x ^ x.y ^ x.z ^ x.w) == key) b[i] = x;
@@ -420,6 +447,10 @@ inline void split(const void* in, const void* io, size_t count, size_t& head, si
     head = h; nvec = rest / epv; tail = rest - nvec * epv;
 }
 
+// k_combine_shift's cross-lane move: 0 = DPP wave_shl:1, 1 = ds_bpermute,
+// 2 = DPP with the previous (one-vector-skewed) wave grid
+int g_shift_mode = 0;
+
 // The realigning path (k_combine_shift): both operands element-aligned but
 // at different offsets from 16-byte alignment, and at least 3 vectors.
 template <class T>
@@ -451,8 +482,15 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
         const size_t sc = (head + tail + 2 * (16 / sizeof(T)) + BLOCK - 1) / BLOCK;
         if (grid < sc) grid = sc;
         if (grid > 0x7fffffffu) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
-                           static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
+        if (g_shift_mode == 0)
+            hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK, true>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
+                               static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
+        else if (g_shift_mode == 2)
+            hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK, true, true>), dim3((unsigned)grid), dim3(BLOCK), 0,
+                               s, static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
+        else
+            hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK, false>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
+                               static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
         return hipGetLastError();
     }
     split<T>(in, io, count, head, nvec, tail);
@@ -614,6 +652,13 @@ hipError_t dispatch_loc(Kind k, const void* in, void* io, size_t n, hipStream_t 
 
 TreeTune g_tree_tune;
 
+int shift_tune_set(int mode)
+{
+    if (mode < 0 || mode > 2) return -1;
+    g_shift_mode = mode;
+    return 0;
+}
+
 int tree_tune_set(int mode, int grid_cap)
 {
     if (mode < 0 || mode > 8 || grid_cap < 0) return -1;
@@ -774,10 +819,11 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
 
 hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s)
 {
-    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 5) return hipErrorInvalidValue;
+    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 7) return hipErrorInvalidValue;
     if (mode == 4) return launch_copy_segs(&a, &b, &bytes, 1, false, s);      // the engine's copy kernel
     if (mode == 5) return hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, s);   // HIP's blit
-    const size_t nvec = bytes / 16;
+    // modes 6 / 7 touch every other 16-B vector of `bytes`: nvec = bytes / 32
+    const size_t nvec = (mode >= 6) ? bytes / 32 : bytes / 16;
     const size_t grid = (nvec + 255) / 256;
     if (grid == 0) return hipSuccess;
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
@@ -788,6 +834,8 @@ hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStrea
     case 0: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
     case 1: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
     case 2: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
+    case 6: hipLaunchKernelGGL(k_probe<6>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
+    case 7: hipLaunchKernelGGL(k_probe<7>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
     default: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
     }
     return hipGetLastError();

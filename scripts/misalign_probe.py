@@ -19,9 +19,11 @@ sp = ctypes.c_void_p(stream.cuda_stream)
 NB = 256 << 20
 a = torch.empty(NB + 64, dtype=torch.uint8, device="cuda")
 b = torch.empty(NB + 64, dtype=torch.uint8, device="cuda")
-a.view(torch.float32)[:].uniform_(-1, 1) if False else None
+a.view(torch.float32)[:].uniform_(-1, 1)
+b.view(torch.float32)[:].uniform_(-1, 1)
 torch.cuda.synchronize()
 out = {}
+MODES = {"dpp": 0, "bpermute": 1, "dpp_skewed_grid": 2}
 
 
 def timed(fn, reps=10):
@@ -44,6 +46,12 @@ for dtn, esz in (("MPI_FLOAT", 4), ("MPI_DOUBLE", 8), ("MPI_INT8_T", 1), ("MPI_I
         if oa % esz or ob % esz:
             continue
         n = (NB - 16) // esz
-        ms = timed(lambda: L.msx_reduce_local_dev(a.data_ptr() + oa, b.data_ptr() + ob, n, dt, C.MPI_SUM, sp))
-        out[f"{dtn}/in+{oa}/io+{ob}"] = {"us": round(ms * 1e3, 1), "GB_s": round(3 * n * esz / ms / 1e6, 1)}
+        for mname, mode in MODES.items():     # the realigning kernel's cross-lane move, A/B in one process
+            if (oa - ob) % 16 == 0 and mode:
+                continue                       # aligned pairs do not use it
+            L.msx_tune_shift(mode)
+            ms = timed(lambda: L.msx_reduce_local_dev(a.data_ptr() + oa, b.data_ptr() + ob, n, dt, C.MPI_SUM, sp))
+            key = f"{dtn}/in+{oa}/io+{ob}" + ("" if (oa - ob) % 16 == 0 else f"/{mname}")
+            out[key] = {"us": round(ms * 1e3, 1), "GB_s": round(3 * n * esz / ms / 1e6, 1)}
+L.msx_tune_shift(0)
 print(json.dumps(out), flush=True)

@@ -26,5 +26,7 @@ def test_op_table_from_c_on_device_buffers():
     pr = subprocess.run([EXE], capture_output=True, text=True, timeout=240, env=env)
     assert pr.returncode == 0, (pr.stdout + pr.stderr)[-3000:]
     assert pr.stdout.startswith("OK"), pr.stdout
+    import oracle
+    from _cases import legal_pairs
     legal = int(pr.stdout.split()[1])
-    assert legal >= 400, pr.stdout        # every legal (op, predefined type) pair
+    assert legal == len(legal_pairs(oracle)), pr.stdout     # every legal (op, predefined type) pair
