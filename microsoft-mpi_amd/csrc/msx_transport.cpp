@@ -1338,6 +1338,21 @@ Bounce& engine_bounce(int i)
     return b[i];
 }
 
+// Whether the tree workgroups of a small flag-synchronised call may spin on
+// the peers' flags themselves (MSX_SPIN_TREE=1, the round-2 design: push and
+// tree in one launch).  Default off: ONE workgroup of the push launch waits
+// (k_push_wait) and the tree follows in stream order, so no call ever parks a
+// grid of spinning workgroups on the GPU whose progress depends on another
+// process's kernel being scheduled.
+bool spin_tree_allowed()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_SPIN_TREE");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
+
 // The barrier-free small allreduce pushes and reduces in one launch
 // (MSX_FUSED_PUSH=0: a separate push launch first).
 bool fused_push()
@@ -1889,7 +1904,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             // workgroup of the push launch waits, the tree follows on the
             // stream -- thousands of spinning workgroups per rank starved the
             // other ranks' pushes on a shared GPU until the 20 s bound.
-            const bool spin_tree = nbytes <= ((size_t)256 << 10);
+            const bool spin_tree = spin_tree_allowed() && nbytes <= ((size_t)256 << 10);
             const bool fuse = spin_tree && want && fused_push() && !sg.src.empty() && disjoint;
             unsigned* counter = nullptr;
             if (rc == MPI_SUCCESS && !sg.src.empty()) {
@@ -2598,7 +2613,7 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
         const char* cur_r = exclusive ? nullptr : srcv; // current result (have)
         bool same = !exclusive;                         // partial and result hold one value
         char* outv = dst_dev ? static_cast<char*>(dstv) : dst_stage;
-        const bool fuse = fused_push() && bytes <= kScanFuseMax;
+        const bool fuse = spin_tree_allowed() && fused_push() && bytes <= kScanFuseMax;
         int step = 0;
         for (int mask = 1; mask < p && rc == MPI_SUCCESS; mask <<= 1, ++step) {
             const int dst = me ^ mask;
