@@ -35,6 +35,7 @@ sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 N_ELEM = 64 << 20              # 256 MiB of fp32 per operand (config 2)
 BYTES_PER_ELEM = 12            # 2 x 4 B read + 4 B write
+HOST_SIZES = (8, 4 << 10, 64 << 10, 1 << 20, 16 << 20, 256 << 20)   # host-operand crossover table
 
 
 def parse():
@@ -302,6 +303,19 @@ def cpu_baseline(seconds, elems):
         out["all_cores"] = {"value": round(n * BYTES_PER_ELEM / tN / 2**30, 3), "unit": "GiB/s", "cores": cores,
                             "payload_GiB_s": round(n * 4 / tN / 2**30, 3), "ms_per_call": round(tN * 1e3, 3),
                             "sample": f"median of {kN} calls after 3 warm-ups, {cores} threads"}
+    # the same loop by operand size (the host-operand crossover table beside
+    # host_path.pageable_by_size_fp32_sum); one thread and every core
+    by = {}
+    for nb in HOST_SIZES:
+        m = max(1, nb // 4)
+        x, y = a[:m].copy(), b[:m].copy()
+        t1, _ = _median_rate(lambda: oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, x, y), 0, 0.2)
+        row = {"us_1core": round(t1 * 1e6, 3)}
+        if cores > 1 and nb >= (1 << 20):
+            tN, _ = _median_rate(lambda: oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, x, y, nthreads=cores), 0, 0.2)
+            row[f"us_{cores}cores"] = round(tN * 1e6, 3)
+        by[str(nb)] = row
+    out["by_size_fp32_sum"] = by
     return out
 
 
@@ -866,6 +880,28 @@ def main():
                            "payload_GiB_s": round(n * 4 / dt_h / 2**30, 2),
                            "traffic_GiB_s": round(n * BYTES_PER_ELEM / dt_h / 2**30, 2)}
         L.msx_set_host_mode(0)
+        # crossover table: pageable host operands by size, the
+        # default host path (bounce buffers up to 256 KiB, then pinned for the
+        # call); cpu_baseline.by_size times the CPU loop on the same sizes
+        import numpy as np
+        by = {}
+        for nb in HOST_SIZES:
+            m = max(1, nb // 4)
+            ha = np.random.default_rng(1).uniform(-1, 1, m).astype(np.float32)
+            hb = np.random.default_rng(2).uniform(-1, 1, m).astype(np.float32)
+            reps = 200 if nb <= (1 << 20) else (20 if nb <= (16 << 20) else 5)
+            for _ in range(3):
+                L.MPI_Reduce_local(ha.ctypes.data, hb.ctypes.data, m, C.MPI_FLOAT, C.MPI_SUM)
+            ts = []
+            for _ in range(reps):
+                t1 = time.perf_counter()
+                rc = L.MPI_Reduce_local(ha.ctypes.data, hb.ctypes.data, m, C.MPI_FLOAT, C.MPI_SUM)
+                ts.append(time.perf_counter() - t1)
+                assert rc == 0, msx.last_error()
+            ts.sort()
+            by[str(nb)] = {"us": round(ts[len(ts) // 2] * 1e6, 2),
+                           "payload_GiB_s": round(nb / ts[len(ts) // 2] / 2**30, 3)}
+        host["pageable_by_size_fp32_sum"] = by
         # blocking MPI_Reduce_local on device buffers (adds launch + sync per call)
         reps, t1 = 10, time.perf_counter()
         for _ in range(reps):
