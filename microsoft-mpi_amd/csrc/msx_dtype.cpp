@@ -1041,7 +1041,10 @@ Dtype* dtype_from_blob(const int64_t* b, int64_t avail)
 {
     if (avail >= 10 && b[3] == -2) {
         const int64_t lim = (int64_t)1 << 40;
-        if (b[5] <= 0 || b[7] <= 0 || b[9] <= 1 || b[7] > lim || b[9] > lim / b[7] || b[7] * b[9] * b[5] != b[0])
+        // every product bounded before it is formed (the blob comes from
+        // another process): b[7] * b[9] <= 2^40, then rlen <= 2^62 / that
+        if (b[5] <= 0 || b[7] <= 0 || b[9] <= 1 || b[7] > lim || b[9] > lim / b[7] ||
+            b[5] > ((int64_t)1 << 62) / (b[7] * b[9]) || b[7] * b[9] * b[5] != b[0])
             return nullptr;
         auto* t = new Dtype();
         t->size = b[0];
@@ -1059,7 +1062,9 @@ Dtype* dtype_from_blob(const int64_t* b, int64_t avail)
         return t;
     }
     if (avail >= 8 && b[3] == -1) {
-        if (b[7] <= 0 || b[5] <= 0 || b[7] > ((int64_t)1 << 40) || b[7] * b[5] != b[0]) return nullptr;
+        if (b[7] <= 0 || b[5] <= 0 || b[7] > ((int64_t)1 << 40) || b[5] > ((int64_t)1 << 62) / b[7] ||
+            b[7] * b[5] != b[0])
+            return nullptr;
         auto* t = new Dtype();
         t->size = b[0];
         t->extent = b[1];

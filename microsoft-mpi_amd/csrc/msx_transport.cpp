@@ -1261,10 +1261,21 @@ constexpr size_t kFlagBytes = 64 << 10;
 // pieces (MSX_RMA_BYTES, default 512 MiB), below the 2 GiB IPC limit.  256 MiB lock / PSCW accumulates, 2 ranks on one MI355X
 // (profiles/r02/rma_area_*.json): 1.27 ms with 64 MiB, 0.66 ms with 256 MiB,
 // 0.53 ms with 512 MiB (= the fence epoch's 0.54 ms).
+// The area belongs to the communicator's transport: every communicator with a
+// window holds one per rank.  Without MSX_RMA_BYTES the default is capped per
+// GPU: 512 MiB divided by the ranks of the job that share this GPU (8 ranks on
+// one GPU: 64 MiB each), at least 64 MiB.
 size_t rma_bytes()
 {
     static size_t v = [] {
         size_t b = (size_t)512 << 20;
+        const char* ws = getenv("MSX_SIZE");
+        if (!ws) ws = getenv("WORLD_SIZE");
+        const int ndev = device_count_noinit();
+        if (ws && ndev > 0) {
+            const size_t share = ((size_t)std::max(1, atoi(ws)) + (size_t)ndev - 1) / (size_t)ndev;
+            b = std::max(b / share, (size_t)64 << 20);
+        }
         if (const char* e = getenv("MSX_RMA_BYTES")) b = (size_t)atoll(e);
         const size_t cap = ((size_t)2 << 30) - ((size_t)1 << 20);      // IPC mapping limit
         b = std::min(b, cap);
@@ -1429,8 +1440,11 @@ int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
         const BufInfo bs = classify(src), bd = classify(dst);
         int cur = -1;
         (void)hipGetDevice(&cur);
-        // both on this GPU (a peer's window or another GPU's buffer: the blit)
-        if (bs.place == Place::Device && bd.place == Place::Device && bs.device == cur && bd.device == cur) {
+        // both on this GPU (a peer's window or another GPU's buffer: the blit),
+        // 16-byte aligned (otherwise the kernel falls back to one byte per
+        // lane, far below the blit)
+        if (bs.place == Place::Device && bd.place == Place::Device && bs.device == cur && bd.device == cur &&
+            (((uintptr_t)bs.dev | (uintptr_t)bd.dev) & 15) == 0) {
             const void* ps = bs.dev;
             void* pd = bd.dev;
             hipError_t e = launch_copy_segs(&ps, &pd, &bytes, 1, sys_fences(), s);
