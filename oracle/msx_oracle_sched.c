@@ -206,8 +206,16 @@ int oracle_reduce_scatter(MPI_Op op, MPI_Datatype dt, int p, const int* recvcoun
     int rc = MPI_SUCCESS;
     if (total == 0) { free(disps); return MPI_SUCCESS; }
     const int64_t bytes = total * esz;
-    /* :1705 nbytes = (unsigned)(total_count * type_size); the NBC builder
-     * gates on the same product, cbBuffer (:3201) */
+    /* :1705 nbytes = (unsigned)(total_count * type_size).  MPI_Ireduce_scatter
+     * takes this same simulation: IreduceScatterBuildTaskList gates on the
+     * same product (cbBuffer, :3201 -- type size, unlike the allreduce /
+     * reduce NBC gates), its short list (:1987-2406) has the blocking fold,
+     * newcnts/newdisps merge, BinomialChildBuilderDescending = mask pof2/2..1
+     * (tasks.h:448-469), TrimmedToOriginalRankOdd = newdst*2+1 / newdst+rem
+     * (:1975-1981) and keep-lower-half rule, and its long list (:2412-2676)
+     * walks src = rank-1, rank-2, ... like the blocking pairwise loop; for
+     * the (commutative) builtin ops NbcTask::ExecuteReduce ignores rightOrder
+     * and calls Uop(recv, reduce) (tasks.cpp:665-686), the blocking roles. */
     const uint32_t nbytes = (uint32_t)((uint64_t)total * (uint64_t)oracle_type_size(dt));
     char** res = (char**)calloc((size_t)p, sizeof(char*));
     char** tmp = (char**)calloc((size_t)p, sizeof(char*));
