@@ -170,6 +170,33 @@ def test_no_gpu_fails_loudly_not_silently(msxlib):
                                        None) == C.MPI_ERR_OTHER
 
 
+def test_config1_cpu_plumbing_and_oracle(msxlib):
+    """BASELINE configs[0] ("MPI_Reduce_local MPI_SUM MPI_INT, 1 MiB, single
+    process on CPU: plumbing + bit-exact oracle, no GPU").  Plumbing: MPI_Init,
+    the reference's checks and the (op, type) table pass for the 1 MiB call,
+    which then reaches the device dispatch and, with no GPU, returns
+    MPI_ERR_OTHER without touching inoutbuf -- the product has no CPU combine.
+    Oracle: the C restatement of Op<int>::Sum (op.cpp:42-52) on the same
+    1 MiB equals two's-complement wrap arithmetic bit for bit (the survey's
+    recorded int32 SUM answer over 1 MiB is test_oracle's known-answer case).
+    On the GPU box the same call runs through the product: test_gpu_local's
+    examples/reduce_local_demo.c test."""
+    n = (1 << 20) // 4
+    rng = np.random.default_rng(20)
+    a = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+    b0 = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+    b = b0.copy()
+    assert msxlib.msx_op_check(C.MPI_SUM, C.MPI_INT) == 0
+    if msxlib.msx_device_count() == 0:
+        rc = msxlib.MPI_Reduce_local(a.ctypes.data, b.ctypes.data, n, C.MPI_INT, C.MPI_SUM)
+        assert rc == C.MPI_ERR_OTHER and "no usable MI355X" in msx.last_error()
+        assert np.array_equal(b, b0)
+    want = ((a.astype(np.int64) + b0.astype(np.int64) + 2**31) % 2**32 - 2**31).astype(np.int32)
+    got = b0.copy()
+    assert oracle.reduce_local(C.MPI_SUM, C.MPI_INT, a, got) == 0
+    assert np.array_equal(got, want)
+
+
 def test_op_table_entries_without_gpu(msxlib):
     """msx_op_table / msx_op_<op> (the MPIR_Op_table replacement, op.cpp:618-622,
     703-1923): lookups, the MPI_User_function shape, op_errno semantics
