@@ -24,16 +24,26 @@ SSE_BIN(mul_f, float, "mulss")
 SSE_BIN(add_d, double, "addsd")
 SSE_BIN(sub_d, double, "subsd")
 SSE_BIN(mul_d, double, "mulsd")
+/* MAXSS x, y = (x > y) ? x : y and MINSS x, y = (x < y) ? x : y: the
+ * Windows max/min macros op.cpp:26,38 apply to (inout, in) */
+SSE_BIN(max_f, float, "maxss")
+SSE_BIN(min_f, float, "minss")
+SSE_BIN(max_d, double, "maxsd")
+SSE_BIN(min_d, double, "minsd")
 
-/* inout[i] = inout[i] op in[i] (op 0 = SUM, 1 = PROD) */
+/* inout[i] = inout[i] op in[i] (op 0 = SUM, 1 = PROD, 2 = MAX, 3 = MIN) */
 void sse_f32(int op, const float* in, float* inout, int64_t n)
 {
-    for (int64_t i = 0; i < n; ++i) inout[i] = op ? mul_f(inout[i], in[i]) : add_f(inout[i], in[i]);
+    for (int64_t i = 0; i < n; ++i)
+        inout[i] = op == 0 ? add_f(inout[i], in[i]) : op == 1 ? mul_f(inout[i], in[i])
+                 : op == 2 ? max_f(inout[i], in[i]) : min_f(inout[i], in[i]);
 }
 
 void sse_f64(int op, const double* in, double* inout, int64_t n)
 {
-    for (int64_t i = 0; i < n; ++i) inout[i] = op ? mul_d(inout[i], in[i]) : add_d(inout[i], in[i]);
+    for (int64_t i = 0; i < n; ++i)
+        inout[i] = op == 0 ? add_d(inout[i], in[i]) : op == 1 ? mul_d(inout[i], in[i])
+                 : op == 2 ? max_d(inout[i], in[i]) : min_d(inout[i], in[i]);
 }
 
 /* complex<T>::operator*= (op.cpp:294-303), pairs (re, im):

@@ -8,8 +8,9 @@ X86_OP: first operand's NaN quieted, else the second's, else the default NaN
 (msx_dev_ops.h), checked bit for bit against the oracle on the GPU
 (test_gpu_local.py).  A rule shared by kernel and oracle could still be wrong
 in both; this test pins it to the silicon: tests/c/x86_sse_probe.c executes
-addss/subss/mulss/addsd/subsd/mulsd with op.cpp's operand order fixed by
-inline assembly, and every special-value pair (signed quiet and signalling
+addss/subss/mulss/addsd/subsd/mulsd (and maxss/minss/maxsd/minsd, whose
+definition is the Windows max/min macro of op.cpp:26,38) with op.cpp's
+operand order fixed by inline assembly, and every special-value pair (signed quiet and signalling
 NaNs with payloads, infinities, zeros, denormals, finite values) must give
 the oracle's bits.  What stays unpinned: the operand order MSVC emitted for
 the commutative `+`/`*`."""
@@ -57,25 +58,28 @@ def _pairs(vals, udt):
     return np.array(x, udt), np.array(y, udt)
 
 
-@pytest.mark.parametrize("op", ["MPI_SUM", "MPI_PROD"])
+OPNUM = {"MPI_SUM": 0, "MPI_PROD": 1, "MPI_MAX": 2, "MPI_MIN": 3}
+
+
+@pytest.mark.parametrize("op", list(OPNUM))
 @pytest.mark.parametrize("width", [32, 64])
-def test_real_sum_prod_nan_payloads_match_sse(sse, op, width):
+def test_real_ops_nan_payloads_match_sse(sse, op, width):
     vals, udt, fdt = (F32, np.uint32, np.float32) if width == 32 else (F64, np.uint64, np.float64)
     inout_bits, in_bits = _pairs(vals, udt)          # every (inout, in) pair, both orders
     dt = C.MPI_FLOAT if width == 32 else C.MPI_DOUBLE
     want = inout_bits.copy()
     fn = sse.sse_f32 if width == 32 else sse.sse_f64
-    fn(1 if op == "MPI_PROD" else 0, in_bits.ctypes.data, want.ctypes.data, want.size)
+    fn(OPNUM[op], in_bits.ctypes.data, want.ctypes.data, want.size)
     got = inout_bits.copy().view(fdt)
     assert oracle.reduce_local(getattr(C, op), dt, in_bits.view(fdt), got) == 0
     bad = np.nonzero(got.view(udt) != want)[0]
     assert bad.size == 0, [(hex(inout_bits[i]), hex(in_bits[i]), hex(got.view(udt)[i]), hex(want[i]))
                            for i in bad[:8]]
     # the table really exercises the rule: NaN results from NaN operands and
-    # default NaNs from invalid operations on numbers
+    # default NaNs from invalid operations on numbers (MAX/MIN: NaN in `in`)
     isnan = (want & (0x7F800000 if width == 32 else 0x7FF0000000000000)) == \
         (0x7F800000 if width == 32 else 0x7FF0000000000000)
-    assert isnan.sum() > len(vals) * 8
+    assert isnan.sum() > len(vals) * (6 if op in ("MPI_MAX", "MPI_MIN") else 8)
 
 
 @pytest.mark.parametrize("width", [32, 64])
