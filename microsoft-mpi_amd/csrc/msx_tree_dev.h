@@ -243,7 +243,22 @@ struct TreeArgs {
     unsigned* done_counter;       // kCountWords block: [0] count_done, [1] launches done
     unsigned done_launches;
     PostFlags done_flags;
+    // tile order (tuning only, msx_tune_tree modes 9-11): 0 = XCD-contiguous
+    // eighths, > 0 = XCD x owns interleaved runs of xg consecutive tiles,
+    // -1 = dispatch order
+    int xg;
 };
+
+// Workgroup b of nb -> tile under TreeArgs::xg (a bijection on [0, nb)).
+__device__ __forceinline__ size_t tree_tile(int xg, unsigned b, unsigned nb)
+{
+    if (xg == 0) return xcd_tile(b, nb);
+    if (xg < 0) return b;
+    const unsigned g = (unsigned)xg, full = (nb / (8u * g)) * (8u * g);
+    if (b >= full) return b;
+    const unsigned x = b & 7, j = b >> 3;
+    return ((size_t)(j / g) * 8 + x) * g + (j % g);
+}
 
 // End of a tree workgroup when the launch posts result-ready flags: the
 // threadFenceReduction pattern of push_post_body, extended over the launches
@@ -505,7 +520,7 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
         nb -= a.npush;
     }
     const size_t stride = (size_t)nb * BLOCK;
-    const size_t bid = xcd_tile(b, nb);      // XCD-contiguous (see combine_body)
+    const size_t bid = tree_tile(a.xg, b, nb);   // XCD-contiguous by default (see combine_body)
     if (a.wait_flags && !arrival_wait(a)) return;
     if (a.sys) acquire_system();
     if constexpr (NL > 0) {

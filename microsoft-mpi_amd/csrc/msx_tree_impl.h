@@ -15,7 +15,7 @@ constexpr int kTreeGridCap = 4096;          // generic kernel: grid-stride beyon
 constexpr int kFixedGridCap = 1 << 20;      // compile-time-source kernel: one tile per workgroup
 
 template <int OP, class T, class VT, bool UPFRONT = false, bool NT = false, int NL = 0, int U = 1,
-          bool CHAIN = false>
+          bool CHAIN = false, int BLOCK = kTreeBlock>
 hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     bool ok = ((uintptr_t)out & 15) == 0;
@@ -25,14 +25,14 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
     const size_t epv = 16 / ES;
     const size_t nvec = count / epv, tail = count - nvec * epv;
     const size_t work = ok ? (nvec + U - 1) / U + tail : count;
-    size_t grid = (work + kTreeBlock - 1) / kTreeBlock;
+    size_t grid = (work + BLOCK - 1) / BLOCK;
     const size_t cap = g_tree_tune.grid_cap > 0 ? (size_t)g_tree_tune.grid_cap
                                                 : (size_t)(NL > 0 ? kFixedGridCap : kTreeGridCap);
     if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
     grid += a.npush;                         // fused push workgroups come first
-    hipLaunchKernelGGL((k_tree<OP, T, VT, kTreeBlock, UPFRONT, NT, NL, U, CHAIN>), dim3((unsigned)grid),
-                       dim3(kTreeBlock), 0, s, a, static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
+    hipLaunchKernelGGL((k_tree<OP, T, VT, BLOCK, UPFRONT, NT, NL, U, CHAIN>), dim3((unsigned)grid),
+                       dim3(BLOCK), 0, s, a, static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
     return hipGetLastError();
 }
 

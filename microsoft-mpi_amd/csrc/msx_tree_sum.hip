@@ -10,7 +10,11 @@ template hipError_t tree_dispatch<O_PROD>(Kind, const dev::TreeArgs&, int, void*
 // loads up front / up front + non-temporal / interleaved + non-temporal,
 // 4/5/6 the compile-time-source kernel with 1/2/4 vectors per lane, 7 = 5 with
 // non-temporal loads, 8 the generic kernel as it is (the dispatch before the
-// compile-time-source kernel); mode 0 (not routed here) is the default dispatch.
+// compile-time-source kernel); 9 = 4 with the tile order of the grid_cap
+// argument (TreeArgs::xg: 0 XCD-contiguous, > 0 runs of that many tiles per
+// XCD, -1 passed as 0x7fffffff: dispatch order, no grid cap in this mode),
+// 10/11 = 4 with 512- / 1024-lane workgroups; mode 0 (not routed here) is the
+// default dispatch.
 hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
 {
     switch (mode) {
@@ -22,6 +26,21 @@ hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out
     case 6: return run_tree_auto<O_SUM, float, float, 4, false>(a, ns, out, n, s);
     case 7: return run_tree_auto<O_SUM, float, float, 2, true>(a, ns, out, n, s);
     case 8: return run_tree<O_SUM, float, float>(a, ns, out, n, s);
+    case 9: {
+        TreeArgs b = a;
+        b.xg = g_tree_tune.grid_cap == 0x7fffffff ? -1 : g_tree_tune.grid_cap;
+        const int cap = g_tree_tune.grid_cap;
+        g_tree_tune.grid_cap = 0;
+        const hipError_t e = run_tree_auto<O_SUM, float, float, 1, false>(b, ns, out, n, s);
+        g_tree_tune.grid_cap = cap;
+        return e;
+    }
+    case 10:
+    case 11:
+        if (!a.chain && a.pairmask == 0 && a.nleaves == a.P && a.P == 8)
+            return mode == 10 ? run_tree<O_SUM, float, float, false, false, 8, 1, false, 512>(a, ns, out, n, s)
+                              : run_tree<O_SUM, float, float, false, false, 8, 1, false, 1024>(a, ns, out, n, s);
+        return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
     }
 }
