@@ -59,12 +59,13 @@ def parse():
 
 def run_collectives_child(world, rank, local, scale, transport="ipc"):
     """c3-c5 in a child MPI process per rank (isolated from the headline line).
-    transport "ipc": IPC windows + xGMI remote writes; "rccl": RCCL send/recv."""
+    transport "ipc": IPC windows + xGMI remote writes; "rccl": RCCL send/recv;
+    "rccl_native": RCCL's own collectives where the (op, type) pair maps."""
     import subprocess
     import tempfile
     out = os.path.join(tempfile.gettempdir(), f"msx_coll_{transport}_{os.environ.get('MASTER_PORT', '0')}.json")
     env = dict(os.environ)
-    off = 113 if transport == "ipc" else 127
+    off = {"ipc": 113, "rccl": 127, "rccl_native": 139}[transport]
     env.update({"MSX_SIZE": str(world), "MSX_RANK": str(rank), "MSX_DEVICE": str(local),
                 "MSX_TRANSPORT": transport,
                 "MSX_BOOTSTRAP_ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
@@ -835,7 +836,7 @@ def main():
 
     # N > 1: the collective configs c3-c5 in child MPI processes (not part of
     # `value`); each rank reports whether its child succeeded.
-    coll = coll_rccl = rccl_native = None
+    coll = coll_rccl = coll_native = rccl_native = None
     distinct = torch.cuda.device_count() >= world      # one GPU per rank (RCCL needs it)
     if world > 1 and not args.no_collectives:
         def collect(transport):
@@ -851,6 +852,11 @@ def main():
         coll = collect("ipc")
         if distinct:
             coll_rccl = collect("rccl")
+            # this library's MPI calls on RCCL's own collectives (MSX_TRANSPORT=
+            # rccl_native: ncclAllReduce / ncclReduce / ncclReduceScatter where
+            # the pair maps, RCCL order; the harness's integer-valued inputs
+            # make every order exact, so `correct` still checks in full)
+            coll_native = collect("rccl_native")
             mine = rccl_native_allreduce(world, rank, local, args.coll_scale)
             ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -972,11 +978,14 @@ def main():
                 sm["error"] = c["error"]
             return sm
         if coll is not None or coll_rccl is not None:
-            out["collectives_summary"] = {"ipc": summarize(coll), "rccl": summarize(coll_rccl)}
+            out["collectives_summary"] = {"ipc": summarize(coll), "rccl": summarize(coll_rccl),
+                                          "rccl_native": summarize(coll_native)}
         if coll is not None:
             out["collectives"] = coll
         if coll_rccl is not None:
             out["collectives_rccl_transport"] = coll_rccl
+        if coll_native is not None:
+            out["collectives_rccl_native_transport"] = coll_native
         if rccl_native is not None:
             out["rccl_native_allreduce_f32"] = rccl_native
         if per_op is not None:

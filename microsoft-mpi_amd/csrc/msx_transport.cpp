@@ -1524,6 +1524,10 @@ struct RcclApi {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) err = nullptr;
+    // RCCL's own collectives (MSX_TRANSPORT=rccl_native)
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclReduce) reduce = nullptr;
+    decltype(&ncclReduceScatter) reduce_scatter = nullptr;
     bool ok = false;
 };
 
@@ -1542,6 +1546,9 @@ const RcclApi* rccl_api()
         r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
         r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
         r.err = reinterpret_cast<decltype(r.err)>(dlsym(h, "ncclGetErrorString"));
+        r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
+        r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(h, "ncclReduce"));
+        r.reduce_scatter = reinterpret_cast<decltype(r.reduce_scatter)>(dlsym(h, "ncclReduceScatter"));
         r.ok = r.get_id && r.init_rank && r.destroy && r.send && r.recv && r.group_start && r.group_end && r.err;
         return r;
     }();
@@ -1552,9 +1559,48 @@ bool rccl_requested()
 {
     static const bool v = [] {
         const char* e = getenv("MSX_TRANSPORT");
-        return e && strcmp(e, "rccl") == 0;
+        return e && (strcmp(e, "rccl") == 0 || strcmp(e, "rccl_native") == 0);
     }();
     return v;
+}
+
+// MSX_TRANSPORT=rccl_native: (op, type) pairs that map onto RCCL's reductions
+// run as ncclAllReduce / ncclReduce / ncclReduceScatter on the user's device
+// buffers -- RCCL's ring/tree association, NOT the reference's: integer
+// results are identical (two's-complement wrap), fp32/fp64 SUM and PROD agree
+// within |y - y_ref| <= 2(p-1) 2^-p_mant sum_r |x_r|, MAX and
+// MIN agree except where NaN / signed-zero ties decide.  Every other pair,
+// host operands and ragged reduce_scatter counts keep the reference-order
+// trees on the RCCL send/recv plane.
+bool rccl_native_requested()
+{
+    static const bool v = [] {
+        const char* e = getenv("MSX_TRANSPORT");
+        return e && strcmp(e, "rccl_native") == 0;
+    }();
+    return v;
+}
+
+bool rccl_map(int opidx, Kind k, ncclRedOp_t* op, ncclDataType_t* t)
+{
+    switch (opidx) {
+    case O_SUM: *op = ncclSum; break;
+    case O_PROD: *op = ncclProd; break;
+    case O_MAX: *op = ncclMax; break;
+    case O_MIN: *op = ncclMin; break;
+    default: return false;
+    }
+    switch (k) {
+    case K_I8: *t = ncclInt8; return true;
+    case K_U8: *t = ncclUint8; return true;
+    case K_I32: *t = ncclInt32; return true;
+    case K_U32: *t = ncclUint32; return true;
+    case K_I64: *t = ncclInt64; return true;
+    case K_U64: *t = ncclUint64; return true;
+    case K_F32: *t = ncclFloat32; return true;
+    case K_F64: *t = ncclFloat64; return true;
+    default: return false;
+    }
 }
 
 std::map<Transport*, ncclComm_t> g_rccl_comms;
@@ -1639,6 +1685,32 @@ int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf,
     const char* src = static_cast<const char*>(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf);
     char* dst = static_cast<char*>(recvbuf);
     const bool want = (root < 0 || root == me);
+    ncclRedOp_t nop;
+    ncclDataType_t nty;
+    const RcclApi* api = rccl_api();
+    if (rccl_native_requested() && rccl_map(op.opidx, k, &nop, &nty) &&
+        (root < 0 ? api->all_reduce != nullptr : api->reduce != nullptr)) {
+        // every rank decides alike: the pair and the buffers' placement
+        // (agreed, since one rank with a host operand must not leave the others
+        // in an RCCL collective alone)
+        const int mine_dev = classify(src).place == Place::Device && (!want || classify(dst).place == Place::Device);
+        std::vector<int> all((size_t)p);
+        int rc = tp->allgather(&mine_dev, sizeof(int), all.data());
+        if (rc != MPI_SUCCESS) return rc;
+        bool all_dev = true;
+        for (int v : all) all_dev = all_dev && v;
+        if (all_dev) {
+            ncclResult_t r = root < 0 ? api->all_reduce(src, dst, count, nty, nop, comm, s)
+                                      : api->reduce(src, want ? static_cast<void*>(dst) : const_cast<char*>(src), count,
+                                                    nty, nop, root, comm, s);
+            trace("rccl native %s: count=%zu rc=%d", root < 0 ? "allreduce" : "reduce", count, (int)r);
+            if (r != ncclSuccess) {
+                set_error("%s: %s", root < 0 ? "ncclAllReduce" : "ncclReduce", api->err(r));
+                return MPI_ERR_OTHER;
+            }
+            return sync_stream(s, root < 0 ? "allreduce" : "reduce");
+        }
+    }
     const bool is_reduce = root >= 0;
     const int gate = gate_type_size(dt, nbc);
     const int algo = is_reduce ? reduce_algo(p, count, gate, true) : allreduce_algo(p, count, gate, true);
@@ -1742,6 +1814,34 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
     const char* src = static_cast<const char*>(in_place ? recvbuf : sendbuf);
     const Kind k = type_info(dt)->kind;
     hipStream_t s = tp->stream();
+    ncclRedOp_t nop;
+    ncclDataType_t nty;
+    const RcclApi* api = rccl_api();
+    if (rccl_native_requested() && api->reduce_scatter && rccl_map(op.opidx, k, &nop, &nty) &&
+        maxcnt * (size_t)p == total) {
+        // equal blocks (recvcounts are the same on every rank by MPI rule):
+        // ncclReduceScatter; in place, my block moves to recvbuf[0]
+        const int mine_dev = classify(src).place == Place::Device && classify(recvbuf).place == Place::Device;
+        std::vector<int> all((size_t)p);
+        int rc = tp->allgather(&mine_dev, sizeof(int), all.data());
+        if (rc != MPI_SUCCESS) return rc;
+        bool all_dev = true;
+        for (int v : all) all_dev = all_dev && v;
+        if (all_dev) {
+            void* out = recvbuf;
+            char* tmp = nullptr;
+            if (in_place && me != 0 && maxcnt) {
+                tmp = dev_scratch(maxcnt * esz);      // RCCL's in-place form wants recvbuf + rank*count
+                if (!tmp) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+                out = tmp;
+            }
+            ncclResult_t r = api->reduce_scatter(src, out, maxcnt, nty, nop, comm, s);
+            trace("rccl native reduce_scatter: count=%zu rc=%d", maxcnt, (int)r);
+            if (r != ncclSuccess) { set_error("ncclReduceScatter: %s", api->err(r)); return MPI_ERR_OTHER; }
+            if (tmp) rc = copy_async(recvbuf, tmp, maxcnt * esz, s);
+            return rc == MPI_SUCCESS ? sync_stream(s, "reduce_scatter") : rc;
+        }
+    }
     size_t qe = (chunk_bytes() / (size_t)p) / esz;
     qe -= qe % 16;
     const int algo = reduce_scatter_algo(p, total, gate_type_size(dt, false), op.commutative);
@@ -3607,7 +3707,8 @@ int engine_peer_write_probe(Comm* c, size_t bytes, int reps, double* seconds, in
 const char* engine_transport_name(Transport* tp)
 {
     if (!tp) return "self";
-    return worker().submit([tp]() -> int { return g_rccl_comms.count(tp) ? 1 : 0; }).get() ? "rccl" : "ipc";
+    if (!worker().submit([tp]() -> int { return g_rccl_comms.count(tp) ? 1 : 0; }).get()) return "ipc";
+    return rccl_native_requested() ? "rccl_native" : "rccl";
 }
 
 std::shared_future<int> engine_async(std::function<int()> fn) { return worker().submit(std::move(fn)); }

@@ -397,7 +397,7 @@ def _free_port():
                                                         (3, None, None, "switch0"), (5, None, None, "switchmax"),
                                                         (5, 65536, None, "switch0"), (7, None, None, "switchmax"),
                                                         (8, None, None, "switch0"), (3, None, None, "staged"),
-                                                        (4, 1 << 20, None, "cached")])
+                                                        (4, 1 << 20, None, "cached"), (3, None, "rccl_native", None)])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
@@ -455,7 +455,7 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
         used = [l.split()[1] for l in o.splitlines() if l.startswith("TRANSPORT")]
         # RCCL needs one GPU per rank: ranks sharing a GPU keep the IPC engine
         n_dev = torch.cuda.device_count()
-        assert used == ["rccl" if transport == "rccl" and n_dev >= p else "ipc"], used
+        assert used == [transport if transport in ("rccl", "rccl_native") and n_dev >= p else "ipc"], used
 
 
 # One rank per GPU -- the deployment the north star names.  The one-GPU box
