@@ -652,6 +652,16 @@ hipError_t dispatch_loc(Kind k, const void* in, void* io, size_t n, hipStream_t 
 
 TreeTune g_tree_tune;
 
+size_t tree_nt_min()
+{
+    static const size_t v = [] {
+        size_t b = (size_t)256 << 20;        // the Infinity Cache (MALL) of one MI355X
+        if (const char* e = getenv("MSX_TREE_NT_MIN")) b = (size_t)atoll(e);
+        return b;
+    }();
+    return v;
+}
+
 int shift_tune_set(int mode)
 {
     if (mode < 0 || mode > 2) return -1;
@@ -661,7 +671,7 @@ int shift_tune_set(int mode)
 
 int tree_tune_set(int mode, int grid_cap)
 {
-    if (mode < 0 || mode > 11 || grid_cap < 0) return -1;
+    if (mode < 0 || mode > 13 || grid_cap < 0) return -1;
     g_tree_tune.mode = mode;
     g_tree_tune.grid_cap = grid_cap;
     return 0;

@@ -558,6 +558,8 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
 
 // host side: the per-op tree launchers (msx_tree_*.hip) and the tuning knob
 extern TreeTune g_tree_tune;
+// source bytes of one tree launch above which its loads are non-temporal
+size_t tree_nt_min();
 template <int OP>
 hipError_t tree_dispatch(Kind k, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s);
 // fp32 SUM tuning modes of msx_tune_tree (msx_tree_sum.hip)

@@ -41,7 +41,7 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
 // kernel otherwise (non-power-of-two folds, binomial trees with absent
 // leaves, other chain lengths, p = 16).
 template <int OP, class T, class VT, int U = 1, bool NT = false>
-hipError_t run_tree_auto(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
+hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     if (a.chain) {
         switch (a.P) {
@@ -58,7 +58,23 @@ hipError_t run_tree_auto(const TreeArgs& a, int nsrc, void* out, size_t count, h
         default: break;
         }
     }
-    return run_tree<OP, T, VT>(a, nsrc, out, count, s);
+    return run_tree<OP, T, VT, false, NT>(a, nsrc, out, count, s);
+}
+
+// Source loads: plain while the call's sources fit the 256 MiB Infinity Cache
+// (just written by the scatter, so partly resident: plain loads hit it),
+// non-temporal beyond (streaming: the cache only churns).  p = 8 fp32 SUM,
+// per-source MiB -> us plain / non-temporal (scripts/tree_probe.py,
+// profiles/r03/tree/size_sweep/): 32: 46.7 / 47.8, 48: 85.6 / 72.5,
+// 64: 117.4 / 96.6, 128: 224.3 / 189.3.  MSX_TREE_NT_MIN overrides the bound
+// (tree_nt_min, msx_kernels.hip).
+
+template <int OP, class T, class VT, int U = 1>
+hipError_t run_tree_auto(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
+{
+    if (count * sizeof(T) * (size_t)nsrc > tree_nt_min())
+        return run_tree_sel<OP, T, VT, U, true>(a, nsrc, out, count, s);
+    return run_tree_sel<OP, T, VT, U, false>(a, nsrc, out, count, s);
 }
 
 template <int OP>

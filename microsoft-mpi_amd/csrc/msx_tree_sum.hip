@@ -13,25 +13,25 @@ template hipError_t tree_dispatch<O_PROD>(Kind, const dev::TreeArgs&, int, void*
 // compile-time-source kernel); 9 = 4 with the tile order of the grid_cap
 // argument (TreeArgs::xg: 0 XCD-contiguous, > 0 runs of that many tiles per
 // XCD, -1 passed as 0x7fffffff: dispatch order, no grid cap in this mode),
-// 10/11 = 4 with 512- / 1024-lane workgroups; mode 0 (not routed here) is the
-// default dispatch.
+// 10/11 = 4 with 512- / 1024-lane workgroups, 12/13 = 4/6 with non-temporal
+// loads; mode 0 (not routed here) is the default dispatch.
 hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
 {
     switch (mode) {
     case 1: return run_tree<O_SUM, float, float, true, false>(a, ns, out, n, s);
     case 2: return run_tree<O_SUM, float, float, true, true>(a, ns, out, n, s);
     case 3: return run_tree<O_SUM, float, float, false, true>(a, ns, out, n, s);
-    case 4: return run_tree_auto<O_SUM, float, float, 1, false>(a, ns, out, n, s);
-    case 5: return run_tree_auto<O_SUM, float, float, 2, false>(a, ns, out, n, s);
-    case 6: return run_tree_auto<O_SUM, float, float, 4, false>(a, ns, out, n, s);
-    case 7: return run_tree_auto<O_SUM, float, float, 2, true>(a, ns, out, n, s);
+    case 4: return run_tree_sel<O_SUM, float, float, 1, false>(a, ns, out, n, s);
+    case 5: return run_tree_sel<O_SUM, float, float, 2, false>(a, ns, out, n, s);
+    case 6: return run_tree_sel<O_SUM, float, float, 4, false>(a, ns, out, n, s);
+    case 7: return run_tree_sel<O_SUM, float, float, 2, true>(a, ns, out, n, s);
     case 8: return run_tree<O_SUM, float, float>(a, ns, out, n, s);
     case 9: {
         TreeArgs b = a;
         b.xg = g_tree_tune.grid_cap == 0x7fffffff ? -1 : g_tree_tune.grid_cap;
         const int cap = g_tree_tune.grid_cap;
         g_tree_tune.grid_cap = 0;
-        const hipError_t e = run_tree_auto<O_SUM, float, float, 1, false>(b, ns, out, n, s);
+        const hipError_t e = run_tree_sel<O_SUM, float, float, 1, false>(b, ns, out, n, s);
         g_tree_tune.grid_cap = cap;
         return e;
     }
@@ -41,6 +41,8 @@ hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out
             return mode == 10 ? run_tree<O_SUM, float, float, false, false, 8, 1, false, 512>(a, ns, out, n, s)
                               : run_tree<O_SUM, float, float, false, false, 8, 1, false, 1024>(a, ns, out, n, s);
         return hipErrorInvalidValue;
+    case 12: return run_tree_sel<O_SUM, float, float, 1, true>(a, ns, out, n, s);
+    case 13: return run_tree_sel<O_SUM, float, float, 4, true>(a, ns, out, n, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -19,8 +19,8 @@ C = msx.C
 dev = torch.device("cuda:0")
 stream = torch.cuda.Stream()
 sp = ctypes.c_void_p(stream.cuda_stream)
-P, M = 8, 8 << 20                    # 8 x 32 MiB of fp32
-skew = 68 << 10
+P, M = 8, int(os.environ.get("TREE_MIB", "32")) << 18   # 8 sources of TREE_MIB MiB of fp32 (default 32)
+skew = int(os.environ.get("TREE_SKEW_KB", "68")) << 10
 SLOT = M * 4 + skew
 HBM = 8000.0
 
@@ -48,7 +48,7 @@ def timed(fn, reps=10):
 out = {}
 modes = [(0, "default"), (8, "generic"), (1, "generic_upfront"), (4, "fixed_u1"), (5, "fixed_u2"),
          (6, "fixed_u4"), (7, "fixed_u2_nt"), (9, "fixed_u1_order"), (10, "fixed_u1_b512"),
-         (11, "fixed_u1_b1024")]
+         (11, "fixed_u1_b1024"), (12, "fixed_u1_nt"), (13, "fixed_u4_nt")]
 if os.environ.get("TREE_MODES"):
     keep = {int(m) for m in os.environ["TREE_MODES"].split(",")}
     modes = [(m, n) for m, n in modes if m in keep]
