@@ -42,7 +42,24 @@ __device__ __forceinline__ void issued_together(u32x4& x, u32x4& y)
 // T  = element type used for scalar elements;
 // VT = lane type used inside a 16-byte vector (== T except bitwise ops, which
 //      run on 32-bit words regardless of the MPI element type).
-template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, bool XCD = true>
+// XG: tile order -- 0 XCD-contiguous eighths, -1 dispatch order (round-robin
+// over XCDs), G > 0 XCD x owns interleaved runs of G consecutive tiles.
+template <int XG>
+__device__ __forceinline__ size_t combine_tile(unsigned b, unsigned nb)
+{
+    if constexpr (XG == 0) {
+        return xcd_tile(b, nb);
+    } else if constexpr (XG < 0) {
+        return b;
+    } else {
+        const unsigned full = (nb / (8u * XG)) * (8u * XG);
+        if (b >= full) return b;
+        const unsigned x = b & 7, j = b >> 3;
+        return ((size_t)(j / XG) * 8 + x) * XG + (j % XG);
+    }
+}
+
+template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, int XG = 0>
 __device__ __forceinline__ void combine_body(const T* __restrict__ in, T* __restrict__ io, size_t head,
                                              size_t nvec, size_t tail)
 {
@@ -50,7 +67,7 @@ __device__ __forceinline__ void combine_body(const T* __restrict__ in, T* __rest
     constexpr size_t TILE = (size_t)BLOCK * UNROLL;
     const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in + head);
     u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
-    const size_t bid = XCD ? (size_t)xcd_tile(blockIdx.x, gridDim.x) : (size_t)blockIdx.x;
+    const size_t bid = combine_tile<XG>(blockIdx.x, gridDim.x);
 
     for (size_t t0 = bid * TILE; t0 < nvec; t0 += (size_t)gridDim.x * TILE) {
         const size_t i0 = t0 + threadIdx.x;
@@ -101,12 +118,12 @@ __global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* 
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
 }
 
-// Tuning variant: the same body in plain dispatch (round-robin over XCDs) order.
-template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
+// Tuning variant: the same body in another tile order (XG, see combine_tile).
+template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, int XG>
 __global__ __launch_bounds__(BLOCK) void k_combine_rr(const T* __restrict__ in, T* __restrict__ io,
                                                       size_t head, size_t nvec, size_t tail)
 {
-    combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST, false>(in, io, head, nvec, tail);
+    combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST, XG>(in, io, head, nvec, tail);
 }
 
 // Same body, launched by the host-memory path of MPI_Reduce_local (pinned
@@ -512,7 +529,7 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
     return hipGetLastError();
 }
 
-template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
+template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, int XG = -1>
 hipError_t run_combine_rr(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
 {
     size_t head, nvec, tail;
@@ -524,7 +541,7 @@ hipError_t run_combine_rr(const void* in, void* io, size_t count, hipStream_t s,
     if (grid == 0) return hipSuccess;
     if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
     if (grid > 0x7fffffffu) grid = 0x7fffffffu;
-    hipLaunchKernelGGL((k_combine_rr<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid), dim3(BLOCK), 0,
+    hipLaunchKernelGGL((k_combine_rr<OP, T, VT, UNROLL, BLOCK, NTLD, NTST, XG>), dim3((unsigned)grid), dim3(BLOCK), 0,
                        s, static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail);
     return hipGetLastError();
 }
@@ -603,6 +620,18 @@ const Variant kF32SumVariants[] = {
     {"k2_b256_ntld_unr", run_combine_kt<O_SUM, float, float, 256, 2, true>},
     {"k4_b256_ntld_unr", run_combine_kt<O_SUM, float, float, 256, 4, true>},
     {"k2_b128_ntld_unr", run_combine_kt<O_SUM, float, float, 128, 2, true>},
+    // tile-order variants for DRAM-bound sizes (operands far above the 256 MiB
+    // Infinity Cache, scripts/combine_size_sweep.py)
+    {"u1_b256_ntld_xg2", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 2>},
+    {"u1_b256_ntld_xg8", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 8>},
+    {"u1_b256_ntld_xg32", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 32>},
+    {"u1_b256_ntld_xg128", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 128>},
+    {"u1_b256_ntld_xg512", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 512>},
+    {"u1_b64_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 64, true, false, -1>},
+    {"u1_b128_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 128, true, false, -1>},
+    {"u1_b512_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 512, true, false, -1>},
+    {"u1_b256_ntall_rr", run_combine_rr<O_SUM, float, float, 1, 256, true, true, -1>},
+    {"u4_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 4, 256, true, false, -1>},
 };
 constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
 
