@@ -126,6 +126,20 @@ __global__ __launch_bounds__(BLOCK) void k_combine_rr(const T* __restrict__ in, 
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST, XG>(in, io, head, nvec, tail);
 }
 
+// Same body for operands far above the 256 MiB Infinity Cache (DRAM-bound):
+// one-wave workgroups in dispatch order (round-robin over XCDs), so the eight
+// XCDs stream neighbouring tiles and DRAM sees three streams instead of 24.
+// Interleaved A/B (scripts/combine_cold_ab.sh, profiles/r03/mall/ab/): 1 GiB
+// back to back 5.63 -> 6.06 TB/s, 256 MiB with the cache cold 5.83 -> 6.05,
+// 256 MiB back to back (cache-assisted) 7.12 -> 7.01 -- so it is taken only
+// above kDramMin bytes per operand.
+template <int OP, class T, class VT, int BLOCK, bool NTLD, bool NTST>
+__global__ __launch_bounds__(BLOCK) void k_combine_dram(const T* __restrict__ in, T* __restrict__ io,
+                                                        size_t head, size_t nvec, size_t tail)
+{
+    combine_body<OP, T, VT, 1, BLOCK, NTLD, NTST, -1>(in, io, head, nvec, tail);
+}
+
 // Same body, launched by the host-memory path of MPI_Reduce_local (pinned
 // operands read over PCIe, or HBM staging chunks): a separate symbol so the
 // rocprof statistics of the device-resident kernel stay clean.
@@ -464,6 +478,18 @@ inline void split(const void* in, const void* io, size_t count, size_t& head, si
     head = h; nvec = rest / epv; tail = rest - nvec * epv;
 }
 
+// Bytes per operand above which the device combine takes k_combine_dram
+// (MSX_COMBINE_DRAM_MIN overrides; the Infinity Cache is 256 MiB).
+size_t combine_dram_min()
+{
+    static const size_t v = [] {
+        size_t b = (size_t)256 << 20;
+        if (const char* e = getenv("MSX_COMBINE_DRAM_MIN")) b = (size_t)atoll(e);
+        return b;
+    }();
+    return v;
+}
+
 // k_combine_shift's cross-lane move: 0 = DPP wave_shl:1, 1 = ds_bpermute,
 // 2 = DPP with the previous (one-vector-skewed) wave grid
 int g_shift_mode = 0;
@@ -511,6 +537,16 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
         return hipGetLastError();
     }
     split<T>(in, io, count, head, nvec, tail);
+    if (!cfg.host && cfg.variant == 0 && cfg.grid_cap == 0 && UNROLL == 1 && nvec * 16 > combine_dram_min()) {
+        constexpr int DB = 64;
+        size_t grid = (nvec + DB - 1) / DB;
+        const size_t sc = (head + tail + DB - 1) / DB;
+        if (grid < sc) grid = sc;
+        if (grid > 0x7fffffffu) return hipErrorInvalidValue;    // > 2^37 bytes per operand
+        hipLaunchKernelGGL((k_combine_dram<OP, T, VT, DB, NTLD, NTST>), dim3((unsigned)grid), dim3(DB), 0, s,
+                           static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail);
+        return hipGetLastError();
+    }
     const size_t tile = (size_t)BLOCK * UNROLL;
     size_t grid = (nvec + tile - 1) / tile;
     const size_t sc = (head + tail + BLOCK - 1) / BLOCK;

@@ -486,3 +486,54 @@ def test_device_entry_beyond_4gib_bytes(L):
     assert torch.equal(b[1:], exp)
     del a, b, exp
     torch.cuda.empty_cache()
+
+
+_DRAM_CHILD = r'''
+import ctypes, os, sys, zlib
+sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd")); sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np, torch
+import msx, oracle
+from _cases import KIND, gen, h, legal_pairs
+L = msx.init(errors_return=True)
+s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+bad = []
+for op, dt in legal_pairs(oracle):
+    rng = np.random.default_rng(zlib.crc32(f"dram/{op}/{dt}".encode()))
+    for n, off in ((17, 0), (65537, 0), (40000, 8)):
+        a0, b0 = gen(KIND[dt], op, n, rng), gen(KIND[dt], op, n, rng)
+        a = np.frombuffer(bytearray(a0.tobytes()), dtype=a0.dtype)
+        b = np.frombuffer(bytearray(b0.tobytes()), dtype=b0.dtype)
+        exp = np.frombuffer(bytearray(b.tobytes()), dtype=a.dtype)
+        assert oracle.reduce_local(h(op), h(dt), a, exp) == 0
+        if off % a.dtype.itemsize and off % 8:
+            continue
+        ta = torch.zeros(a.nbytes + off + 64, dtype=torch.uint8, device="cuda")
+        tb = torch.zeros(b.nbytes + off + 64, dtype=torch.uint8, device="cuda")
+        ta[off:off + a.nbytes] = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).cuda()
+        tb[off:off + b.nbytes] = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).cuda()
+        torch.cuda.synchronize()
+        rc = L.msx_reduce_local_dev(ta.data_ptr() + off, tb.data_ptr() + off, n, h(dt), h(op), s)
+        torch.cuda.synchronize()
+        got = tb[off:off + b.nbytes].cpu().numpy().tobytes()
+        if rc or got != exp.tobytes():
+            bad.append(f"{op} {dt} n={n} off={off} rc={rc}")
+print("DRAM_BAD", len(bad), bad[:5], flush=True)
+'''
+
+
+def test_dram_regime_kernel_every_pair(L, tmp_path):
+    """k_combine_dram (operands above the Infinity Cache: one-wave workgroups
+    in dispatch order) for every legal pair: MSX_COMBINE_DRAM_MIN=0 makes a
+    child process route every vector-path call through it; bit-exact against
+    the oracle, aligned and with an 8-byte common offset (head/tail paths).
+    The in-process tests above cover it at its natural sizes (8 GiB fp32,
+    4 GiB + 13 B BXOR)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MSX_COMBINE_DRAM_MIN="0")
+    r = subprocess.run([sys.executable, "-c", f"REPO={msx.REPO_ROOT!r}\n" + _DRAM_CHILD], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("DRAM_BAD")]
+    assert line and line[0].split()[1] == "0", (r.stdout + r.stderr)[-3000:]
