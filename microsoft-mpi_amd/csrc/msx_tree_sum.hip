@@ -14,7 +14,7 @@ template hipError_t tree_dispatch<O_PROD>(Kind, const dev::TreeArgs&, int, void*
 // argument (TreeArgs::xg: 0 XCD-contiguous, > 0 runs of that many tiles per
 // XCD, -1 passed as 0x7fffffff: dispatch order, no grid cap in this mode),
 // 10/11 = 4 with 512- / 1024-lane workgroups, 12/13 = 4/6 with non-temporal
-// loads; mode 0 (not routed here) is the default dispatch.
+// loads, 14 = 12 with mode 9's tile order; mode 0 (not routed here) is the default dispatch.
 hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
 {
     switch (mode) {
@@ -42,6 +42,15 @@ hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out
                               : run_tree<O_SUM, float, float, false, false, 8, 1, false, 1024>(a, ns, out, n, s);
         return hipErrorInvalidValue;
     case 12: return run_tree_sel<O_SUM, float, float, 1, true>(a, ns, out, n, s);
+    case 14: {   // 12 with the tile order of the grid_cap argument (as mode 9)
+        TreeArgs b = a;
+        b.xg = g_tree_tune.grid_cap == 0x7fffffff ? -1 : g_tree_tune.grid_cap;
+        const int cap = g_tree_tune.grid_cap;
+        g_tree_tune.grid_cap = 0;
+        const hipError_t e = run_tree_sel<O_SUM, float, float, 1, true>(b, ns, out, n, s);
+        g_tree_tune.grid_cap = cap;
+        return e;
+    }
     case 13: return run_tree_sel<O_SUM, float, float, 4, true>(a, ns, out, n, s);
     default: return hipErrorInvalidValue;
     }

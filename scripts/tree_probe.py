@@ -48,7 +48,7 @@ def timed(fn, reps=10):
 out = {}
 modes = [(0, "default"), (8, "generic"), (1, "generic_upfront"), (4, "fixed_u1"), (5, "fixed_u2"),
          (6, "fixed_u4"), (7, "fixed_u2_nt"), (9, "fixed_u1_order"), (10, "fixed_u1_b512"),
-         (11, "fixed_u1_b1024"), (12, "fixed_u1_nt"), (13, "fixed_u4_nt")]
+         (11, "fixed_u1_b1024"), (12, "fixed_u1_nt"), (13, "fixed_u4_nt"), (14, "fixed_u1_nt_order")]
 if os.environ.get("TREE_MODES"):
     keep = {int(m) for m in os.environ["TREE_MODES"].split(",")}
     modes = [(m, n) for m, n in modes if m in keep]
@@ -80,7 +80,7 @@ for uncached in (0, 1):
     ref = xs[0]
     del xs
     for mode, name in modes:
-        for cap in (orders if mode == 9 else caps if mode in (0, 1, 4, 5, 6, 7, 8) else [0]):
+        for cap in (orders if mode in (9, 14) else caps if mode in (0, 1, 4, 5, 6, 7, 8) else [0]):
             L.msx_tune_tree(mode, cap)
             ms = timed(lambda: L.msx_reduce_tree_dev(srcs, P, dst, M, C.MPI_FLOAT, C.MPI_SUM, sp))
             gbs = (P + 1) * M * 4 / ms / 1e6
