@@ -599,6 +599,13 @@ def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12):
     cold method gives the copy-like stream mix is what the kernel does without
     the cache.  Reported beside `value`, never part of it."""
     sp = ctypes.c_void_p(stream.cuda_stream)
+    # the default kernel body under its probe symbol (k_combine_rr<..., 0>), so
+    # these single launches stay out of the headline symbol's rocprof average
+    L.msx_tune_variant_name.restype = ctypes.c_char_p
+    probe_v = [v for v in range(L.msx_tune_variant_count())
+               if L.msx_tune_variant_name(v).decode() == "default_body_probe"]
+    if not probe_v or L.msx_tune_set(probe_v[0], 0) != 0:
+        return {"error": "default_body_probe variant missing"}
     flush = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
     ts, warm = [], []
     for _ in range(reps):
@@ -639,12 +646,15 @@ def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12):
         pms = sorted(pt)[reps // 2]
         mixes[name] = round(streams * n * 4 / pms / 1e6, 1)
     del flush, a2, b2
+    L.msx_tune_set(0, 0)
     cms, wms = sorted(ts)[reps // 2], sorted(warm)[reps // 2]
     gbs = n * BYTES_PER_ELEM / cms / 1e6
     return {"cold_us": round(cms * 1e3, 1), "cold_GB_s": round(gbs, 1), "cold_frac": round(gbs / HBM_PEAK_GBS, 4),
             "warm_single_us": round(wms * 1e3, 1), "cold_probe_GB_s": mixes,
             "method": "median of 12 single launches, each after a 1 GiB read + write pass over other data "
-                      "(cold) or right after the previous launch (warm); HIP events on the launch stream"}
+                      "(cold) or right after the previous launch (warm); HIP events on the launch stream; "
+                      "the default kernel body under its probe symbol k_combine_rr<3, float, float, 1, 256, "
+                      "true, false, 0>"}
 
 
 def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
