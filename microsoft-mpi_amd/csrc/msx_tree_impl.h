@@ -72,7 +72,10 @@ hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hi
 template <int OP, class T, class VT, int U = 1>
 hipError_t run_tree_auto(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
-    if (count * sizeof(T) * (size_t)nsrc > tree_nt_min())
+    // sources actually read: a tree's leaves plus the second operand of each
+    // folded pair (nsrc counts the 2P slots), a chain's P vectors
+    const size_t nread = a.chain ? (size_t)a.P : (size_t)a.nleaves + (size_t)__builtin_popcount(a.pairmask);
+    if (count * sizeof(T) * nread > tree_nt_min())
         return run_tree_sel<OP, T, VT, U, true>(a, nsrc, out, count, s);
     return run_tree_sel<OP, T, VT, U, false>(a, nsrc, out, count, s);
 }
