@@ -902,6 +902,9 @@ public:
 private:
     void loop()
     {
+        // a new thread starts on HIP device 0: bind it to this rank's GPU
+        // before any task allocates (one rank per GPU on a multi-GPU node)
+        (void)ensure_device();
         for (;;) {
             std::shared_ptr<std::packaged_task<int()>> t;
             {
@@ -1295,20 +1298,29 @@ size_t sub_skew(size_t per_rank)
     return (per_rank / 16) & ~(size_t)255;
 }
 
-// usable bytes of one sub-slot of a window with chunk C over p ranks
+// usable bytes of one sub-slot of a window with chunk C over p ranks: the
+// whole C/p, so p sub-slots hold a full chunk (the skew is added on top, see
+// in_bytes).  Rounds 1-3 carved the skew out of C/p, so a chunk held
+// C - p*68 KiB and a 1 GiB allreduce took 3 chunks instead of 2, the last of
+// them ~1 MiB long but paying a chunk's five synchronisation points.
 size_t sub_len(size_t C, int p)
 {
-    const size_t per = C / (size_t)p;
-    return (per - sub_skew(per)) & ~(size_t)255;
+    return (C / (size_t)p) & ~(size_t)255;
+}
+
+// IN area of a window: p sub-slots of sub_len, sub_skew apart
+size_t in_bytes(size_t C, int p)
+{
+    return (size_t)p * (sub_len(C, p) + sub_skew(C / (size_t)p));
 }
 
 struct Windows {
     std::vector<char*> base;
-    size_t C = 0, Q = 0, S = 0;
+    size_t C = 0, Q = 0, S = 0, I = 0;   // chunk, sub-slot length, sub-slot stride, IN area bytes
     char* in(int r) const { return base[(size_t)r]; }
     char* sub(int r, int k) const { return base[(size_t)r] + (size_t)k * S; }
-    char* out(int r) const { return base[(size_t)r] + C; }
-    unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + 2 * C); }
+    char* out(int r) const { return base[(size_t)r] + I; }
+    unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + I + C); }
     // passive-target staging (rma_window), when the communicator has one
     std::vector<char*> rbase;
     size_t rma_slot() const { return (rma_bytes() / (2 * rbase.size())) & ~(size_t)255; }
@@ -1409,7 +1421,10 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
     w->C = chunk_bytes();
     w->Q = sub_len(w->C, tp->size);
     w->S = w->Q + sub_skew(w->C / (size_t)tp->size);
-    int rc = tp->window(2 * w->C + kFlagBytes, w->base);
+    w->I = in_bytes(w->C, tp->size);
+    // [IN: p sub-slots][OUT: C][flags]; at most 17/16 C + C + 64 KiB, below
+    // the 2 GiB IPC mapping limit for C <= 960 MiB
+    int rc = tp->window(w->I + w->C + kFlagBytes, w->base);
     if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
         // the last recursive-doubling call left without its closing barrier:
         // peers may still be reading their IN areas
