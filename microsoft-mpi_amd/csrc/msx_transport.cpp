@@ -1423,7 +1423,13 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
     w->S = w->Q + sub_skew(w->C / (size_t)tp->size);
     w->I = in_bytes(w->C, tp->size);
     // [IN: p sub-slots][OUT: C][flags]; at most 17/16 C + C + 64 KiB, below
-    // the 2 GiB IPC mapping limit for C <= 960 MiB
+    // the 2 GiB IPC mapping limit for C <= 960 MiB (checked: a larger
+    // allocation would hang hipIpcOpenMemHandle, see map_peers)
+    if (w->I + w->C + kFlagBytes > ((size_t)2046 << 20)) {
+        set_error("window of %zu bytes exceeds the IPC mapping limit (MSX_CHUNK_BYTES too large)",
+                  w->I + w->C + kFlagBytes);
+        return MPI_ERR_INTERN;
+    }
     int rc = tp->window(w->I + w->C + kFlagBytes, w->base);
     if (rc == MPI_SUCCESS && tp->window_open && !rd_single) {
         // the last recursive-doubling call left without its closing barrier:
