@@ -110,6 +110,8 @@ def main(out_path, scale):
     stats = (ctypes.c_double * 7)()
     L.msx_engine_stats(stats, 7, 1)                 # reset the phase timers
     for it in range(4):
+        if it == 1:
+            L.msx_engine_stats(stats, 7, 1)         # phases of the timed calls only (not the warm-up's setup)
         barrier()
         t0 = time.perf_counter()
         rc = L.MPI_Allreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
@@ -348,14 +350,20 @@ def main(out_path, scale):
         t0 = time.perf_counter()
         host_work(K)
         t_host = min(t_host, time.perf_counter() - t0)
-    barrier()
-    req = ctypes.c_int()
-    t0 = time.perf_counter()
-    rc2 = L.MPI_Iallreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND, C.MPI_COMM_WORLD,
-                           ctypes.byref(req))
-    host_work(K)
-    rc3 = L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1))
-    t_total = time.perf_counter() - t0
+    # best of 3, like t_comm and t_host (one sample of a ~1 ms overlap on a
+    # shared box varied 0.71-0.82 between runs)
+    t_total, rc2, rc3 = 1e30, 0, 0
+    for _ in range(3):
+        barrier()
+        req = ctypes.c_int()
+        t0 = time.perf_counter()
+        rc2 = rc2 or L.MPI_Iallreduce(send.data_ptr(), recv.data_ptr(), n, C.MPI_UINT64_T, C.MPI_BAND,
+                                      C.MPI_COMM_WORLD, ctypes.byref(req))
+        host_work(K)
+        rc3 = rc3 or L.MPI_Wait(ctypes.byref(req), ctypes.c_void_p(1))
+        t_total = min(t_total, time.perf_counter() - t0)
+        if rc2 or rc3:
+            break
     log(f"c5 done rc={rc},{rc2},{rc3} comm={t_comm:.4f} host={t_host:.4f} total={t_total:.4f}")
     if rc or rc2 or rc3:
         fail("c5", rc or rc2 or rc3)
