@@ -136,7 +136,9 @@ int msx_tune_shift(int mode);
  * pointers): mode 0 reads a and b, 1 writes b, 2 copies a -> b, 3 reads a;
  * 4 copies a -> b with the engine's segment-copy kernel (k_copy_segs), 5 with
  * hipMemcpyAsync; 6 writes 16 B of every 32 B of b (gapped store), 7 reads
- * 16 B of every 32 B of a (gapped load).
+ * 16 B of every 32 B of a (gapped load); 8 / 9 copy a -> b in a forced
+ * geometry (8: k_copy_segs' XCD-contiguous 4-KiB tiles, 9: k_copy_dram's
+ * one-wave workgroups in dispatch order).
  * Stream-ordered; b's contents are unspecified afterwards. */
 int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream);
 /* device allocation for measurements: uncached = the engine windows' memory

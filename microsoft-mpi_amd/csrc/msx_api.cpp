@@ -2425,7 +2425,7 @@ MSX_EXPORT int msx_tune_tree(int mode, int grid_cap)
 
 MSX_EXPORT int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream)
 {
-    if (mode < 0 || mode > 7 || bytes < 0 || !b || (mode != 1 && mode != 6 && !a)) return MPI_ERR_ARG;
+    if (mode < 0 || mode > 9 || bytes < 0 || !b || (mode != 1 && mode != 6 && !a)) return MPI_ERR_ARG;
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
     hipError_t e = launch_probe(mode, a, b, (size_t)bytes, static_cast<hipStream_t>(stream));

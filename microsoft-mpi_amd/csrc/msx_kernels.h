@@ -139,6 +139,8 @@ int shift_tune_set(int mode);
 // HBM ceiling probe (measurement only, see k_probe): mode 0 reads a and b,
 // 1 writes b, 2 copies a -> b, 3 reads a; `bytes` per stream, 16-B aligned.
 hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s);
+// one aligned local copy in a forced geometry: dram = 0 k_copy_segs, 1 k_copy_dram
+hipError_t launch_copy_one(const void* src, void* dst, size_t nbytes, hipStream_t s, int dram);
 
 // Number of tuning variants compiled for the fp32 SUM hot path.
 int combine_variant_count();

@@ -407,6 +407,16 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
     if (c.sys) release_system();
 }
 
+// One local copy far above the 256 MiB Infinity Cache (DRAM-bound): the
+// combine's DRAM-regime geometry (k_combine_dram) -- one-wave workgroups in
+// dispatch order, so the eight XCDs stream neighbouring 1-KiB tiles and DRAM
+// sees two streams instead of 16.  16-byte aligned, whole vectors only.
+__global__ __launch_bounds__(64) void k_copy_dram(const u32x4* __restrict__ s, u32x4* __restrict__ d, size_t nv)
+{
+    const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (i < nv) d[i] = ld<true>(s + i);
+}
+
 // The small-allreduce push with its arrival flags in one launch: every
 // workgroup copies its part of its segment with system-coherent stores
 // (sc0 sc1: written through to the owner's memory, never left dirty in this
@@ -740,7 +750,7 @@ int shift_tune_set(int mode)
 
 int tree_tune_set(int mode, int grid_cap)
 {
-    if (mode < 0 || mode > 14 || grid_cap < 0) return -1;
+    if (mode < 0 || mode > 16 || grid_cap < 0) return -1;
     g_tree_tune.mode = mode;
     g_tree_tune.grid_cap = grid_cap;
     return 0;
@@ -898,8 +908,9 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
 
 hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s)
 {
-    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 7) return hipErrorInvalidValue;
+    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 9) return hipErrorInvalidValue;
     if (mode == 4) return launch_copy_segs(&a, &b, &bytes, 1, false, s);      // the engine's copy kernel
+    if (mode == 8 || mode == 9) return launch_copy_one(a, b, bytes, s, mode == 8 ? 0 : 1);   // forced geometry
     if (mode == 5) return hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, s);   // HIP's blit
     // modes 6 / 7 touch every other 16-B vector of `bytes`: nvec = bytes / 32
     const size_t nvec = (mode >= 6) ? bytes / 32 : bytes / 16;
@@ -1019,9 +1030,50 @@ hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned lon
     return hipGetLastError();
 }
 
+// Bytes of one local copy above which it takes k_copy_dram (MSX_COPY_DRAM_MIN,
+// default the combine's 256 MiB, see combine_dram_min).
+size_t copy_dram_min()
+{
+    static const size_t v = [] {
+        size_t b = (size_t)256 << 20;
+        if (const char* e = getenv("MSX_COPY_DRAM_MIN")) b = (size_t)atoll(e);
+        return b;
+    }();
+    return v;
+}
+
+// One aligned local copy in a forced geometry (probe modes 8 / 9): 0 =
+// k_copy_segs' XCD-contiguous 4-KiB tiles, 1 = k_copy_dram.
+hipError_t launch_copy_one(const void* src, void* dst, size_t nbytes, hipStream_t s, int dram)
+{
+    if ((((uintptr_t)src | (uintptr_t)dst | nbytes) & 15) != 0) return hipErrorInvalidValue;
+    const size_t nv = nbytes / 16;
+    if (nv == 0) return hipSuccess;
+    if (dram) {
+        const size_t grid = (nv + 63) / 64;
+        if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_copy_dram, dim3((unsigned)grid), dim3(64), 0, s, static_cast<const u32x4*>(src),
+                           static_cast<u32x4*>(dst), nv);
+        return hipGetLastError();
+    }
+    CopySegs c{};
+    c.n = 1;
+    c.src[0] = src;
+    c.dst[0] = dst;
+    c.nbytes[0] = nbytes;
+    const size_t gx = (nv + 255) / 256;
+    if (gx > 0x7fffffffu) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_copy_segs, dim3((unsigned)gx), dim3(256), 0, s, c);
+    return hipGetLastError();
+}
+
 hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             bool sys, hipStream_t s)
 {
+    // one local copy in the DRAM regime (the collect of a 512 MiB chunk)
+    if (nseg == 1 && !sys && nbytes[0] > copy_dram_min() &&
+        ((((uintptr_t)src[0] | (uintptr_t)dst[0] | nbytes[0]) & 15) == 0))
+        return launch_copy_one(src[0], dst[0], nbytes[0], s, 1);
     for (int base = 0; base < nseg; base += kMaxSegs) {
         CopySegs c{};
         c.sys = sys ? 1 : 0;

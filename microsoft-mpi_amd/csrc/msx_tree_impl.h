@@ -40,21 +40,43 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
 // a chain of 2, 4 or 8 sources (p = 2, 4, 8: the node sizes); the generic
 // kernel otherwise (non-power-of-two folds, binomial trees with absent
 // leaves, other chain lengths, p = 16).
+// DRAM-regime geometry of the compile-time-source kernel (NT: the sources
+// exceed the Infinity Cache): one-wave workgroups in dispatch order, as
+// k_combine_dram, so the eight XCDs read neighbouring tiles of every source.
+// p = 8 fp32 SUM, uncached sources, two interleaved rounds
+// (scripts/tree_dram_ab.sh, profiles/r03/tree/dram_geometry/): 64 MiB per
+// source 96.3 -> 90.9 us (0.78 -> 0.83 of peak), 128 MiB 201.7 -> 186.8 us
+// (0.75 -> 0.81); 64-lane workgroups in XCD-contiguous order and 256-lane ones
+// in dispatch order gain 1-2 % only.  Not with fused push workgroups (their
+// copy loop assumes 256 lanes; only small calls fuse).
+template <int OP, class T, class VT, bool NT, int NL, int U, bool CHAIN>
+hipError_t run_tree_fixed(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
+{
+    if constexpr (NT) {
+        if (a.npush == 0) {
+            TreeArgs b = a;
+            b.xg = -1;
+            return run_tree<OP, T, VT, false, NT, NL, U, CHAIN, 64>(b, nsrc, out, count, s);
+        }
+    }
+    return run_tree<OP, T, VT, false, NT, NL, U, CHAIN>(a, nsrc, out, count, s);
+}
+
 template <int OP, class T, class VT, int U = 1, bool NT = false>
 hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     if (a.chain) {
         switch (a.P) {
-        case 2: return run_tree<OP, T, VT, false, NT, 2, U, true>(a, nsrc, out, count, s);
-        case 4: return run_tree<OP, T, VT, false, NT, 4, U, true>(a, nsrc, out, count, s);
-        case 8: return run_tree<OP, T, VT, false, NT, 8, U, true>(a, nsrc, out, count, s);
+        case 2: return run_tree_fixed<OP, T, VT, NT, 2, U, true>(a, nsrc, out, count, s);
+        case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, true>(a, nsrc, out, count, s);
+        case 8: return run_tree_fixed<OP, T, VT, NT, 8, U, true>(a, nsrc, out, count, s);
         default: break;
         }
     } else if (a.pairmask == 0 && a.nleaves == a.P) {
         switch (a.P) {
-        case 2: return run_tree<OP, T, VT, false, NT, 2, U>(a, nsrc, out, count, s);
-        case 4: return run_tree<OP, T, VT, false, NT, 4, U>(a, nsrc, out, count, s);
-        case 8: return run_tree<OP, T, VT, false, NT, 8, U>(a, nsrc, out, count, s);
+        case 2: return run_tree_fixed<OP, T, VT, NT, 2, U, false>(a, nsrc, out, count, s);
+        case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, false>(a, nsrc, out, count, s);
+        case 8: return run_tree_fixed<OP, T, VT, NT, 8, U, false>(a, nsrc, out, count, s);
         default: break;
         }
     }

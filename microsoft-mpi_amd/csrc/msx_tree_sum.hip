@@ -14,7 +14,10 @@ template hipError_t tree_dispatch<O_PROD>(Kind, const dev::TreeArgs&, int, void*
 // argument (TreeArgs::xg: 0 XCD-contiguous, > 0 runs of that many tiles per
 // XCD, -1 passed as 0x7fffffff: dispatch order, no grid cap in this mode),
 // 10/11 = 4 with 512- / 1024-lane workgroups, 12/13 = 4/6 with non-temporal
-// loads, 14 = 12 with mode 9's tile order; mode 0 (not routed here) is the default dispatch.
+// loads and 256-lane workgroups (p = 8 full trees only), 14 = 12 with mode 9's
+// tile order, 15/16 = 12 with 64-lane workgroups in dispatch order (the
+// default above tree_nt_min) / XCD-contiguous; mode 0 (not routed here) is the
+// default dispatch.
 hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
 {
     switch (mode) {
@@ -41,17 +44,26 @@ hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out
             return mode == 10 ? run_tree<O_SUM, float, float, false, false, 8, 1, false, 512>(a, ns, out, n, s)
                               : run_tree<O_SUM, float, float, false, false, 8, 1, false, 1024>(a, ns, out, n, s);
         return hipErrorInvalidValue;
-    case 12: return run_tree_sel<O_SUM, float, float, 1, true>(a, ns, out, n, s);
+    case 12:     // non-temporal loads, 256-lane workgroups (the DRAM-regime default before r03's one-wave form)
     case 14: {   // 12 with the tile order of the grid_cap argument (as mode 9)
+        if (a.chain || a.pairmask != 0 || a.nleaves != a.P || a.P != 8) return hipErrorInvalidValue;
         TreeArgs b = a;
-        b.xg = g_tree_tune.grid_cap == 0x7fffffff ? -1 : g_tree_tune.grid_cap;
+        if (mode == 14) b.xg = g_tree_tune.grid_cap == 0x7fffffff ? -1 : g_tree_tune.grid_cap;
         const int cap = g_tree_tune.grid_cap;
         g_tree_tune.grid_cap = 0;
-        const hipError_t e = run_tree_sel<O_SUM, float, float, 1, true>(b, ns, out, n, s);
+        const hipError_t e = run_tree<O_SUM, float, float, false, true, 8, 1, false>(b, ns, out, n, s);
         g_tree_tune.grid_cap = cap;
         return e;
     }
     case 13: return run_tree_sel<O_SUM, float, float, 4, true>(a, ns, out, n, s);
+    case 15:     // 64-lane workgroups, non-temporal loads, dispatch order (k_combine_dram's geometry)
+    case 16:     // 64-lane workgroups, non-temporal loads, XCD-contiguous
+        if (!a.chain && a.pairmask == 0 && a.nleaves == a.P && a.P == 8) {
+            TreeArgs b = a;
+            b.xg = mode == 15 ? -1 : 0;
+            return run_tree<O_SUM, float, float, false, true, 8, 1, false, 64>(b, ns, out, n, s);
+        }
+        return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
     }
 }

@@ -1,7 +1,8 @@
 """Local copy probe (measurement only): 256 MiB device-to-device copies with
 the HBM probe's copy kernel (msx_probe_hbm mode 2), the engine's segment-copy
 kernel k_copy_segs (mode 4, the scatter/collect/allgather copies) and
-hipMemcpyAsync (mode 5), between cached (hipMalloc) and uncached (the engine
+hipMemcpyAsync (mode 5), and the copy kernel forced into each geometry
+(modes 8 / 9: XCD-contiguous 4-KiB tiles / one-wave dispatch order), between cached (hipMalloc) and uncached (the engine
 windows' memory type) allocations.  GB/s counts read + write bytes."""
 import ctypes
 import json
@@ -43,7 +44,8 @@ def timed(fn, reps=20):
 out = {}
 for src_uc, dst_uc in ((0, 0), (1, 0), (0, 1)):
     a, b = alloc(NB, src_uc), alloc(NB, dst_uc)
-    for mode, name in ((2, "probe_copy"), (4, "k_copy_segs"), (5, "hipMemcpyAsync")):
+    for mode, name in ((2, "probe_copy"), (4, "k_copy_segs"), (5, "hipMemcpyAsync"), (8, "forced_xcd_tiles"),
+                       (9, "forced_dram_dispatch")):
         ms = timed(lambda: L.msx_probe_hbm(mode, a, b, NB, sp))
         out[f"{'uc' if src_uc else 'c'}->{'uc' if dst_uc else 'c'}/{name}"] = {
             "us": round(ms * 1e3, 1), "GB_s": round(2 * NB / ms / 1e6, 1)}

@@ -387,7 +387,7 @@ def test_tree_tuning_modes_agree(L):
     for offset in (0, 4):
         dv = [_dev(x, offset if r == 3 else 0) for r, x in enumerate(xs)]
         arr = (ctypes.c_void_p * 8)(*[d[1] for d in dv])
-        for mode in range(9):
+        for mode in range(17):
             for cap in (0, 1024):
                 assert L.msx_tune_tree(mode, cap) == 0
                 out = torch.zeros(n, dtype=torch.float32, device="cuda")
@@ -395,6 +395,22 @@ def test_tree_tuning_modes_agree(L):
                 torch.cuda.synchronize()
                 assert np.array_equal(out.cpu().numpy().view(np.uint32), want), (mode, cap, offset)
     assert L.msx_tune_tree(0, 0) == 0
+
+
+def test_copy_geometries_exact(L):
+    # the engine's local copy in both geometries (probe modes 8 / 9: k_copy_segs'
+    # XCD-contiguous tiles, k_copy_dram's one-wave dispatch order) and the
+    # default launcher (mode 4: k_copy_dram above 256 MiB) copy every byte
+    for nbytes in (4096, (1 << 20) + 48, (300 << 20) + 16):
+        a = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
+        for mode in (4, 8, 9):
+            b = torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()      # the library's streams do not order after torch's
+            assert L.msx_probe_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, _stream()) == 0, msx.last_error()
+            torch.cuda.synchronize()
+            assert torch.equal(b[:nbytes], a), (mode, nbytes)
+            assert int(b[nbytes:].count_nonzero()) == 0, (mode, nbytes)     # nothing written past the end
+        del a, b
 
 
 def test_benchmark_size_fp32_sum_bit_exact(L):
