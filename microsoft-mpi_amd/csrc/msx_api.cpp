@@ -2418,6 +2418,11 @@ MSX_EXPORT int msx_tune_shift(int mode)
     return shift_tune_set(mode) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
 }
 
+MSX_EXPORT int msx_tune_pack(int mode)
+{
+    return pack_tune_set(mode) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
+}
+
 MSX_EXPORT int msx_tune_tree(int mode, int grid_cap)
 {
     return tree_tune_set(mode, grid_cap) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;

@@ -139,6 +139,8 @@ int shift_tune_set(int mode);
 // HBM ceiling probe (measurement only, see k_probe): mode 0 reads a and b,
 // 1 writes b, 2 copies a -> b, 3 reads a; `bytes` per stream, 16-B aligned.
 hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s);
+// pack/unpack geometry: 0 by size, 1 grid-stride form, 2 tile form (msx_pack.hip)
+int pack_tune_set(int mode);
 // one aligned local copy in a forced geometry: dram = 0 k_copy_segs, 1 k_copy_dram
 hipError_t launch_copy_one(const void* src, void* dst, size_t nbytes, hipStream_t s, int dram);
 

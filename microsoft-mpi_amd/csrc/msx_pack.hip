@@ -148,6 +148,37 @@ __global__ __launch_bounds__(kPackBlock) void k_dt_pack(CopyArgs a)
     }
 }
 
+// Tile form for spans far above the 256 MiB Infinity Cache (the combine's
+// DRAM-regime geometry, k_combine_dram): one-wave workgroups in dispatch
+// order, each owning kUnroll x 64 consecutive granules, so the eight XCDs
+// stream neighbouring tiles of both sides instead of the grid-stride form's
+// 4 x 8 streams per side.  Same map, loads before stores, same cache policy.
+template <int G, bool REG, bool NARROW, bool UNPACK>
+__global__ __launch_bounds__(64) void k_dt_pack_tile(CopyArgs a)
+{
+    typedef typename GranT<G>::T T;
+    const int64_t g0 = (int64_t)blockIdx.x * (64 * kUnroll) + threadIdx.x;
+    T v[kUnroll];
+    int64_t off[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const int64_t g = g0 + u * 64;
+        if (g < a.ngran) {
+            off[u] = typed_off<G, REG, NARROW>(a, g);
+            if constexpr (UNPACK) v[u] = __builtin_nontemporal_load(reinterpret_cast<const T*>(a.packed) + g);
+            else v[u] = *reinterpret_cast<const T*>(a.typed + off[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const int64_t g = g0 + u * 64;
+        if (g < a.ngran) {
+            if constexpr (UNPACK) *reinterpret_cast<T*>(a.typed + off[u]) = v[u];
+            else __builtin_nontemporal_store(v[u], reinterpret_cast<T*>(a.packed) + g);
+        }
+    }
+}
+
 // Run-parallel form for layouts whose runs are long (subarray rows, big
 // indexed blocks): one wavefront per (instance, run) unit, its 64 lanes
 // stream the run's granules with coalesced accesses on both sides.  No
@@ -261,6 +292,32 @@ CopyArgs make_args(const DevLayout& L, int64_t count, void* typed, void* packed,
 // per-granule binary search.
 constexpr int64_t kRunParallelMin = 8;
 
+}  // namespace dev
+
+// Pack/unpack geometry (msx_tune_pack): 0 = by size (the tile form when the
+// call's typed span plus packed bytes exceed pack_tile_min()), 1 = always the
+// grid-stride form, 2 = always the tile form.
+int g_pack_mode = 0;
+
+size_t pack_tile_min()
+{
+    static const size_t v = [] {
+        size_t b = (size_t)512 << 20;
+        if (const char* e = getenv("MSX_PACK_TILE_MIN")) b = (size_t)atoll(e);
+        return b;
+    }();
+    return v;
+}
+
+int pack_tune_set(int mode)
+{
+    if (mode < 0 || mode > 2) return -1;
+    g_pack_mode = mode;
+    return 0;
+}
+
+namespace dev {
+
 template <int G, bool UNPACK>
 hipError_t run_copy(const CopyArgs& a, bool reg, hipStream_t s)
 {
@@ -273,6 +330,17 @@ hipError_t run_copy(const CopyArgs& a, bool reg, hipStream_t s)
         const dim3 grid((unsigned)(want < 8192 ? want : 8192));
         hipLaunchKernelGGL((k_dt_runs<G, UNPACK>), grid, block, 0, s, a);
         return hipGetLastError();
+    }
+    const size_t span = (size_t)(a.ngran / a.gsize) * (size_t)a.extent + (size_t)a.ngran * G;
+    if (g_pack_mode == 2 || (g_pack_mode == 0 && span > pack_tile_min())) {
+        const int64_t want = (a.ngran + 64 * kUnroll - 1) / (64 * kUnroll);
+        if (want <= 0x7fffffffll) {
+            const dim3 tg((unsigned)want), tb(64);
+            if (reg && narrow) hipLaunchKernelGGL((k_dt_pack_tile<G, true, true, UNPACK>), tg, tb, 0, s, a);
+            else if (reg) hipLaunchKernelGGL((k_dt_pack_tile<G, true, false, UNPACK>), tg, tb, 0, s, a);
+            else hipLaunchKernelGGL((k_dt_pack_tile<G, false, false, UNPACK>), tg, tb, 0, s, a);
+            return hipGetLastError();
+        }
     }
     const dim3 grid(grid_for(a.ngran));
     if (reg && narrow) hipLaunchKernelGGL((k_dt_pack<G, true, true, UNPACK>), grid, block, 0, s, a);

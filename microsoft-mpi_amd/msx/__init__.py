@@ -171,6 +171,7 @@ def lib():
         "msx_reduce_tree_dev": (i, [ctypes.POINTER(p), i, p, i64, i, i, p]),
         "msx_tune_set": (i, [i, i]),
         "msx_tune_tree": (i, [i, i]),
+        "msx_tune_pack": (i, [i]),
         "msx_tune_variant_count": (i, []),
         "msx_tune_variant_name": (ctypes.c_char_p, [i]),
         "msx_probe_hbm": (i, [i, p, p, i64, p]),

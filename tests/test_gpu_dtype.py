@@ -111,8 +111,17 @@ def test_pack_unpack_host_buffers(L, case):
     free_all(L, keep)
 
 
+@pytest.mark.parametrize("mode", [0, 2])      # 2: the one-wave tile form forced (msx_tune_pack)
 @pytest.mark.parametrize("case", _recipes(25, 5000))
-def test_pack_unpack_device_buffers(L, case):
+def test_pack_unpack_device_buffers(L, case, mode):
+    assert L.msx_tune_pack(mode) == 0
+    try:
+        _pack_unpack_device(L, case)
+    finally:
+        assert L.msx_tune_pack(0) == 0
+
+
+def _pack_unpack_device(L, case):
     r, count, mis = case
     keep = []
     h = _commit(L, r, keep)
