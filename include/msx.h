@@ -131,9 +131,10 @@ const char* msx_tune_variant_name(int variant);
  * the `in` chunks, 0 = DPP wave shift (default), 1 = ds_bpermute, 2 = DPP on
  * the earlier wave grid skewed by one vector (measurement) */
 int msx_tune_shift(int mode);
-/* Pack / unpack kernel geometry (tuning only): 0 = by size (default; the
- * one-wave tile form when typed span + packed bytes exceed MSX_PACK_TILE_MIN,
- * 512 MiB), 1 = always the grid-stride form, 2 = always the tile form. */
+/* Pack / unpack and derived-target accumulate geometry (tuning only): 0 = by
+ * size (default; the one-wave tile form when typed span + packed bytes exceed
+ * MSX_PACK_TILE_MIN, 512 MiB, for pack / unpack and MSX_ACC_TILE_MIN, 0, for
+ * the accumulate), 1 = always the grid-stride form, 2 = always the tile form. */
 int msx_tune_pack(int mode);
 /* HBM ceiling probe (measurement only): the default combine's launch geometry
  * with another stream mix over `bytes` per stream (16-B aligned device

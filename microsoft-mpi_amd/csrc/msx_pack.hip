@@ -232,23 +232,60 @@ __global__ __launch_bounds__(kPackBlock) void k_dt_runs(CopyArgs a)
 // typed element (op)= packed element.  E = element bytes; granules are whole
 // elements.  ALIGNED: every element address is a multiple of alignof(T);
 // otherwise the element moves through byte copies.
+template <int OP, class T, bool ALIGNED>
+__device__ __forceinline__ void acc_elem(char* t, const char* p)
+{
+    constexpr int E = (int)sizeof(T);
+    if constexpr (ALIGNED) {
+        T* tt = reinterpret_cast<T*>(t);
+        *tt = Fn<OP>::apply(*tt, *reinterpret_cast<const T*>(p));
+    } else {
+        T x, y;
+        __builtin_memcpy(&x, t, E);
+        __builtin_memcpy(&y, p, E);
+        x = Fn<OP>::apply(x, y);
+        __builtin_memcpy(t, &x, E);
+    }
+}
+
 template <int OP, class T, bool REG, bool ALIGNED>
 __global__ __launch_bounds__(kPackBlock) void k_dt_acc(CopyArgs a)
 {
     constexpr int E = (int)sizeof(T);
     const int64_t stride = (int64_t)gridDim.x * kPackBlock;
-    for (int64_t g = (int64_t)blockIdx.x * kPackBlock + threadIdx.x; g < a.ngran; g += stride) {
-        char* t = a.typed + typed_off<E, REG, false>(a, g);
-        const char* p = a.packed + g * E;
-        if constexpr (ALIGNED) {
-            T* tt = reinterpret_cast<T*>(t);
-            *tt = Fn<OP>::apply(*tt, *reinterpret_cast<const T*>(p));
-        } else {
-            T x, y;
-            __builtin_memcpy(&x, t, E);
-            __builtin_memcpy(&y, p, E);
-            x = Fn<OP>::apply(x, y);
-            __builtin_memcpy(t, &x, E);
+    for (int64_t g = (int64_t)blockIdx.x * kPackBlock + threadIdx.x; g < a.ngran; g += stride)
+        acc_elem<OP, T, ALIGNED>(a.typed + typed_off<E, REG, false>(a, g), a.packed + g * E);
+}
+
+// Tile form of k_dt_acc (the pack kernels' k_dt_pack_tile): one-wave
+// workgroups in dispatch order, kUnroll x 64 consecutive elements each, every
+// operand of the tile loaded before the first combine when the elements are
+// aligned.
+template <int OP, class T, bool REG, bool ALIGNED>
+__global__ __launch_bounds__(64) void k_dt_acc_tile(CopyArgs a)
+{
+    constexpr int E = (int)sizeof(T);
+    const int64_t g0 = (int64_t)blockIdx.x * (64 * kUnroll) + threadIdx.x;
+    if constexpr (ALIGNED) {
+        T x[kUnroll], y[kUnroll];
+        T* tt[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t g = g0 + u * 64;
+            if (g < a.ngran) {
+                tt[u] = reinterpret_cast<T*>(a.typed + typed_off<E, REG, false>(a, g));
+                x[u] = *tt[u];
+                y[u] = reinterpret_cast<const T*>(a.packed)[g];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+            if (g0 + u * 64 < a.ngran) *tt[u] = Fn<OP>::apply(x[u], y[u]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t g = g0 + u * 64;
+            if (g < a.ngran) acc_elem<OP, T, false>(a.typed + typed_off<E, REG, false>(a, g), a.packed + g * E);
         }
     }
 }
@@ -304,6 +341,22 @@ size_t pack_tile_min()
     static const size_t v = [] {
         size_t b = (size_t)512 << 20;
         if (const char* e = getenv("MSX_PACK_TILE_MIN")) b = (size_t)atoll(e);
+        return b;
+    }();
+    return v;
+}
+
+// Bytes (typed span + packed) of one derived-target accumulate above which it
+// runs k_dt_acc_tile (MSX_ACC_TILE_MIN, default 0: always).  Self-targeted
+// fp32 SUM MPI_Accumulate through a 16-B-block vector target type, grid-stride
+// -> tile form, three interleaved rounds (scripts/acc_probe.py,
+// profiles/r03/acc_geometry/): 256 MiB window 144 -> 140 us per call, 1 GiB
+// 663 -> 521 us.
+size_t acc_tile_min()
+{
+    static const size_t v = [] {
+        size_t b = (size_t)0;
+        if (const char* e = getenv("MSX_ACC_TILE_MIN")) b = (size_t)atoll(e);
         return b;
     }();
     return v;
@@ -386,6 +439,16 @@ hipError_t run_acc(const DevLayout& L, int64_t count, const void* packed, void* 
         if (L.regular && (L.blen % E)) return hipErrorInvalidValue;
         const bool aligned = L.align >= (int)alignof(T);
         const bool reg = L.regular != 0;
+        const size_t span = (size_t)(a.ngran / a.gsize) * (size_t)a.extent + (size_t)a.ngran * E;
+        const int64_t tiles = (a.ngran + 64 * kUnroll - 1) / (64 * kUnroll);
+        if (tiles <= 0x7fffffffll && (g_pack_mode == 2 || (g_pack_mode == 0 && span > acc_tile_min()))) {
+            const dim3 tg((unsigned)tiles), tb(64);
+            if (reg && aligned) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, true, true>), tg, tb, 0, s, a);
+            else if (reg) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, true, false>), tg, tb, 0, s, a);
+            else if (aligned) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, false, true>), tg, tb, 0, s, a);
+            else hipLaunchKernelGGL((k_dt_acc_tile<OP, T, false, false>), tg, tb, 0, s, a);
+            return hipGetLastError();
+        }
         const dim3 grid(grid_for(a.ngran)), block(kPackBlock);
         if (reg && aligned) hipLaunchKernelGGL((k_dt_acc<OP, T, true, true>), grid, block, 0, s, a);
         else if (reg) hipLaunchKernelGGL((k_dt_acc<OP, T, true, false>), grid, block, 0, s, a);
