@@ -750,7 +750,7 @@ int shift_tune_set(int mode)
 
 int tree_tune_set(int mode, int grid_cap)
 {
-    if (mode < 0 || mode > 16 || grid_cap < 0) return -1;
+    if (mode < 0 || mode > 17 || grid_cap < 0) return -1;
     g_tree_tune.mode = mode;
     g_tree_tune.grid_cap = grid_cap;
     return 0;

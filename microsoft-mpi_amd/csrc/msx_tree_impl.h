@@ -26,8 +26,10 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
     const size_t nvec = count / epv, tail = count - nvec * epv;
     const size_t work = ok ? (nvec + U - 1) / U + tail : count;
     size_t grid = (work + BLOCK - 1) / BLOCK;
+    // one tile per workgroup for the compile-time-source kernel and for the
+    // one-wave DRAM-regime form of the generic one; grid-stride beyond
     const size_t cap = g_tree_tune.grid_cap > 0 ? (size_t)g_tree_tune.grid_cap
-                                                : (size_t)(NL > 0 ? kFixedGridCap : kTreeGridCap);
+                                                : (size_t)(NL > 0 || BLOCK == 64 ? kFixedGridCap : kTreeGridCap);
     if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
     grid += a.npush;                         // fused push workgroups come first
@@ -78,6 +80,14 @@ hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hi
         case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, false>(a, nsrc, out, count, s);
         case 8: return run_tree_fixed<OP, T, VT, NT, 8, U, false>(a, nsrc, out, count, s);
         default: break;
+        }
+    }
+    if constexpr (NT) {
+        // the generic kernel in the same DRAM-regime geometry (run_tree_fixed)
+        if (a.npush == 0) {
+            TreeArgs b = a;
+            b.xg = -1;
+            return run_tree<OP, T, VT, false, NT, 0, 1, false, 64>(b, nsrc, out, count, s);
         }
     }
     return run_tree<OP, T, VT, false, NT>(a, nsrc, out, count, s);

@@ -16,8 +16,9 @@ template hipError_t tree_dispatch<O_PROD>(Kind, const dev::TreeArgs&, int, void*
 // 10/11 = 4 with 512- / 1024-lane workgroups, 12/13 = 4/6 with non-temporal
 // loads and 256-lane workgroups (p = 8 full trees only), 14 = 12 with mode 9's
 // tile order, 15/16 = 12 with 64-lane workgroups in dispatch order (the
-// default above tree_nt_min) / XCD-contiguous; mode 0 (not routed here) is the
-// default dispatch.
+// default above tree_nt_min) / XCD-contiguous, 17 = the generic kernel in mode
+// 15's geometry (its default above tree_nt_min); mode 0 (not routed here) is
+// the default dispatch.
 hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s)
 {
     switch (mode) {
@@ -56,6 +57,11 @@ hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out
         return e;
     }
     case 13: return run_tree_sel<O_SUM, float, float, 4, true>(a, ns, out, n, s);
+    case 17: {   // the generic kernel, non-temporal loads, 64-lane workgroups in dispatch order
+        TreeArgs b = a;
+        b.xg = -1;
+        return run_tree<O_SUM, float, float, false, true, 0, 1, false, 64>(b, ns, out, n, s);
+    }
     case 15:     // 64-lane workgroups, non-temporal loads, dispatch order (k_combine_dram's geometry)
     case 16:     // 64-lane workgroups, non-temporal loads, XCD-contiguous
         if (!a.chain && a.pairmask == 0 && a.nleaves == a.P && a.P == 8) {

@@ -46,10 +46,11 @@ def timed(fn, reps=10):
 
 
 out = {}
-modes = [(0, "default"), (8, "generic"), (1, "generic_upfront"), (4, "fixed_u1"), (5, "fixed_u2"),
+modes = [(0, "default"), (8, "generic"), (1, "generic_upfront"), (2, "generic_upfront_nt"), (3, "generic_nt"),
+         (4, "fixed_u1"), (5, "fixed_u2"),
          (6, "fixed_u4"), (7, "fixed_u2_nt"), (9, "fixed_u1_order"), (10, "fixed_u1_b512"),
          (11, "fixed_u1_b1024"), (12, "fixed_u1_nt"), (13, "fixed_u4_nt"), (14, "fixed_u1_nt_order"),
-         (15, "fixed_u1_nt_b64_dispatch"), (16, "fixed_u1_nt_b64_xcd")]
+         (15, "fixed_u1_nt_b64_dispatch"), (16, "fixed_u1_nt_b64_xcd"), (17, "generic_nt_b64_dispatch")]
 if os.environ.get("TREE_MODES"):
     keep = {int(m) for m in os.environ["TREE_MODES"].split(",")}
     modes = [(m, n) for m, n in modes if m in keep]

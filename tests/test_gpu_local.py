@@ -387,7 +387,7 @@ def test_tree_tuning_modes_agree(L):
     for offset in (0, 4):
         dv = [_dev(x, offset if r == 3 else 0) for r, x in enumerate(xs)]
         arr = (ctypes.c_void_p * 8)(*[d[1] for d in dv])
-        for mode in range(17):
+        for mode in range(18):
             for cap in (0, 1024):
                 assert L.msx_tune_tree(mode, cap) == 0
                 out = torch.zeros(n, dtype=torch.float32, device="cuda")
