@@ -66,6 +66,29 @@ for mib in sizes:
                     key = f"{mib}/{name}/{label}/{'grid_stride' if mode == 1 else 'tile'}"
                     out.setdefault(key, []).append(round(ms * 1e3, 1))
         del packed, ref
+    # the run-parallel kernel (k_dt_runs: 3-D fp32 subarray with 1536-B rows, the
+    # bench's shape scaled along the outer dimension): one geometry, timed alone
+    if os.environ.get("PACK_SUBARRAY", "1") == "1":
+        ia = lambda v: (ctypes.c_int * len(v))(*v)
+        d0 = nf // (512 * 512)
+        dims, sub, st = (d0, 512, 512), (d0 * 3 // 4, 400, 384), (d0 // 8, 56, 64)
+        t3 = ctypes.c_int()
+        assert L.MPI_Type_create_subarray(3, ia(dims), ia(sub), ia(st), C.MPI_ORDER_C, C.MPI_FLOAT,
+                                          ctypes.byref(t3)) == 0
+        assert L.MPI_Type_commit(ctypes.byref(t3)) == 0
+        nb = sub[0] * sub[1] * sub[2] * 4
+        packed = torch.empty(nb, dtype=torch.uint8, device=dev)
+        want = typed.view(*dims)[st[0]:st[0] + sub[0], st[1]:st[1] + sub[1], st[2]:st[2] + sub[2]].contiguous()
+        torch.cuda.synchronize()
+        assert L.msx_pack_dev(typed.data_ptr(), 1, t3.value, packed.data_ptr(), sp) == 0
+        torch.cuda.synchronize()
+        out[f"{mib}/subarray3d_rows1536B/correct"] = bool(torch.equal(packed, want.view(-1).view(torch.uint8)))
+        for label, fn, a, b in (("pack", L.msx_pack_dev, typed, packed), ("unpack", L.msx_unpack_dev, packed, typed)):
+            ms = timed(lambda: fn(a.data_ptr(), 1, t3.value, b.data_ptr(), sp))
+            out[f"{mib}/subarray3d_rows1536B/{label}"] = {"us": round(ms * 1e3, 1),
+                                                          "frac": round(2 * nb / ms / 1e6 / HBM, 4)}
+        del packed, want
+        L.MPI_Type_free(ctypes.byref(t3))
     L.MPI_Type_free(ctypes.byref(vt))
     del typed
     torch.cuda.empty_cache()
