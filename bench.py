@@ -509,7 +509,8 @@ KERNEL_OF = {
                                     "unpack": "k_dt_pack<16, true, true, true>"},
     "double_int_records_12of16B": {"pack": "k_dt_pack<4, true, true, false>",
                                    "unpack": "k_dt_pack<4, true, true, true>"},
-    "subarray3d_fp32_rows1536B": {"pack": "k_dt_runs<16, false>", "unpack": "k_dt_runs<16, true>"},
+    "subarray3d_fp32_rows1536B": {"pack": "k_dt_pack_tile<16, true, true, false>",
+                                  "unpack": "k_dt_pack_tile<16, true, true, true>"},
 }
 
 

@@ -376,8 +376,17 @@ hipError_t run_copy(const CopyArgs& a, bool reg, hipStream_t s)
 {
     const bool narrow = a.ngran < (int64_t)0xffffffffll;
     const dim3 block(kPackBlock);
-    // long runs: irregular tables, or a two-level regular layout (3-D subarrays)
-    if ((!reg || a.n1) && a.gsize >= kRunParallelMin * a.nruns) {
+    // Two-level regular layouts (2-D / 3-D subarrays) map granules by two
+    // magic-number divisions in the tile form, which beats the wave-per-run
+    // kernel at every size measured (3-D fp32 subarray, 1536-B rows, runs ->
+    // tile: 256 MiB pack 35.0 -> 34.3 us, unpack 37.7 -> 37.1; 2 GiB pack
+    // 348.5 -> 313.5, unpack 378.4 -> 347.4; scripts/pack_size_probe.py,
+    // profiles/r03/pack_geometry/).  msx_tune_pack 1 keeps the wave-per-run
+    // kernel for them, 2 forces the tile form for every layout.
+    const bool two_level = reg && a.n1 != 0;
+    const bool tile_first = g_pack_mode == 2 || (g_pack_mode == 0 && two_level);
+    // long runs: irregular tables, or a two-level regular layout under mode 1
+    if (!tile_first && (!reg || a.n1) && a.gsize >= kRunParallelMin * a.nruns) {
         const int64_t units = (a.ngran / a.gsize) * a.nruns;
         const int64_t want = (units + kPackBlock / 64 - 1) / (kPackBlock / 64);
         const dim3 grid((unsigned)(want < 8192 ? want : 8192));
@@ -385,7 +394,7 @@ hipError_t run_copy(const CopyArgs& a, bool reg, hipStream_t s)
         return hipGetLastError();
     }
     const size_t span = (size_t)(a.ngran / a.gsize) * (size_t)a.extent + (size_t)a.ngran * G;
-    if (g_pack_mode == 2 || (g_pack_mode == 0 && span > pack_tile_min())) {
+    if (tile_first || (g_pack_mode == 0 && span > pack_tile_min())) {
         const int64_t want = (a.ngran + 64 * kUnroll - 1) / (64 * kUnroll);
         if (want <= 0x7fffffffll) {
             const dim3 tg((unsigned)want), tb(64);

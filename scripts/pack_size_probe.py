@@ -83,10 +83,19 @@ for mib in sizes:
         assert L.msx_pack_dev(typed.data_ptr(), 1, t3.value, packed.data_ptr(), sp) == 0
         torch.cuda.synchronize()
         out[f"{mib}/subarray3d_rows1536B/correct"] = bool(torch.equal(packed, want.view(-1).view(torch.uint8)))
-        for label, fn, a, b in (("pack", L.msx_pack_dev, typed, packed), ("unpack", L.msx_unpack_dev, packed, typed)):
-            ms = timed(lambda: fn(a.data_ptr(), 1, t3.value, b.data_ptr(), sp))
-            out[f"{mib}/subarray3d_rows1536B/{label}"] = {"us": round(ms * 1e3, 1),
-                                                          "frac": round(2 * nb / ms / 1e6 / HBM, 4)}
+        for rnd in range(2):
+            for mode, mname in ((1, "runs"), (2, "tile")):
+                assert L.msx_tune_pack(mode) == 0
+                assert L.msx_pack_dev(typed.data_ptr(), 1, t3.value, packed.data_ptr(), sp) == 0
+                torch.cuda.synchronize()
+                if not torch.equal(packed, want.view(-1).view(torch.uint8)):
+                    out[f"{mib}/subarray3d_rows1536B/{mname}/mismatch"] = True
+                for label, fn, a, b in (("pack", L.msx_pack_dev, typed, packed),
+                                        ("unpack", L.msx_unpack_dev, packed, typed)):
+                    ms = timed(lambda: fn(a.data_ptr(), 1, t3.value, b.data_ptr(), sp))
+                    out.setdefault(f"{mib}/subarray3d_rows1536B/{label}/{mname}", []).append(
+                        {"us": round(ms * 1e3, 1), "frac": round(2 * nb / ms / 1e6 / HBM, 4)})
+        assert L.msx_tune_pack(0) == 0
         del packed, want
         L.MPI_Type_free(ctypes.byref(t3))
     L.MPI_Type_free(ctypes.byref(vt))
