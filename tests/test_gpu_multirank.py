@@ -54,6 +54,12 @@ def fromdev(t, like, n=None):
 
 def check(tag, got, exp):
     if got.tobytes() != exp.tobytes():
+        # where it differs (element ranges), for diagnosing a mismatch from one run
+        g, e = np.frombuffer(got.tobytes(), np.uint8), np.frombuffer(exp.tobytes(), np.uint8)
+        if g.size == e.size and exp.itemsize:
+            bad = np.nonzero(g.reshape(-1, exp.itemsize) != e.reshape(-1, exp.itemsize))[0]
+            bad = np.unique(bad)
+            tag = f"{tag} [{bad.size} differ, first {bad[0]} last {bad[-1]}]" if bad.size else tag
         fails.append(tag)
 
 def inputs(op, dt, count, seed):
