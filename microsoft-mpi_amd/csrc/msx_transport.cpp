@@ -1298,20 +1298,23 @@ size_t sub_skew(size_t per_rank)
     return (per_rank / 16) & ~(size_t)255;
 }
 
-// usable bytes of one sub-slot of a window with chunk C over p ranks: the
-// whole C/p, so p sub-slots hold a full chunk (the skew is added on top, see
-// in_bytes).  Rounds 1-3 carved the skew out of C/p, so a chunk held
-// C - p*68 KiB and a 1 GiB allreduce took 3 chunks instead of 2, the last of
-// them ~1 MiB long but paying a chunk's five synchronisation points.
+// usable bytes of one sub-slot of a window with chunk C over p ranks: C/p
+// minus the skew, so the IN area is exactly C.  (Late round 3 tried the whole
+// C/p with the skew on top -- c3's 1 GiB in 2 chunks instead of 3, 1.93 ->
+// 1.88 ms on the shared-GPU rehearsal -- and reverted it: the only wrong
+// results seen in round 3, in the 8-ranks-on-one-GPU stress, appeared after
+// that change; DESIGN.md §2 "Open issue".)
 size_t sub_len(size_t C, int p)
 {
-    return (C / (size_t)p) & ~(size_t)255;
+    const size_t per = C / (size_t)p;
+    return (per - sub_skew(per)) & ~(size_t)255;
 }
 
-// IN area of a window: p sub-slots of sub_len, sub_skew apart
+// IN area of a window: p sub-slots sub_skew apart, C bytes in all
 size_t in_bytes(size_t C, int p)
 {
-    return (size_t)p * (sub_len(C, p) + sub_skew(C / (size_t)p));
+    (void)p;
+    return C;
 }
 
 struct Windows {
