@@ -1425,9 +1425,9 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
     w->Q = sub_len(w->C, tp->size);
     w->S = w->Q + sub_skew(w->C / (size_t)tp->size);
     w->I = in_bytes(w->C, tp->size);
-    // [IN: p sub-slots][OUT: C][flags]; at most 17/16 C + C + 64 KiB, below
-    // the 2 GiB IPC mapping limit for C <= 960 MiB (checked: a larger
-    // allocation would hang hipIpcOpenMemHandle, see map_peers)
+    // [IN: p sub-slots, C bytes][OUT: C][flags]: 2 C + 64 KiB, below the
+    // 2 GiB IPC mapping limit for C <= 960 MiB (checked: a larger allocation
+    // would hang hipIpcOpenMemHandle, see map_peers)
     if (w->I + w->C + kFlagBytes > ((size_t)2046 << 20)) {
         set_error("window of %zu bytes exceeds the IPC mapping limit (MSX_CHUNK_BYTES too large)",
                   w->I + w->C + kFlagBytes);
