@@ -335,50 +335,56 @@ PER_OP = [
 ]
 
 
-def cpu_baseline_collectives(p=8, seconds_each=2.0):
-    """The reference's collective schedules restated on the CPU
-    (oracle/msx_oracle_sched.c, from mpid/reduce.cpp: Rabenseifner allreduce,
-    recursive-halving reduce_scatter), p ranks simulated in lock step on ONE
-    core with memcpy as the transport: the combine + copy work of a p-rank
-    MS-MPI job, serialised.  Bounded samples (SURVEY.md §8(d) CPU baseline for
-    c3-c5): 16 MiB per rank for c3 / c5, a 64 MiB sendbuf per rank for c4 --
-    with the simulator's per-rank scratch, 0.5-1 GiB of host memory per call,
-    far above the LLC, so the memory-bound rate does not depend on the size;
-    median of >= 20 calls after 3 warm-ups.
-    busBW uses the same formulas as the GPU numbers (S/t·2(p-1)/p, S/t·(p-1)/p)."""
-    import numpy as np
+def _mem_available():
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 16 << 30
+
+
+def cpu_baseline_collectives(p=8, reps=3):
+    """The reference's collective schedules on the host CPU with p THREADS as
+    the p ranks (oracle/msx_oracle_threads.c, restated from mpid/reduce.cpp:
+    Rabenseifner allreduce :3927-4066, recursive-halving reduce_scatter
+    :917-1219 -- the branch c4's wrapped 32-bit byte count selects), each
+    thread running its own rank's step loop with memcpy from the peer's buffer
+    as the transport and oracle_reduce_local as MPID_Uop_call: what a p-rank
+    MS-MPI job on one host computes, SURVEY.md §8(d).  At the configs' own
+    per-rank sizes (c3 1 GiB fp32 SUM, c4 4 GiB MAX fp64 send buffer, c5
+    512 MiB BAND u64) unless host memory is short, then halved until the
+    footprint (send + recv + tmp per rank) fits half of MemAvailable; the
+    median of `reps` calls (inputs refilled outside the timed region),
+    checked against the closed form.  busBW uses the GPU formulas
+    (S/t*2(p-1)/p for allreduce, S/t*(p-1)/p for reduce_scatter)."""
     import oracle
     import msx
     C = msx.C
-    rng = np.random.default_rng(0x5EED)
-
-    def timed(fn):
-        return _median_rate(fn, 0, seconds_each)
-
-    out = {"ranks_simulated": p, "cores": 1, "kind": "port"}
-    n = 1 << 22
-    send = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(p)]
-    recv = [np.empty(n, np.float32) for _ in range(p)]
-    t, k = timed(lambda: oracle.allreduce(C.MPI_SUM, C.MPI_FLOAT, send, recv))
-    S = n * 4
-    out["c3_allreduce_sum_f32"] = {"bytes_per_rank": S, "seconds": round(t, 5), "calls": k,
-                                   "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 3)}
-    del send, recv
-    per = (1 << 23) // p
-    send = [rng.integers(0, 1000003, per * p).astype(np.float64) for _ in range(p)]
-    recv = [np.empty(per, np.float64) for _ in range(p)]
-    t, k = timed(lambda: oracle.reduce_scatter(C.MPI_MAX, C.MPI_DOUBLE, [per] * p, send, recv))
-    S = per * p * 8
-    out["c4_reduce_scatter_max_f64"] = {"bytes_per_rank": S, "seconds": round(t, 5), "calls": k,
-                                        "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 3)}
-    del send, recv
-    n = 1 << 21
-    send = [rng.integers(0, 2**63 - 1, n, dtype=np.int64).astype(np.uint64) for _ in range(p)]
-    recv = [np.empty(n, np.uint64) for _ in range(p)]
-    t, k = timed(lambda: oracle.allreduce(C.MPI_BAND, C.MPI_UINT64_T, send, recv))
-    S = n * 8
-    out["c5_allreduce_band_u64"] = {"bytes_per_rank": S, "seconds": round(t, 5), "calls": k,
-                                    "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 3)}
+    avail = _mem_available()
+    out = {"ranks": p, "threads": p, "cores": p, "kind": "port",
+           "transport": "one memcpy per MPIC_Sendrecv (the reference's shared-memory channel copies twice)",
+           "mem_available_GiB": round(avail / 2**30, 1)}
+    cfgs = (("c3_allreduce_sum_f32", 0, C.MPI_SUM, C.MPI_FLOAT, 4, 1 << 28, 3.0, 2.0),
+            ("c4_reduce_scatter_max_f64", 1, C.MPI_MAX, C.MPI_DOUBLE, 8, (4 << 30) // 8 // p, 2.5, 1.0),
+            ("c5_allreduce_band_u64", 0, C.MPI_BAND, C.MPI_UINT64_T, 8, 1 << 26, 3.0, 2.0))
+    for name, which, op, dt, esz, count, foot, bus in cfgs:
+        full = count
+        per_rank_vec = count * (p if which == 1 else 1) * esz          # S: the rank's input bytes
+        while count > 1024 and p * foot * (count * (p if which == 1 else 1) * esz) > avail / 2:
+            count //= 2
+        rc, ts = oracle.coll_threads(which, op, dt, p, count, reps)
+        ts = sorted(ts)
+        t = ts[len(ts) // 2]
+        S = count * (p if which == 1 else 1) * esz
+        out[name] = {"bytes_per_rank": S, "config_bytes_per_rank": per_rank_vec,
+                     "scaled": count != full, "seconds": round(t, 5), "calls": reps,
+                     "correct": rc == 0,
+                     "busbw_GB_s": round(S / t / 1e9 * bus * (p - 1) / p, 3)}
+        if rc:
+            out[name]["rc"] = rc
     return out
 
 
@@ -590,7 +596,7 @@ def pack_roofline(L, C, torch, dev, stream):
     return out
 
 
-def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12):
+def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12, mixes=True):
     """The headline launch with the Infinity Cache cold.  MI355X has a 256 MiB
     memory-side cache (MALL); back to back on the same 256 MiB operands it
     serves part of every launch (scripts/mall_probe.py: 256 MiB 115 us warm vs
@@ -632,8 +638,8 @@ def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12):
     a2.random_(0, 256)
     b2.random_(0, 256)
     torch.cuda.synchronize()
-    mixes = {}
-    for mode, name, streams in ((2, "copy_r1w1", 2), (0, "read2", 2)):
+    kinds, mixes = (((2, "copy_r1w1", 2), (0, "read2", 2)) if mixes else ()), {}
+    for mode, name, streams in kinds:
         pt = []
         for _ in range(reps):
             L.msx_probe_hbm(3, flush.data_ptr(), flush.data_ptr(), flush.numel(), sp)
@@ -994,7 +1000,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_per_op:
         rma = rma_self_roofline(L, C, torch, dev, n)
         probe = hbm_ceiling_probe(L, torch, dev, stream, n * 4)
-        cold = cold_cache_launch(L, C, torch, dev, stream, step, n)
+    if rank == 0:
+        # SURVEY.md §7 "use cold buffers": the headline launch with the Infinity
+        # Cache flushed first, reported in `roofline` beside the back-to-back frac
+        cold = cold_cache_launch(L, C, torch, dev, stream, step, n, mixes=(world == 1 and not args.no_per_op))
 
     if rank == 0:
         total_bytes = world * args.steps * n * BYTES_PER_ELEM
@@ -1029,6 +1038,15 @@ def main():
                          "kernel_us_mean_max_rank": round(kern_ms_max * 1e3, 2),
                          "kernel_us_mean_per_rank": [round(k * 1e3, 2) for k in kern_all]},
         }
+        if cold is not None and "cold_frac" in cold:
+            # the same kernel body with the 256 MiB Infinity Cache flushed before
+            # each launch: the DRAM-only fraction (the >= 70 % target is against it)
+            out["roofline"].update({"frac_cold": cold["cold_frac"], "achieved_cold": cold["cold_GB_s"],
+                                    "kernel_us_cold": cold["cold_us"],
+                                    "cold_method": "median of 12 single launches, each after a 1 GiB read + "
+                                                   "write pass over other data (flushes the 256 MiB MALL); "
+                                                   "kernel symbol k_combine_rr<3, float, float, 1, 256, true, "
+                                                   "false, 0> (the default body under its probe name)"})
         if host is not None:
             out["host_path"] = host
         def summarize(c):
@@ -1074,8 +1092,20 @@ def main():
             del src, acc
             torch.cuda.empty_cache()
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
+            hp = out.get("host_path", {}).get("pageable_by_size_fp32_sum")
+            cb = out["cpu_baseline"].get("by_size_fp32_sum")
+            if hp and cb:
+                # the smallest pageable host operand size at which the offload beats
+                # one core running the reference loop (INTEGRATION.md §2 routes
+                # host operands of the op table to that loop)
+                sizes = sorted(int(k) for k in hp if str(k) in cb)
+                wins = [b for b in sizes if hp[str(b)]["us"] < cb[str(b)]["us_1core"]]
+                out["host_path"]["crossover"] = {
+                    "bytes_offload_beats_1core": wins[0] if wins else None,
+                    "per_size_us_offload_vs_1core": {str(b): [hp[str(b)]["us"], cb[str(b)]["us_1core"]]
+                                                     for b in sizes}}
             if not args.no_collectives:
-                out["cpu_baseline_collectives"] = cpu_baseline_collectives(8, min(2.0, args.cpu_seconds))
+                out["cpu_baseline_collectives"] = cpu_baseline_collectives(8)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -89,6 +89,12 @@ void msx_op_maxloc(void* in, void* inout, int* len, MPI_Datatype* dt);
 void msx_op_replace(void* in, void* inout, int* len, MPI_Datatype* dt);   /* MPIR_Op_replace op.cpp:1886 */
 void msx_op_noop(void* in, void* inout, int* len, MPI_Datatype* dt);      /* MPIR_Op_noop op.cpp:1906 */
 MPI_User_function* msx_op_table(MPI_Op op);
+/* 1 when both operands are device memory (HBM, managed or IPC-mapped), else 0
+ * (host memory, NULL, or no GPU).  The routing test of the table binding
+ * (INTEGRATION.md section 2): device operands go to msx_op_table(op); host
+ * operands keep the reference's own MPIR_Op_<op> loop, which beats an offload
+ * below ~1 MiB (bench.py host_path.crossover).  Never initialises a GPU. */
+int msx_operands_on_device(const void* in, const void* inout);
 /* op_errno of the calling thread (Mpi.CallState->op_errno,
  * include/MpiCallState.h:13) and its reset (reduce.cpp:97, 3794) */
 int msx_op_errno(void);

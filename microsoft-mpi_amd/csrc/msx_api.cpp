@@ -2363,6 +2363,16 @@ MSX_EXPORT MPI_User_function* msx_op_table(MPI_Op op)
     return kTable[idx - 1];
 }
 
+// The routing test of the table binding: both operands in
+// device memory.  Host operands stay on the reference's own MPIR_Op_<op> loop,
+// which the offload beats only above ~1 MiB (bench.py host_path.crossover);
+// the library itself has no CPU combine.  No GPU -> 0, without initialising one.
+MSX_EXPORT int msx_operands_on_device(const void* in, const void* inout)
+{
+    if (!in || !inout || device_count_noinit() <= 0) return 0;
+    return classify(in).place == Place::Device && classify(inout).place == Place::Device ? 1 : 0;
+}
+
 // Mpi.CallState->op_errno of the calling thread: read it, and clear it before
 // a sequence of calls (the collectives do `op_errno = 0`, reduce.cpp:97,3794).
 MSX_EXPORT int msx_op_errno(void) { return t_op_errno; }

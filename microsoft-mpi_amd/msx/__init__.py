@@ -164,6 +164,7 @@ def lib():
         "msx_device_count": (i, []),
         "msx_last_error": (ctypes.c_char_p, []),
         "msx_op_check": (i, [i, i]),
+        "msx_operands_on_device": (i, [p, p]),
         "msx_type_size": (i, [i]),
         "msx_reduce_local_dev": (i, [p, p, i64, i, i, p]),
         "msx_pack_dev": (i, [p, i64, i, p, p]),

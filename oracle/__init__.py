@@ -55,6 +55,8 @@ def lib():
     L.oracle_ireduce.argtypes = [i, i, i, i, i64, ctypes.POINTER(p), p]
     L.oracle_reduce_scatter.restype = i
     L.oracle_reduce_scatter.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(p), ctypes.POINTER(p)]
+    L.oracle_coll_threads.restype = i
+    L.oracle_coll_threads.argtypes = [i, i, i, i, i64, i, ctypes.POINTER(ctypes.c_double)]
     _lib = L
     return L
 
@@ -126,3 +128,12 @@ def scan(op, dt, sendbufs, recvbufs, exclusive=False):
     S = (ctypes.c_void_p * p)(*[_addr(b) for b in sendbufs])
     R = (ctypes.c_void_p * p)(*[_addr(b) for b in recvbufs])
     return lib().oracle_scan(op, dt, p, sendbufs[0].size, 1 if exclusive else 0, S, R)
+
+
+def coll_threads(which, op, dt, p, count, reps):
+    """p threads as p ranks run the reference's collective step loop
+    (msx_oracle_threads.c): which 0 = allreduce, 1 = reduce_scatter_block.
+    Returns (rc, [seconds per call])."""
+    t = (ctypes.c_double * reps)()
+    rc = lib().oracle_coll_threads(which, op, dt, p, count, reps, t)
+    return rc, list(t)

@@ -84,6 +84,14 @@ int oracle_iallreduce(MPI_Op op, MPI_Datatype dt, int p, int64_t count,
 int oracle_ireduce(MPI_Op op, MPI_Datatype dt, int p, int root, int64_t count,
                    const void* const* sendbufs, void* recvbuf_root);
 
+/* CPU baseline of the collective configs (msx_oracle_threads.c): p threads as
+ * the p ranks of one host running the reference's step loop for their own
+ * rank.  which 0: Rabenseifner allreduce of `count` elements per rank;
+ * which 1: recursive-halving reduce_scatter_block of `count` per rank.
+ * p a power of two; dt MPI_FLOAT / MPI_DOUBLE / MPI_UINT64_T.  times[rep]
+ * receives each call's seconds; the result is checked on a sample. */
+int oracle_coll_threads(int which, MPI_Op op, MPI_Datatype dt, int p, int64_t count, int reps, double* times);
+
 #ifdef __cplusplus
 }
 #endif

@@ -185,6 +185,12 @@ int main(int argc, char** argv)
         msx_op_errno_reset();
         if (msx_op_errno() != 0) { fprintf(stderr, "op_errno reset\n"); ++fails; }
     }
+    /* the binding's routing test: device pairs only */
+    if (msx_operands_on_device(din, dio) != 1 || msx_operands_on_device(hin, dio) != 0 ||
+        msx_operands_on_device(din, hio) != 0 || msx_operands_on_device(NULL, dio) != 0) {
+        fprintf(stderr, "msx_operands_on_device\n");
+        ++fails;
+    }
     /* host operands: offloaded like MPI_Reduce_local; MPI_REPLACE copies */
     {
         fill(MPI_DOUBLE, hin, n); fill(MPI_DOUBLE, hio, n);

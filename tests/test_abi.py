@@ -229,6 +229,10 @@ def test_op_table_entries_without_gpu(msxlib):
     fr = UF(L.msx_op_table(C.MPI_REPLACE))
     fr(a.ctypes.data, b.ctypes.data, ctypes.byref(n), ctypes.byref(dt))
     assert L.msx_op_errno() == 0 and (b == a).all()
+    # the binding's routing test: host operands stay on the
+    # reference's own loop, NULL is never "device"
+    assert L.msx_operands_on_device(a.ctypes.data, b.ctypes.data) == 0
+    assert L.msx_operands_on_device(None, b.ctypes.data) == 0
     if L.msx_device_count() == 0:
         x = np.ones(8, np.float32)
         y = np.full(8, 2, np.float32)

@@ -25,3 +25,37 @@ def test_cpu_info_and_median_helpers():
     calls = []
     t, k = bench._median_rate(lambda: calls.append(1), 0, 0.0)
     assert k == 20 and len(calls) == 23 and t >= 0          # 3 warm-ups + 20 timed
+
+
+def test_threaded_collective_baseline_is_correct():
+    """oracle/msx_oracle_threads.c (bench.py cpu_baseline_collectives): p
+    threads as ranks run the reference's Rabenseifner allreduce / recursive-
+    halving reduce_scatter_block step loops; ragged counts (count % p != 0) and
+    p = 2, 4, 8 must give the closed-form result on every rank."""
+    sys.path.insert(0, REPO)
+    import oracle
+    C = msx.C
+    for which, op, dt in ((0, C.MPI_SUM, C.MPI_FLOAT), (0, C.MPI_BAND, C.MPI_UINT64_T),
+                          (1, C.MPI_MAX, C.MPI_DOUBLE)):
+        for p in (2, 4, 8):
+            for count in (p, 1000 + p - 1, (1 << 16) + 3):
+                rc, ts = oracle.coll_threads(which, op, dt, p, count, 2)
+                assert rc == 0, (which, p, count, rc)
+                assert len(ts) == 2 and all(t > 0 for t in ts)
+    # refused: non-power-of-two p, unsupported type
+    assert oracle.coll_threads(0, C.MPI_SUM, C.MPI_FLOAT, 6, 1000, 1)[0] == C.MPI_ERR_ARG
+    assert oracle.coll_threads(0, C.MPI_SUM, C.MPI_INT, 8, 1000, 1)[0] == C.MPI_ERR_ARG
+
+
+def test_cpu_baseline_collectives_scales_to_memory(monkeypatch):
+    """At the configs' sizes when host memory allows, halved otherwise; each
+    entry states its size, threads and busBW (VERDICT r03 'Next' 7)."""
+    sys.path.insert(0, REPO)
+    import bench
+    monkeypatch.setattr(bench, "_mem_available", lambda: 3 << 30)   # force scaling on this host
+    out = bench.cpu_baseline_collectives(8, reps=1)
+    assert out["threads"] == 8 and out["kind"] == "port"
+    for k in ("c3_allreduce_sum_f32", "c4_reduce_scatter_max_f64", "c5_allreduce_band_u64"):
+        e = out[k]
+        assert e["correct"] and e["busbw_GB_s"] > 0 and e["scaled"], e
+        assert e["bytes_per_rank"] < e["config_bytes_per_rank"]
