@@ -122,6 +122,13 @@ int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count
 
 /* benchmark knobs for the fp32 SUM hot path: variant index (0 = default) and
  * a cap on workgroups (0 = one tile per workgroup). */
+/* Any reference-order tree the engine evaluates: P leaves (power of two <= 16)
+ * over srcs[2k] and, when bit k of pairmask is set, its fold pair srcs[2k+1]
+ * (leaf k = op(srcs[2k] as inout, srcs[2k+1] as in)); leaves >= nleaves absent
+ * (0 = all); or with chain != 0 the left-deep chain over srcs[0..P-1].
+ * Stream-ordered, device pointers (tests and probes of the tree kernels). */
+int msx_reduce_tree_spec_dev(const void* const* srcs, int P, unsigned pairmask, int nleaves, int chain,
+                             void* out, int64_t count, MPI_Datatype datatype, MPI_Op op, void* stream);
 int msx_tune_set(int variant, int grid_cap);
 int msx_tune_variant_count(void);
 /* collective tree combine (msx_reduce_tree_dev and the engine), fp32 SUM only:

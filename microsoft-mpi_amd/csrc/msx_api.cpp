@@ -2415,6 +2415,39 @@ MSX_EXPORT int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, in
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "tree kernel launch");
 }
 
+// Any reference-order tree the engine evaluates (TreeSpec): P leaves (a power
+// of two <= 16) over srcs[2k] (leaf k) and srcs[2k+1] (its fold pair when bit
+// k of pairmask is set), leaves >= nleaves absent (0 = all present); or, with
+// chain set, the left-deep chain over srcs[0..P-1].  Stream-ordered, device
+// pointers.  For tests and probes of the tree kernels outside a collective.
+MSX_EXPORT int msx_reduce_tree_spec_dev(const void* const* srcs, int P, unsigned pairmask, int nleaves, int chain,
+                                        void* out, int64_t count, MPI_Datatype dt, MPI_Op op, void* stream)
+{
+    if (count == 0) return MPI_SUCCESS;
+    OpRef r;
+    int rc = v_op(op, dt, &r);
+    if (rc != MPI_SUCCESS) return rc;
+    if (r.opidx == O_NULL) { set_error("device entry point takes builtin ops only"); return MPI_ERR_OP; }
+    if (count < 0) { set_error("negative count"); return MPI_ERR_COUNT; }
+    const bool pow2 = P >= 1 && P <= 16 && (P & (P - 1)) == 0;
+    if (!srcs || !out || (chain ? (P < 1 || P > 16) : !pow2) || nleaves < 0 || nleaves > P ||
+        (!chain && (pairmask >> P) != 0)) {
+        set_error("bad tree spec (P=%d pairmask=0x%x nleaves=%d chain=%d)", P, pairmask, nleaves, chain);
+        return MPI_ERR_ARG;
+    }
+    rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    TreeSpec t;
+    t.P = P;
+    t.chain = chain != 0;
+    t.pairmask = chain ? 0 : pairmask;
+    t.nleaves = chain ? 0 : nleaves;
+    const int ns = chain ? P : 2 * P;
+    for (int i = 0; i < ns; ++i) t.src[i] = srcs[i];
+    hipError_t e = launch_tree_spec(r.opidx, type_info(dt)->kind, t, out, (size_t)count, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "tree kernel launch");
+}
+
 MSX_EXPORT int msx_tune_set(int variant, int grid_cap)
 {
     if (variant < 0 || variant >= combine_variant_count() || grid_cap < 0) return MPI_ERR_ARG;

@@ -803,6 +803,27 @@ hipError_t launch_tree(int opidx, Kind k, const void* const* srcs, int p, void* 
 // the two-step pushes (k_push_wait) and tree results behind result-ready
 // flags.  MSX_WT_STORES=0 keeps plain stores (correct only while the peer
 // windows are mapped uncached on the writer).
+// Workgroup-level agent release before each completion count of a
+// flag-announced push / tree (wg_release, msx_tree_dev.h), MSX_WG_RELEASE=1.
+// Off by default: the pushed and result bytes are written through at system
+// scope (sc0 sc1) and every lane waits for their completion before its
+// workgroup counts itself -- the guide's valid write-through producer form --
+// and the per-workgroup buffer_wbl2 costs 5.7x at 64 MiB (2 ranks on one
+// MI355X, 2-step allreduce 123-131 -> 746-747 us; 4 KiB and 1 MiB within
+// noise; scripts/wg_release_ab.sh, profiles/r04/wg_release_ab.log).
+static bool wg_release_on()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_WG_RELEASE");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
+
+// the `sys` word of push_post_body / copy_post_body: 1 = system fences (cached
+// windows), 2 = workgroup release, 0 = store completion only
+static int post_mode(bool sys) { return sys ? 1 : (wg_release_on() ? 2 : 0); }
+
 static bool wt_stores()
 {
     static const bool on = [] {
@@ -871,11 +892,12 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         a.push_gx = (unsigned)gx;
         a.npush = (unsigned)(gx * (size_t)t.push_nseg);
         a.push_counter = t.push_counter;
-        a.push_sys = t.push_sys ? 1 : 0;
+        a.push_sys = post_mode(t.push_sys);
     }
     if (t.done_counter) {
         if (t.done_nflags < 0 || t.done_nflags > 64 || t.done_launches < 1) return hipErrorInvalidValue;
         a.done_counter = t.done_counter;
+        a.rel = wg_release_on() ? 1 : 0;
         // buffer-store offsets are 32-bit: larger ranges keep plain stores
         a.wt = (wt_stores() && n * kind_size(k) < ((size_t)1 << 32)) ? 1 : 0;
         a.done_launches = t.done_launches;
@@ -954,7 +976,7 @@ hipError_t launch_push_post(const void* const* src, void* const* dst, const size
     if (gx < 1) gx = 1;
     if (gx > 16) gx = 16;
     hipLaunchKernelGGL(k_push_post, dim3((unsigned)gx, (unsigned)nseg), dim3(256), 0, s, c, f, counter,
-                       (unsigned)(gx * (size_t)nseg), sys ? 1 : 0);
+                       (unsigned)(gx * (size_t)nseg), post_mode(sys));
     return hipGetLastError();
 }
 
@@ -1013,7 +1035,7 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     if (gx > cap) gx = cap;
     const unsigned total = nseg > 0 ? (unsigned)(gx * (size_t)nseg) : 0u;
     c.wt = (wt_stores() && maxb < ((size_t)1 << 32)) ? 1 : 0;   // 32-bit buffer offsets
-    hipLaunchKernelGGL(k_push_wait, dim3(total + 1), dim3(256), 0, s, c, f, counter, total, sys ? 1 : 0,
+    hipLaunchKernelGGL(k_push_wait, dim3(total + 1), dim3(256), 0, s, c, f, counter, total, post_mode(sys),
                        (unsigned)gx, wait_flags, seq, wait_n, wait_skip, wait_err, flag_wait_ticks(), wait_tag);
     return hipGetLastError();
 }

@@ -943,7 +943,7 @@ Worker& worker()
 int flag_timeout(const char* op, int me, int word, unsigned long long seq, bool index_is_rank = true)
 {
     const int tag = word >> 16, idx = (word & 0xffff) - 1;
-    const char* phase = tag == 2 ? "result" : "arrival";
+    const char* phase = tag == 2 ? "result" : (tag == 3 ? "half_free" : "arrival");
     set_error("flag timeout: op=%s rank=%d phase=%s peer=%d seq=%llu limit_s=%.1f", op, me, phase,
               index_is_rank ? idx : -1, seq, flag_wait_seconds());
     trace("%s", last_error());
@@ -1339,17 +1339,23 @@ constexpr size_t kResultFlags = 4096;
 // Scan partials' arrival flags: slot kScanFlags + k of window r = (call << 6)
 // | step of the last partial rank k pushed to r (only scan writes them).
 constexpr size_t kScanFlags = 2048;
+// GPU "done" flags of the pipelined two-step allreduce: slot kDoneFlags + k of
+// window r = the last chunk (flag sequence number) whose IN / OUT halves rank
+// k finished reading; a chunk two later may then overwrite them.
+constexpr size_t kDoneFlags = 6144;
 
 // Largest message (bytes) of the barrier-free two-step allreduce / reduce
-// (MSX_TWO_STEP_MAX; 0 = always the host-barrier schedule).  The default
-// takes it whenever the message fits the window halves: 2 ranks on one
-// MI355X (scripts/allreduce_probe.sh, profiles/r02/two_step_*) measured
+// (MSX_TWO_STEP_MAX; 0 = always the host-barrier schedule).  By default every
+// Rabenseifner-sized message takes it, longer ones as a GPU-synchronised
+// pipeline of window-half chunks (round 4; rounds 1-3 stopped at 256 MiB and
+// ran the rest through host barriers, five host syncs per chunk).  2 ranks on
+// one MI355X (scripts/allreduce_probe.sh, profiles/r02/two_step_*) measured
 // 1 MiB 62.6 -> 28.5 us, 4 MiB 64.3 -> 32.5, 16 MiB 75.6 -> 45.8,
 // 64 MiB 154.8 -> 133.0, 128 MiB 265 -> 249; 4 ranks 64 MiB 310 -> 254.
 size_t two_step_max()
 {
     static const size_t v = [] {
-        size_t b = (size_t)256 << 20;
+        size_t b = ~(size_t)0;
         if (const char* e = getenv("MSX_TWO_STEP_MAX")) b = (size_t)atoll(e);
         return b;
     }();
@@ -1947,15 +1953,17 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
     const bool rd_single = (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) &&
                            count * esz <= (Qh & ~(size_t)(16 * esz - 1));
-    // Rabenseifner in two GPU-synchronised steps (see below) when one chunk
-    // holds the message in half a sub-slot per piece and half the OUT area
-    // above the recursive-doubling results: only count, type, p and the
-    // environment decide, so every rank takes the same branch
+    // Rabenseifner in two GPU-synchronised steps per chunk (see below): a
+    // chunk is p pieces of at most half an IN sub-slot each and fits half the
+    // OUT area above the recursive-doubling results; a longer message runs as
+    // a pipeline of such chunks.  Only count, type, p and the environment
+    // decide, so every rank takes the same branch and the same chunks.
     const size_t qh_el = (Qh / esz) & ~(size_t)15;
-    const size_t piece_el = (((count + (size_t)p - 1) / (size_t)p) + 15) & ~(size_t)15;
     const size_t out_half = ((chunk_bytes() - Qh) / 2) & ~(size_t)255;
+    size_t pc_el = std::min((size_t)p * qh_el, out_half / esz);
+    pc_el -= pc_el % ((size_t)p * 16);                         // whole 16-element pieces
     const bool two_step = algo == A_RABENSEIFNER && p >= 2 && p <= 32 && rd_flags() && tp->has_done() &&
-                          count * esz <= two_step_max() && piece_el <= qh_el && count * esz <= out_half;
+                          count * esz <= two_step_max() && pc_el > 0;
     Windows w;
     if ((rc = get_windows(tp, &w, rd_single || two_step)) != MPI_SUCCESS) return rc;
     // host buffers: device aliases for the call (pinned in place of staging)
@@ -2144,107 +2152,139 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     if (two_step) {
         // Barrier-free Rabenseifner: the same pieces, trees and result
         // placement as the host-barrier schedule below, synchronised on the
-        // GPU.  Step 1: push piece r of my vector into rank r's IN half and
-        // post its arrival flag, while one workgroup waits for every peer's
-        // piece of mine (k_push_wait); then evaluate my piece (one launch per
-        // owner tree) into the OUT areas of all receivers, the last workgroup
-        // posting result-ready flags to them (tree_done).  Step 2
-        // (receivers): one workgroup waits for every peer's result flag, then
-        // the OUT half is copied into recvbuf.  One host sync.  Only single
-        // workgroups spin, so ranks sharing a GPU cannot starve each other.
-        // Halves alternate with rd_parity and are reused two flag calls later,
-        // guarded by wait_done as in the recursive-doubling path.
+        // GPU, chunk by chunk with no host synchronisation between chunks.
+        // Per chunk (elements [o, o + len), pieces cut in 16-element granules):
+        //  0. (chunks >= 2) one workgroup waits until every peer posted that it
+        //     finished chunk seq - 2 (its GPU "done" flag): the IN / OUT halves
+        //     this chunk writes are free.  The first two chunks of a call are
+        //     guarded on the host by the previous flag calls' post_done.
+        //  1. k_push_wait: piece r of my chunk -> rank r's IN half, then its
+        //     arrival flag; one workgroup waits for every peer's piece of mine.
+        //  2. my piece evaluated (one launch per owner tree, owners by GLOBAL
+        //     element, reduce.cpp:3941-4065) into the OUT half of every
+        //     receiver; the last workgroup posts result-ready flags (tree_done).
+        //  3. receivers: one workgroup waits for every peer's result flag,
+        //     then the OUT half is copied into recvbuf + o.
+        //  4. (when a later chunk of this call reuses the halves) my "done"
+        //     flag into every peer's window, after the copy in stream order.
+        // Halves alternate with rd_parity per chunk.  One host sync per call
+        // (rounds 1-3 paid five per 512 MiB chunk on the host-barrier path).
+        // Only single workgroups spin, so ranks sharing a GPU cannot starve
+        // each other's pushes.
         if (!tp->out_quiet && (rc = tp->barrier()) != MPI_SUCCESS) return rc;
-        const size_t half = (size_t)tp->rd_parity * Qh;
-        const size_t obase = Qh + (size_t)tp->rd_parity * out_half;
-        const size_t len = count;
-        auto lo_of = [&](int r) { return std::min(len, (size_t)r * piece_el); };
-        auto hi_of = [&](int r) { return std::min(len, (size_t)(r + 1) * piece_el); };
-        const char* mine = nullptr;
-        rc = device_view(bs, src, 0, len * esz, stage, s, &mine);
-        const unsigned long long seq = ++tp->rd_seq;
-        Segs sg;
-        std::vector<unsigned long long*> fl, done;
-        for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
-            if (r == me) continue;
-            if (seq > 2) rc = tp->wait_done(r, seq - 2);
-            if (hi_of(r) > lo_of(r)) {
-                sg.add(mine + lo_of(r) * esz, w.sub(r, me) + half, (hi_of(r) - lo_of(r)) * esz);
-                if (!fault_drop_flags(me, seq)) fl.push_back(w.flags(r) + me);
-            }
-        }
-        std::vector<int> dests;
-        if (want) dests.push_back(me);
-        for (int r = 0; r < p; ++r)
-            if (r != me && (root < 0 || r == root)) dests.push_back(r);
-        for (int d : dests)
-            if (d != me) done.push_back(w.flags(d) + kResultFlags + me);
         int* err_host = nullptr;
         int* err_dev = wait_err_word(&err_host);
         unsigned* counter = tp->push_counter();
         if (!err_dev || !counter) { set_error("allreduce: flag word allocation failed"); return MPI_ERR_NO_MEM; }
         *err_host = 0;
-        // my piece, cut where the owner tree changes (block boundaries)
-        const size_t plo = lo_of(me), phi = hi_of(me);
-        struct Range { size_t e0, e1; int owner; };
-        std::vector<Range> ranges;
-        for (size_t e0 = plo; e0 < phi;) {
-            const size_t rs = count / (size_t)pof2;
-            const int j = rs ? (int)std::min((size_t)pof2 - 1, e0 / rs) : pof2 - 1;
-            size_t bst, bl;
-            allreduce_block(p, count, j, &bst, &bl);
-            const size_t e1 = std::min(phi, bst + bl);
-            ranges.push_back({e0, e1, allreduce_block_owner(p, j)});
-            e0 = e1;
-        }
-        for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
-        subs[(size_t)me] = const_cast<char*>(mine) + plo * esz;
-        // step 1a: push my pieces and their arrival flags; one workgroup waits
-        // for the peers' pieces of mine (none when my piece is empty)
-        if (rc == MPI_SUCCESS) {
-            hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
-                                            fl.data(), (int)fl.size(), seq, sys_fences(), counter + kCountWords,
-                                            w.flags(me),
+        std::vector<int> dests;
+        if (want) dests.push_back(me);
+        for (int r = 0; r < p; ++r)
+            if (r != me && (root < 0 || r == root)) dests.push_back(r);
+        std::vector<unsigned long long*> done_to;            // my GPU done flag in every peer's window
+        for (int r = 0; r < p; ++r)
+            if (r != me) done_to.push_back(w.flags(r) + kDoneFlags + me);
+        const size_t nchunks = (count + pc_el - 1) / pc_el;
+        const size_t rs = count / (size_t)pof2;
+        unsigned long long seq = 0;
+        size_t nranges = 0;
+        for (size_t ci = 0; ci < nchunks && rc == MPI_SUCCESS; ++ci) {
+            const size_t o = ci * pc_el, len = std::min(pc_el, count - o);
+            const size_t pel = (((len + (size_t)p - 1) / (size_t)p) + 15) & ~(size_t)15;
+            auto lo_of = [&](int r) { return std::min(len, (size_t)r * pel); };
+            auto hi_of = [&](int r) { return std::min(len, (size_t)(r + 1) * pel); };
+            const size_t half = (size_t)tp->rd_parity * Qh;
+            const size_t obase = Qh + (size_t)tp->rd_parity * out_half;
+            const char* mine = nullptr;
+            rc = device_view(bs, src, o * esz, len * esz, stage, s, &mine);
+            seq = ++tp->rd_seq;
+            if (ci < 2) {
+                for (int r = 0; r < p && rc == MPI_SUCCESS; ++r)
+                    if (r != me && seq > 2) rc = tp->wait_done(r, seq - 2);
+            } else if (rc == MPI_SUCCESS) {
+                hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, false, nullptr,
+                                                w.flags(me) + kDoneFlags, p, me, err_dev, s, 3);
+                if (e != hipSuccess) rc = hip_fail(e, "allreduce half-free wait");
+            }
+            if (rc != MPI_SUCCESS) break;
+            Segs sg;
+            std::vector<unsigned long long*> fl, done;
+            for (int r = 0; r < p; ++r) {
+                if (r == me || hi_of(r) <= lo_of(r)) continue;
+                sg.add(mine + lo_of(r) * esz, w.sub(r, me) + half, (hi_of(r) - lo_of(r)) * esz);
+                if (!fault_drop_flags(me, seq)) fl.push_back(w.flags(r) + me);
+            }
+            for (int d : dests)
+                if (d != me) done.push_back(w.flags(d) + kResultFlags + me);
+            // my piece, cut where the owner tree changes (block boundaries of
+            // the whole vector)
+            const size_t plo = lo_of(me), phi = hi_of(me);
+            struct Range { size_t e0, e1; int owner; };
+            std::vector<Range> ranges;
+            for (size_t e0 = plo; e0 < phi;) {
+                const size_t ge = o + e0;
+                const int j = rs ? (int)std::min((size_t)pof2 - 1, ge / rs) : pof2 - 1;
+                size_t bst, bl;
+                allreduce_block(p, count, j, &bst, &bl);
+                const size_t e1 = std::min(phi, bst + bl - o);
+                ranges.push_back({e0, e1, allreduce_block_owner(p, j)});
+                e0 = e1;
+            }
+            nranges += ranges.size();
+            for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
+            subs[(size_t)me] = const_cast<char*>(mine) + plo * esz;
+            // step 1: push my pieces and their arrival flags; one workgroup
+            // waits for the peers' pieces of mine (none when my piece is empty)
+            hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(), fl.data(),
+                                            (int)fl.size(), seq, sys_fences(), counter + kCountWords, w.flags(me),
                                             ranges.empty() ? 0 : p, me, err_dev, s);
             if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
+            // step 2: my piece into every receiver's OUT half; the last
+            // workgroup of the last launch posts the result flags
+            if (rc == MPI_SUCCESS && ranges.empty() && !done.empty()) {
+                e = launch_post_flags(done.data(), (int)done.size(), seq, s);
+                if (e != hipSuccess) rc = hip_fail(e, "allreduce result flags");
+            }
+            for (size_t i = 0; i < ranges.size() && rc == MPI_SUCCESS; ++i) {
+                const Range& g = ranges[i];
+                const RankTree t = !is_reduce ? tree_allreduce(p, g.owner)
+                                              : (nbc ? tree_ireduce_rsag(p, g.owner, root) : tree_reduce_rsag(p, g.owner));
+                std::vector<char*> extra;
+                for (size_t d = 1; d < dests.size(); ++d) extra.push_back(w.out(dests[d]) + obase + g.e0 * esz);
+                TreeWait tw;
+                tw.done_counter = counter + 2 * kCountWords;
+                tw.done_launches = (unsigned)ranges.size();
+                tw.done_flags = &done;
+                tw.done_seq = seq;
+                rc = run_rank_tree(op.opidx, k, t, subs, esz, g.e0 - plo, g.e1 - g.e0,
+                                   w.out(dests[0]) + obase + g.e0 * esz, s, extra, &tw);
+            }
+            if (rc == MPI_SUCCESS && want) {
+                // step 3: every peer's result in my OUT half, then into recvbuf
+                e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq, false, nullptr,
+                                     w.flags(me) + kResultFlags, p, me, err_dev, s, 2);
+                if (e != hipSuccess) rc = hip_fail(e, "allreduce result wait");
+                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : dst;
+                if (rc == MPI_SUCCESS) rc = copy_async(out + o * esz, w.out(me) + obase, len * esz, s);
+            }
+            // step 4: this chunk's halves are free again (read by my trees and
+            // my copy, both earlier on the stream) -- only a later chunk of
+            // this call waits on it
+            if (rc == MPI_SUCCESS && ci + 2 < nchunks) {
+                e = launch_post_flags(done_to.data(), (int)done_to.size(), seq, s);
+                if (e != hipSuccess) rc = hip_fail(e, "allreduce done flags");
+            }
+            tp->rd_parity ^= 1;
         }
-        // step 1b: my piece into every receiver's OUT half; the last workgroup
-        // of the last launch posts the result flags
-        if (rc == MPI_SUCCESS && ranges.empty() && !done.empty()) {
-            hipError_t e = launch_post_flags(done.data(), (int)done.size(), seq, s);
-            if (e != hipSuccess) rc = hip_fail(e, "allreduce result flags");
-        }
-        for (size_t i = 0; i < ranges.size() && rc == MPI_SUCCESS; ++i) {
-            const Range& g = ranges[i];
-            const RankTree t = !is_reduce ? tree_allreduce(p, g.owner)
-                                          : (nbc ? tree_ireduce_rsag(p, g.owner, root) : tree_reduce_rsag(p, g.owner));
-            std::vector<char*> extra;
-            for (size_t d = 1; d < dests.size(); ++d) extra.push_back(w.out(dests[d]) + obase + g.e0 * esz);
-            TreeWait tw;
-            tw.done_counter = counter + 2 * kCountWords;
-            tw.done_launches = (unsigned)ranges.size();
-            tw.done_flags = &done;
-            tw.done_seq = seq;
-            rc = run_rank_tree(op.opidx, k, t, subs, esz, g.e0 - plo, g.e1 - g.e0,
-                               w.out(dests[0]) + obase + g.e0 * esz, s, extra, &tw);
-        }
-        if (rc == MPI_SUCCESS && want) {
-            // step 2: every peer's result in my OUT half, then into recvbuf
-            hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq, false, nullptr,
-                                            w.flags(me) + kResultFlags, p, me, err_dev, s, 2);
-            if (e != hipSuccess) rc = hip_fail(e, "allreduce result wait");
-            char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : dst;
-            if (rc == MPI_SUCCESS) rc = copy_async(out, w.out(me) + obase, len * esz, s);
-        }
-        const int rs = sync_stream(s, "allreduce two-step");
-        if (rc == MPI_SUCCESS) rc = rs;
+        const int rsy = sync_stream(s, "allreduce two-step");
+        if (rc == MPI_SUCCESS) rc = rsy;
         if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
             rc = flag_timeout(root < 0 ? "allreduce" : "reduce", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), seq);
         tp->post_done(seq);
-        tp->rd_parity ^= 1;
         tp->window_open = true;
         tp->out_quiet = true;
-        trace("allreduce: done (two-step, GPU flags, seq %llu, %zu ranges) rc=%d", seq, ranges.size(), rc);
+        trace("allreduce: done (two-step, GPU flags, %zu chunk(s), last seq %llu, %zu ranges) rc=%d", nchunks, seq,
+              nranges, rc);
         return rc;
     }
 
@@ -2376,15 +2416,18 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
         if (ncclComm_t rcomm = rccl_comm(tp)) return rccl_reduce_scatter(rcomm, c, sendbuf, recvbuf, recvcounts, dt, op);
     const Kind k = type_info(dt)->kind;
     hipStream_t s = tp->stream();
-    // One GPU-synchronised step when every block fits half an IN sub-slot
-    // (decided by recvcounts, type, p and the environment: the same on every
-    // rank): push block r of my input into rank r's IN half with its arrival
-    // flag while one workgroup waits for the peers' blocks of mine
-    // (k_push_wait), evaluate my block, one host sync.  Halves and reuse as
-    // in the two-step allreduce.
+    // GPU-synchronised rounds (decided by recvcounts, type, p and the
+    // environment: the same on every rank): in round k, slice k of block r of
+    // my input (at most half an IN sub-slot) goes into rank r's IN half with
+    // its arrival flag while one workgroup waits for the peers' slices of my
+    // block (k_push_wait), then my slice is evaluated.  One round when every
+    // block fits half a sub-slot; longer blocks (c4: 512 MiB per rank at
+    // p = 8) pipeline their rounds with GPU "half free" flags as the two-step
+    // allreduce does, one host sync per call instead of four per round.
     const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
+    const size_t qh_el = esz ? (Qh / esz) & ~(size_t)15 : 0;
     const bool one_step = p >= 2 && p <= 32 && rd_flags() && tp->has_done() && total * esz <= two_step_max() &&
-                          maxcnt <= ((Qh / esz) & ~(size_t)15);
+                          qh_el > 0;
     Windows w;
     if ((rc = get_windows(tp, &w, one_step)) != MPI_SUCCESS) return rc;
     // sub-slot k of IN(r) receives rank k's contribution to r's block, qe
@@ -2412,51 +2455,74 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
             scratch = dev_scratch(hold_b + stage_b);
             if (!scratch) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
         }
-        const size_t half = (size_t)tp->rd_parity * Qh;
-        const unsigned long long seq = ++tp->rd_seq;
-        std::vector<char*> subs((size_t)p);
-        Segs sg;
-        std::vector<unsigned long long*> fl;
-        for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
-            const size_t cnt = (size_t)recvcounts[r];
-            const char* v = nullptr;
-            if (cnt)
-                rc = device_view(bs, src, disp[r] * esz, cnt * esz, scratch ? scratch + hold_b + disp[r] * esz : nullptr,
-                                 s, &v);
-            if (r == me) { subs[(size_t)me] = const_cast<char*>(v); continue; }
-            subs[(size_t)r] = w.sub(me, r) + half;
-            if (rc == MPI_SUCCESS && seq > 2) rc = tp->wait_done(r, seq - 2);
-            if (cnt && rc == MPI_SUCCESS) {
-                sg.add(v, w.sub(r, me) + half, cnt * esz);
-                if (!fault_drop_flags(me, seq)) fl.push_back(w.flags(r) + me);
-            }
-        }
         int* err_host = nullptr;
         int* err_dev = wait_err_word(&err_host);
         unsigned* counter = tp->push_counter();
         if (!err_dev || !counter) { set_error("reduce_scatter: flag word allocation failed"); return MPI_ERR_NO_MEM; }
         *err_host = 0;
-        if (rc == MPI_SUCCESS) {
-            hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
-                                            fl.data(), (int)fl.size(), seq, sys_fences(), counter + kCountWords,
-                                            w.flags(me), mycnt ? p : 0, me, err_dev, s);
-            if (e != hipSuccess) rc = hip_fail(e, "reduce_scatter push");
+        std::vector<unsigned long long*> done_to;          // my GPU done flag in every peer's window
+        for (int r = 0; r < p; ++r)
+            if (r != me) done_to.push_back(w.flags(r) + kDoneFlags + me);
+        // in place, recvbuf still holds the input later rounds push: results via hold
+        char* out = in_place ? scratch : (bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me));
+        const bool out_window = !in_place && out == w.out(me);   // host recvbuf: round by round via OUT
+        const size_t nrounds = maxcnt ? (maxcnt + qh_el - 1) / qh_el : 1;
+        unsigned long long seq = 0;
+        std::vector<char*> subs((size_t)p);
+        for (size_t ri = 0; ri < nrounds && rc == MPI_SUCCESS; ++ri) {
+            const size_t o = ri * qh_el;
+            const size_t half = (size_t)tp->rd_parity * Qh;
+            seq = ++tp->rd_seq;
+            if (ri < 2) {
+                for (int r = 0; r < p && rc == MPI_SUCCESS; ++r)
+                    if (r != me && seq > 2) rc = tp->wait_done(r, seq - 2);
+            } else if (rc == MPI_SUCCESS) {
+                hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, false, nullptr,
+                                                w.flags(me) + kDoneFlags, p, me, err_dev, s, 3);
+                if (e != hipSuccess) rc = hip_fail(e, "reduce_scatter half-free wait");
+            }
+            Segs sg;
+            std::vector<unsigned long long*> fl;
+            for (int r = 0; r < p && rc == MPI_SUCCESS; ++r) {
+                const size_t cnt = (size_t)recvcounts[r];
+                const size_t len = o < cnt ? std::min(qh_el, cnt - o) : 0;
+                const char* v = nullptr;
+                if (len)
+                    rc = device_view(bs, src, (disp[r] + o) * esz, len * esz,
+                                     scratch ? scratch + hold_b + (disp[r] + o) * esz : nullptr, s, &v);
+                if (r == me) { subs[(size_t)me] = const_cast<char*>(v); continue; }
+                subs[(size_t)r] = w.sub(me, r) + half;
+                if (len && rc == MPI_SUCCESS) {
+                    sg.add(v, w.sub(r, me) + half, len * esz);
+                    if (!fault_drop_flags(me, seq)) fl.push_back(w.flags(r) + me);
+                }
+            }
+            const size_t mylen = o < mycnt ? std::min(qh_el, mycnt - o) : 0;
+            if (rc == MPI_SUCCESS) {
+                hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
+                                                fl.data(), (int)fl.size(), seq, sys_fences(), counter + kCountWords,
+                                                w.flags(me), mylen ? p : 0, me, err_dev, s);
+                if (e != hipSuccess) rc = hip_fail(e, "reduce_scatter push");
+            }
+            if (rc == MPI_SUCCESS && mylen) {
+                char* ro = out_window ? out : out + o * esz;
+                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, mylen, ro, s);
+                if (rc == MPI_SUCCESS && out_window) rc = copy_async(dst + o * esz, ro, mylen * esz, s);
+            }
+            if (rc == MPI_SUCCESS && ri + 2 < nrounds) {     // this round's half is read: free two rounds on
+                hipError_t e = launch_post_flags(done_to.data(), (int)done_to.size(), seq, s);
+                if (e != hipSuccess) rc = hip_fail(e, "reduce_scatter done flags");
+            }
+            tp->rd_parity ^= 1;
         }
-        if (rc == MPI_SUCCESS && mycnt) {
-            // in place, recvbuf still holds the input the tree reads: result via hold
-            char* out = in_place ? scratch
-                                 : (bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me));
-            rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, mycnt, out, s);
-            if (rc == MPI_SUCCESS && out != static_cast<char*>(bd.dev)) rc = copy_async(dst, out, mycnt * esz, s);
-        }
+        if (rc == MPI_SUCCESS && mycnt && in_place) rc = copy_async(dst, out, mycnt * esz, s);
         const int rs = sync_stream(s, "reduce_scatter one-step");
         if (rc == MPI_SUCCESS) rc = rs;
         if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
             rc = flag_timeout("reduce_scatter", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), seq);
         tp->post_done(seq);
-        tp->rd_parity ^= 1;
         tp->window_open = true;
-        trace("reduce_scatter: done (one step, GPU flags, seq %llu) rc=%d", seq, rc);
+        trace("reduce_scatter: done (GPU flags, %zu round(s), last seq %llu) rc=%d", nrounds, seq, rc);
         return rc;
     }
     // scratch: [hold: in-place results][stage: host-resident input pieces]

@@ -42,6 +42,22 @@ __device__ __forceinline__ void stores_done()
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// Producer half of a GPU-flag hand-off, done by ONE lane of a workgroup after
+// every lane waited for its own stores (stores_done) and the workgroup met at a
+// barrier: an agent-scope release (buffer_wbl2 sc1 + wait) before the lane
+// counts the workgroup done, so the count -- and the flag the last workgroup
+// posts with a system-scope release -- is ordered after ALL of the
+// workgroup's stores in the HSA model, not only by the stores' completion
+// (MI355X_MICROARCH.md, inter-workgroup visibility, producer form).  The asm
+// wait keeps the compiler from dropping the wait after the writeback (the
+// guide's ROCm 7.2 hazard).  Mode 2 of the kernels' `sys` word; mode 0 (vmcnt
+// only, rounds 1-3) stays selectable with MSX_WG_RELEASE=0.
+__device__ __forceinline__ void wg_release()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Write-through stores for data a GPU flag announces to another GPU: relaxed
 // system-scope atomic stores, i.e. global_store_* sc0 sc1, which the L2 passes
 // through to the owner's memory whatever MTYPE the importer maps the peer
@@ -114,13 +130,16 @@ __device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlag
     }
     for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride)
         st_wt_elem(dst + i, src[i]);
-    if (sys) __threadfence_system();
+    // sys: 1 = cached windows (system fence per lane), 2 = workgroup release
+    // (wg_release), 0 = stores' completion only
+    if (sys == 1) __threadfence_system();
     else stores_done();                                 // vmcnt(0): this lane's stores completed
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (sys == 2) wg_release();
         const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == total - 1) {
-            if (sys) __threadfence_system();
+            if (sys == 1) __threadfence_system();
             for (int k = 0; k < f.n; ++k)
                 __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
@@ -188,12 +207,13 @@ __device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlag
         if (c.wt) st_wt_elem(dst + i, src[i]);
         else dst[i] = src[i];
     }
-    if (sys) __threadfence_system();
+    if (sys == 1) __threadfence_system();
     else stores_done();
     __syncthreads();
+    if (threadIdx.x == 0 && sys == 2) wg_release();
     // counter: a kCountWords block (count_done); b = this workgroup's index
     if (threadIdx.x == 0 && count_done(counter, (unsigned)sg + bx * (unsigned)c.n, total)) {
-        if (sys) __threadfence_system();
+        if (sys == 1) __threadfence_system();
         for (int k = 0; k < f.n; ++k)
             __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -221,6 +241,7 @@ struct TreeArgs {
     int chain;
     int sys;   // sources/outputs shared with other GPUs: system-coherent access
     int wt;    // results announced by done_flags: write-through stores (st_wt)
+    int rel;   // tree_done: one lane's agent-scope release per workgroup (wg_release)
     const unsigned long long* wait_flags;   // see TreeSpec
     unsigned long long wait_seq;
     int wait_n;
@@ -273,7 +294,9 @@ __device__ __forceinline__ void tree_done(const TreeArgs& a, unsigned b, unsigne
     if (a.sys) __threadfence_system();
     else stores_done();
     __syncthreads();
-    if (threadIdx.x != 0 || !count_done(a.done_counter, b, nb)) return;
+    if (threadIdx.x != 0) return;
+    if (a.rel && !a.sys) wg_release();
+    if (!count_done(a.done_counter, b, nb)) return;
     // launches of the call: word 1 of the block
     const unsigned l = __hip_atomic_fetch_add(a.done_counter + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (l != a.done_launches - 1) return;
@@ -441,41 +464,71 @@ template <int OP, class VT> struct VecFn {
 // Same association and operand roles as tree_vec / tree_eval.  The generic
 // kernel's runtime leaf tests cost 25 % (p = 8, fp32 SUM, 32 MiB per source:
 // 55 us generic vs 44.6 us here, scripts/tree_probe.py).
-template <class F, int NL, int U, int BLOCK, bool NT, bool CHAIN>
+//
+// MASKED (trees only): the same NL-leaf tree with the non-power-of-two fold's
+// leaf pairs (pairmask: leaf k = f(s[2k], s[2k+1])) and absent leaves (k >=
+// nleaves: a binomial tree over p < NL ranks) taken at run time -- NL, the
+// unrolling and the up-front loads stay compile-time, the pattern is a
+// wave-uniform test per leaf (scalar branches, no divergence), so p = 3, 5, 6,
+// 7 and the rooted binomial trees run the fixed form instead of the generic
+// kernel's 16-leaf loop.
+template <class F, int NL, int U, int BLOCK, bool NT, bool CHAIN, bool MASKED = false>
 __device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict__ out, size_t nvec, size_t bid,
                                            size_t nb)
 {
+    static_assert(!(CHAIN && MASKED), "a chain has no pairs or absent leaves");
     constexpr size_t TILE = (size_t)BLOCK * U;
     const u32x4* src[NL];
+    const u32x4* src2[MASKED ? NL : 1];
 #pragma unroll
     for (int k = 0; k < NL; ++k)   // tree leaf k sits in slot 2k (slot 2k+1: its pair); chain source k in slot k
         src[k] = reinterpret_cast<const u32x4*>(a.s[CHAIN ? k : 2 * k]);
-    auto reduce = [](u32x4* v) {
+    if constexpr (MASKED) {
+#pragma unroll
+        for (int k = 0; k < NL; ++k) src2[k] = reinterpret_cast<const u32x4*>(a.s[2 * k + 1]);
+    }
+    const unsigned pm = MASKED ? a.pairmask : 0u;
+    const int nl = MASKED ? a.nleaves : NL;
+    auto reduce = [&](u32x4* v, const u32x4* w) {
         if constexpr (CHAIN) {
 #pragma unroll
             for (int k = 1; k < NL; ++k) v[0] = F::apply(v[0], v[k]);
         } else {
+            if constexpr (MASKED) {
+#pragma unroll
+                for (int k = 0; k < NL; ++k)
+                    if (k < nl && ((pm >> k) & 1u)) v[k] = F::apply(v[k], w[k]);
+            }
 #pragma unroll
             for (int d = 1; d < NL; d *= 2) {
 #pragma unroll
-                for (int k = 0; k + d < NL; k += 2 * d) v[k] = F::apply(v[k], v[k + d]);
+                for (int k = 0; k + d < NL; k += 2 * d)
+                    if (!MASKED || k + d < nl) v[k] = F::apply(v[k], v[k + d]);
             }
         }
         return v[0];
     };
+    auto load = [&](u32x4* v, u32x4* w, size_t i) {
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            if (!MASKED || k < nl) {
+                v[k] = ld<NT>(src[k] + i);
+                if constexpr (MASKED) {
+                    if ((pm >> k) & 1u) w[k] = ld<NT>(src2[k] + i);
+                }
+            }
+        }
+    };
     for (size_t t0 = bid * TILE; t0 < nvec; t0 += nb * TILE) {
         const size_t i0 = t0 + threadIdx.x;
         if (t0 + TILE <= nvec) {
-            u32x4 v[U][NL];
+            u32x4 v[U][NL], w[U][MASKED ? NL : 1];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-#pragma unroll
-                for (int k = 0; k < NL; ++k) v[u][k] = ld<NT>(src[k] + i0 + (size_t)u * BLOCK);
-            }
+            for (int u = 0; u < U; ++u) load(v[u], w[u], i0 + (size_t)u * BLOCK);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const u32x4 r = reduce(v[u]);
+                const u32x4 r = reduce(v[u], w[u]);
                 put_vec(a, out, i0 + (size_t)u * BLOCK, r);
             }
         } else {
@@ -483,10 +536,9 @@ __device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict_
             for (int u = 0; u < U; ++u) {
                 const size_t i = i0 + (size_t)u * BLOCK;
                 if (i < nvec) {
-                    u32x4 v[NL];
-#pragma unroll
-                    for (int k = 0; k < NL; ++k) v[k] = ld<NT>(src[k] + i);
-                    const u32x4 r = reduce(v);
+                    u32x4 v[NL], w[MASKED ? NL : 1];
+                    load(v, w, i);
+                    const u32x4 r = reduce(v, w);
                     put_vec(a, out, i, r);
                 }
             }
@@ -501,7 +553,7 @@ __device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict_
 // 57.1 us -- holding every source vector costs 146 VGPRs instead of 77, half
 // the waves per SIMD -- and non-temporal loads 3-8 % slower either way.
 template <int OP, class T, class VT, int BLOCK, bool UPFRONT = false, bool NT = false, int NL = 0, int U = 1,
-          bool CHAIN = false>
+          bool CHAIN = false, bool MASKED = false>
 __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out, size_t nvec,
                                                 size_t tail, int vec_ok)
 {
@@ -524,7 +576,8 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
     if (a.wait_flags && !arrival_wait(a)) return;
     if (a.sys) acquire_system();
     if constexpr (NL > 0) {
-        if (vec_ok) tree_fixed<VecFn<OP, VT>, NL, U, BLOCK, NT, CHAIN>(a, reinterpret_cast<u32x4*>(out), nvec, bid, nb);
+        if (vec_ok)
+            tree_fixed<VecFn<OP, VT>, NL, U, BLOCK, NT, CHAIN, MASKED>(a, reinterpret_cast<u32x4*>(out), nvec, bid, nb);
     } else if (vec_ok) {
         for (size_t i = bid * BLOCK + threadIdx.x; i < nvec; i += stride) {
             u32x4 r;

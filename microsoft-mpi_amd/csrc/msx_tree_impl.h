@@ -1,7 +1,7 @@
 // msx_tree_impl.h — host-side launch of k_tree (msx_tree_dev.h) for one MPI_Op
-// per translation unit: msx_tree_sum.hip (SUM, PROD and the fp32 SUM tuning
-// modes), msx_tree_cmp.hip (MAX, MIN, MAXLOC, MINLOC), msx_tree_logic.hip
-// (LAND, LOR, LXOR, BAND, BOR, BXOR).  Included by those files only.
+// family per translation unit (msx_tree_sum.hip with the fp32 SUM tuning
+// modes, msx_tree_prod/max/min/loc/land/lor/lxor/bit.hip), so the template
+// instantiations compile in parallel.  Included by those files only.
 #pragma once
 #include "msx_tree_dev.h"
 
@@ -15,7 +15,7 @@ constexpr int kTreeGridCap = 4096;          // generic kernel: grid-stride beyon
 constexpr int kFixedGridCap = 1 << 20;      // compile-time-source kernel: one tile per workgroup
 
 template <int OP, class T, class VT, bool UPFRONT = false, bool NT = false, int NL = 0, int U = 1,
-          bool CHAIN = false, int BLOCK = kTreeBlock>
+          bool CHAIN = false, int BLOCK = kTreeBlock, bool MASKED = false>
 hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     bool ok = ((uintptr_t)out & 15) == 0;
@@ -33,15 +33,15 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
     if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
     grid += a.npush;                         // fused push workgroups come first
-    hipLaunchKernelGGL((k_tree<OP, T, VT, BLOCK, UPFRONT, NT, NL, U, CHAIN>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((k_tree<OP, T, VT, BLOCK, UPFRONT, NT, NL, U, CHAIN, MASKED>), dim3((unsigned)grid),
                        dim3(BLOCK), 0, s, a, static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
     return hipGetLastError();
 }
 
-// The compile-time-source kernel when the call is a full power-of-two tree or
-// a chain of 2, 4 or 8 sources (p = 2, 4, 8: the node sizes); the generic
-// kernel otherwise (non-power-of-two folds, binomial trees with absent
-// leaves, other chain lengths, p = 16).
+// The compile-time-source kernel for every tree of up to 8 leaves and every
+// chain of 2-8 sources: full power-of-two trees, non-power-of-two folds and
+// binomial trees with absent leaves (MASKED, round 4); the generic kernel
+// only beyond 8 (p >= 9) and for the tuning modes.
 // DRAM-regime geometry of the compile-time-source kernel (NT: the sources
 // exceed the Infinity Cache): one-wave workgroups in dispatch order, as
 // k_combine_dram, so the eight XCDs read neighbouring tiles of every source.
@@ -51,26 +51,31 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
 // (0.75 -> 0.81); 64-lane workgroups in XCD-contiguous order and 256-lane ones
 // in dispatch order gain 1-2 % only.  Not with fused push workgroups (their
 // copy loop assumes 256 lanes; only small calls fuse).
-template <int OP, class T, class VT, bool NT, int NL, int U, bool CHAIN>
+template <int OP, class T, class VT, bool NT, int NL, int U, bool CHAIN, bool MASKED = false>
 hipError_t run_tree_fixed(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     if constexpr (NT) {
         if (a.npush == 0) {
             TreeArgs b = a;
             b.xg = -1;
-            return run_tree<OP, T, VT, false, NT, NL, U, CHAIN, 64>(b, nsrc, out, count, s);
+            return run_tree<OP, T, VT, false, NT, NL, U, CHAIN, 64, MASKED>(b, nsrc, out, count, s);
         }
     }
-    return run_tree<OP, T, VT, false, NT, NL, U, CHAIN>(a, nsrc, out, count, s);
+    return run_tree<OP, T, VT, false, NT, NL, U, CHAIN, kTreeBlock, MASKED>(a, nsrc, out, count, s);
 }
 
 template <int OP, class T, class VT, int U = 1, bool NT = false>
 hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     if (a.chain) {
+        // pairwise exchange chains: p sources (every node size up to 8)
         switch (a.P) {
         case 2: return run_tree_fixed<OP, T, VT, NT, 2, U, true>(a, nsrc, out, count, s);
+        case 3: return run_tree_fixed<OP, T, VT, NT, 3, U, true>(a, nsrc, out, count, s);
         case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, true>(a, nsrc, out, count, s);
+        case 5: return run_tree_fixed<OP, T, VT, NT, 5, U, true>(a, nsrc, out, count, s);
+        case 6: return run_tree_fixed<OP, T, VT, NT, 6, U, true>(a, nsrc, out, count, s);
+        case 7: return run_tree_fixed<OP, T, VT, NT, 7, U, true>(a, nsrc, out, count, s);
         case 8: return run_tree_fixed<OP, T, VT, NT, 8, U, true>(a, nsrc, out, count, s);
         default: break;
         }
@@ -79,6 +84,16 @@ hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hi
         case 2: return run_tree_fixed<OP, T, VT, NT, 2, U, false>(a, nsrc, out, count, s);
         case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, false>(a, nsrc, out, count, s);
         case 8: return run_tree_fixed<OP, T, VT, NT, 8, U, false>(a, nsrc, out, count, s);
+        default: break;
+        }
+    } else {
+        // non-power-of-two folds (p = 3, 5, 6, 7: leaf pairs) and binomial
+        // trees with absent leaves: the leaf count compile-time, the pattern
+        // at run time (tree_fixed MASKED)
+        switch (a.P) {
+        case 2: return run_tree_fixed<OP, T, VT, NT, 2, U, false, true>(a, nsrc, out, count, s);
+        case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, false, true>(a, nsrc, out, count, s);
+        case 8: return run_tree_fixed<OP, T, VT, NT, 8, U, false, true>(a, nsrc, out, count, s);
         default: break;
         }
     }

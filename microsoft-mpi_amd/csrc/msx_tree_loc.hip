@@ -1,0 +1,10 @@
+// msx_tree_loc.hip — k_tree launchers (MAXLOC, MINLOC), see msx_tree_impl.h.
+// One translation unit per op family so the instantiations compile in parallel.
+#include "msx_tree_impl.h"
+
+namespace msx {
+
+template hipError_t tree_dispatch<O_MAXLOC>(Kind, const dev::TreeArgs&, int, void*, size_t, hipStream_t);
+template hipError_t tree_dispatch<O_MINLOC>(Kind, const dev::TreeArgs&, int, void*, size_t, hipStream_t);
+
+}  // namespace msx

@@ -1,0 +1,9 @@
+// msx_tree_lxor.hip — k_tree launchers (LXOR), see msx_tree_impl.h.
+// One translation unit per op family so the instantiations compile in parallel.
+#include "msx_tree_impl.h"
+
+namespace msx {
+
+template hipError_t tree_dispatch<O_LXOR>(Kind, const dev::TreeArgs&, int, void*, size_t, hipStream_t);
+
+}  // namespace msx

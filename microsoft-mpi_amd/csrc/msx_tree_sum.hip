@@ -1,10 +1,9 @@
-// msx_tree_sum.hip — k_tree launchers (SUM, PROD; the fp32 SUM tuning modes of msx_tune_tree), see msx_tree_impl.h.
+// msx_tree_sum.hip — k_tree launchers (SUM; the fp32 SUM tuning modes of msx_tune_tree), see msx_tree_impl.h.
 #include "msx_tree_impl.h"
 
 namespace msx {
 
 template hipError_t tree_dispatch<O_SUM>(Kind, const dev::TreeArgs&, int, void*, size_t, hipStream_t);
-template hipError_t tree_dispatch<O_PROD>(Kind, const dev::TreeArgs&, int, void*, size_t, hipStream_t);
 
 // msx_tune_tree modes (fp32 SUM): 1/2/3 the generic kernel with
 // loads up front / up front + non-temporal / interleaved + non-temporal,

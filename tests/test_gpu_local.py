@@ -397,6 +397,97 @@ def test_tree_tuning_modes_agree(L):
     assert L.msx_tune_tree(0, 0) == 0
 
 
+def _oracle_tree(op, dt, srcs, P, pairmask, nleaves, chain):
+    """The engine's tree evaluated with the oracle's combine (msx_tree_dev.h
+    tree_eval): leaf k = srcs[2k] (op)= srcs[2k+1] when paired, then the
+    balanced tree skipping absent leaves, left operand in the inout role; or
+    the left-deep chain."""
+    if chain:
+        v = _raw(srcs[0])
+        for k in range(1, P):
+            assert oracle.reduce_local(h(op), h(dt), srcs[k], v) == 0
+        return v
+    nl = nleaves or P
+    v = [None] * P
+    for k in range(nl):
+        v[k] = _raw(srcs[2 * k])
+        if (pairmask >> k) & 1:
+            assert oracle.reduce_local(h(op), h(dt), srcs[2 * k + 1], v[k]) == 0
+    d = 1
+    while d < P:
+        for k in range(0, P - d, 2 * d):
+            if k + d < nl:
+                assert oracle.reduce_local(h(op), h(dt), v[k + d], v[k]) == 0
+        d *= 2
+    return v[0]
+
+
+TREE_SPEC_PAIRS = [("MPI_SUM", "MPI_FLOAT"), ("MPI_SUM", "MPI_INT"), ("MPI_MAX", "MPI_DOUBLE"),
+                   ("MPI_PROD", "MPI_C_FLOAT_COMPLEX"), ("MPI_MAXLOC", "MPI_2INT"), ("MPI_BXOR", "MPI_BYTE"),
+                   ("MPI_LXOR", "MPI_C_BOOL"), ("MPI_MIN", "MPI_INT8_T")]
+
+
+@pytest.mark.parametrize("pair", TREE_SPEC_PAIRS, ids=lambda p: f"{p[0]}-{p[1]}")
+def test_tree_folds_absent_leaves_and_chains(L, pair):
+    """The compile-time-leaf kernels of round 4 (tree_fixed MASKED: the
+    non-power-of-two folds of p = 3, 5, 6, 7 and binomial trees with absent
+    leaves; chains of 3-8 sources) against the oracle evaluating the same
+    tree, bit for bit, every pattern the engine can produce for P = 2, 4, 8
+    plus random ones, vector body + scalar tail."""
+    op, dt = pair
+    kind = KIND[dt]
+    rng = np.random.default_rng(zlib.crc32(f"spec/{op}/{dt}".encode()))
+    n = 4099
+    srcs = [gen(kind, op, n, rng) for _ in range(16)]
+    devs = [_dev(x) for x in srcs]
+    ptrs = [p for _, p in devs]
+    cases = []
+    for P in (2, 4, 8):
+        for nl in range(1, P + 1):
+            cases.append((P, 0, nl, 0))                        # absent leaves (binomial trees)
+        for pm in range(1, 1 << P) if P < 8 else rng.integers(1, 256, 24):
+            cases.append((P, int(pm), P, 0))                   # folds (pairs)
+        cases.append((P, int(rng.integers(0, 1 << P)), int(rng.integers(1, P + 1)), 0))
+    for P in range(2, 9):
+        cases.append((P, 0, 0, 1))                             # chains
+    out = torch.zeros(n * srcs[0].itemsize + 64, dtype=torch.uint8, device="cuda")
+    for P, pm, nl, chain in cases:
+        ns = P if chain else 2 * P
+        arr = (ctypes.c_void_p * ns)(*ptrs[:ns])
+        rc = L.msx_reduce_tree_spec_dev(arr, P, pm, nl, chain, out.data_ptr(), n, h(dt), h(op), _stream())
+        assert rc == 0, msx.last_error()
+        torch.cuda.synchronize()
+        got = _host(out, 0, srcs[0])
+        exp = _oracle_tree(op, dt, srcs[:ns], P, pm, nl, chain)
+        assert got.tobytes() == exp.tobytes(), (op, dt, P, hex(pm), nl, chain)
+
+
+def test_tree_folds_dram_regime_fp32(L):
+    """The masked kernel in its DRAM-regime form (source bytes above
+    tree_nt_min: non-temporal loads, one-wave workgroups): p = 6's fold
+    (P = 4, two pairs) and a p = 7 binomial tree (P = 8, 7 leaves) over 48 MiB
+    sources, bit-exact against torch evaluating the same association."""
+    n = 12 << 20
+    g = torch.Generator(device="cuda").manual_seed(6)
+    xs = [torch.rand(n, device="cuda", generator=g) * 2 - 1 for _ in range(8)]
+    out = torch.empty_like(xs[0])
+    torch.cuda.synchronize()
+    # p = 6 allreduce fold: leaves 0, 1 paired
+    arr = (ctypes.c_void_p * 8)(*[x.data_ptr() for x in xs])
+    assert L.msx_reduce_tree_spec_dev(arr, 4, 0b11, 4, 0, out.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM,
+                                      _stream()) == 0, msx.last_error()
+    torch.cuda.synchronize()
+    exp = ((xs[0] + xs[1]) + (xs[2] + xs[3])) + (xs[4] + (xs[6]))
+    assert torch.equal(out.view(torch.int32), exp.view(torch.int32))
+    # p = 7 binomial tree: leaves 0..6 of an 8-leaf tree (slots 2k)
+    arr = (ctypes.c_void_p * 16)(*[xs[k // 2].data_ptr() if k % 2 == 0 else xs[0].data_ptr() for k in range(16)])
+    assert L.msx_reduce_tree_spec_dev(arr, 8, 0, 7, 0, out.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM,
+                                      _stream()) == 0, msx.last_error()
+    torch.cuda.synchronize()
+    exp = ((xs[0] + xs[1]) + (xs[2] + xs[3])) + ((xs[4] + xs[5]) + xs[6])
+    assert torch.equal(out.view(torch.int32), exp.view(torch.int32))
+
+
 def test_copy_geometries_exact(L):
     # the engine's local copy in both geometries (probe modes 8 / 9: k_copy_segs'
     # XCD-contiguous tiles, k_copy_dram's one-wave dispatch order) and the

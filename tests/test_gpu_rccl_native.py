@@ -171,7 +171,7 @@ def test_rccl_native_collectives_one_rank_per_gpu():
     n_dev = torch.cuda.device_count()
     if n_dev < 2:
         pytest.skip("needs >= 2 GPUs (one rank per GPU)")
-    p = min(n_dev, 4)
+    p = min(n_dev, 8)                     # every visible GPU
     port = _free_port()
     procs = []
     for r in range(p):
