@@ -70,7 +70,7 @@ def run_collectives_child(world, rank, local, scale, transport="ipc"):
                 "MSX_TRANSPORT": transport,
                 "MSX_BOOTSTRAP_ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
                 "MSX_BOOTSTRAP_PORT": str((int(os.environ.get("MASTER_PORT", "29500")) + off) % 65536),
-                "MSX_BOOTSTRAP_TIMEOUT": "90",
+                "MSX_BOOTSTRAP_TIMEOUT": "90", "MSX_STUCK_SYNC_S": "60",
                 "MSX_BENCH_LOG": os.environ.get("MSX_BENCH_LOG", os.devnull)})
     mine = f"{out}.rank{rank}"
     for path in (out, mine):

@@ -2265,7 +2265,13 @@ MSX_EXPORT int MPI_Rget_accumulate(const void* origin_addr, int origin_count, MP
 // ===========================================================================
 // device-side extension ABI (include/msx.h)
 // ===========================================================================
-MSX_EXPORT const char* msx_version(void) { return "msmpi-mi355x 0.1 (gfx950)"; }
+// Build provenance: MSX_SOURCE_HASH is the SHA-256 prefix of the library's
+// sources and headers at build time (Makefile), so a test can tell whether a
+// prebuilt .so was compiled from the tree it ships with (tests/test_abi.py).
+#ifndef MSX_SOURCE_HASH
+#define MSX_SOURCE_HASH "unknown"
+#endif
+MSX_EXPORT const char* msx_version(void) { return "msmpi-mi355x 0.1 (gfx950) src=" MSX_SOURCE_HASH; }
 
 MSX_EXPORT const char* msx_engine_transport(void)
 {

@@ -78,12 +78,18 @@ const char* last_error() { return g_err; }
 // parent's JSON instead of surfacing as a bare timeout.
 namespace {
 constexpr int kPhaseSlots = 64;
+// A slot is claimed (used 0 -> 1), filled, published (used = 2, gen bumped),
+// and released (used = 0).  Every field is atomic and the watchdog re-reads
+// `gen` after reading the fields, so a slot reclaimed meanwhile is skipped
+// instead of reported with a mix of two steps' fields.
 struct PhaseSlot {
     std::atomic<int> used{0};
-    const char* phase = nullptr;
-    int peer = -1;
-    double t0 = 0;
-    bool reported = false;
+    std::atomic<uint64_t> gen{0};
+    std::atomic<const char*> phase{nullptr};
+    std::atomic<int> peer{-1};
+    std::atomic<double> t0{0.0};
+    std::atomic<bool> sync{false};
+    std::atomic<uint64_t> reported{0};    // gen of the step last reported
 };
 PhaseSlot g_phase[kPhaseSlots];
 std::atomic<int> g_diag_rank{0};
@@ -100,14 +106,25 @@ void watchdog()
 {
     const char* e = getenv("MSX_STUCK_REPORT_S");
     const double limit = e ? atof(e) : 30.0;
+    const char* es = getenv("MSX_STUCK_SYNC_S");
+    const double limit_sync = es ? atof(es) : 300.0;
     for (;;) {
         usleep(250 * 1000);
         const double now = mono_s();
         for (PhaseSlot& sl : g_phase) {
-            if (sl.used.load(std::memory_order_acquire) != 2 || sl.reported || now - sl.t0 < limit) continue;
-            sl.reported = true;
+            const uint64_t g = sl.gen.load(std::memory_order_acquire);
+            if (sl.used.load(std::memory_order_acquire) != 2 || sl.reported.load(std::memory_order_relaxed) == g)
+                continue;
+            const char* ph = sl.phase.load(std::memory_order_relaxed);
+            const int peer = sl.peer.load(std::memory_order_relaxed);
+            const double t0 = sl.t0.load(std::memory_order_relaxed);
+            const bool sync = sl.sync.load(std::memory_order_relaxed);
+            if (sl.gen.load(std::memory_order_acquire) != g || sl.used.load(std::memory_order_acquire) != 2) continue;
+            const double lim = sync ? limit_sync : limit;
+            if (lim <= 0 || now - t0 < lim) continue;
+            sl.reported.store(g, std::memory_order_relaxed);
             fprintf(stderr, "MSX_STUCK {\"rank\":%d,\"phase\":\"%s\",\"peer\":%d,\"seconds\":%.1f}\n",
-                    g_diag_rank.load(), sl.phase ? sl.phase : "?", sl.peer, now - sl.t0);
+                    g_diag_rank.load(), ph ? ph : "?", peer, now - t0);
             fflush(stderr);
         }
     }
@@ -116,17 +133,18 @@ void watchdog()
 
 void set_diag_rank(int r) { g_diag_rank.store(r); }
 
-PhaseScope::PhaseScope(const char* phase, int peer)
+PhaseScope::PhaseScope(const char* phase, int peer, bool sync)
 {
     std::call_once(g_watch_once, [] { std::thread(watchdog).detach(); });
     for (int i = 0; i < kPhaseSlots; ++i) {
         int z = 0;
         if (g_phase[i].used.compare_exchange_strong(z, 1, std::memory_order_acq_rel)) {
             PhaseSlot& sl = g_phase[i];
-            sl.phase = phase;
-            sl.peer = peer;
-            sl.t0 = mono_s();
-            sl.reported = false;
+            sl.phase.store(phase, std::memory_order_relaxed);
+            sl.peer.store(peer, std::memory_order_relaxed);
+            sl.t0.store(mono_s(), std::memory_order_relaxed);
+            sl.sync.store(sync, std::memory_order_relaxed);
+            sl.gen.fetch_add(1, std::memory_order_release);
             sl.used.store(2, std::memory_order_release);
             slot_ = i;
             return;
@@ -136,7 +154,10 @@ PhaseScope::PhaseScope(const char* phase, int peer)
 
 PhaseScope::~PhaseScope()
 {
-    if (slot_ >= 0) g_phase[slot_].used.store(0, std::memory_order_release);
+    if (slot_ >= 0) {
+        g_phase[slot_].gen.fetch_add(1, std::memory_order_release);
+        g_phase[slot_].used.store(0, std::memory_order_release);
+    }
 }
 
 void trace(const char* fmt, ...)

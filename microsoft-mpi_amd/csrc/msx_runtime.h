@@ -31,10 +31,12 @@ const char* last_error();
 
 // A host step that may block on another process or GPU; a watchdog thread
 // prints `MSX_STUCK {"rank":..,"phase":..,"peer":..,"seconds":..}` on stderr
-// once the step exceeds MSX_STUCK_REPORT_S (default 30 s).
+// once the step exceeds MSX_STUCK_REPORT_S (default 30 s) -- or, for a
+// stream synchronisation (sync = true, which a large call on a loaded GPU may
+// legitimately spend long in), MSX_STUCK_SYNC_S (default 300 s, 0 = never).
 class PhaseScope {
 public:
-    PhaseScope(const char* phase, int peer = -1);
+    PhaseScope(const char* phase, int peer = -1, bool sync = false);
     ~PhaseScope();
     PhaseScope(const PhaseScope&) = delete;
     PhaseScope& operator=(const PhaseScope&) = delete;

@@ -339,6 +339,8 @@ struct IpcRec {
     int32_t pad;
 };
 
+size_t rma_bytes_for(int share);   // passive-target staging size for `share` ranks per GPU (below)
+
 class IpcTransport : public Transport {
 public:
     ~IpcTransport() override
@@ -488,11 +490,32 @@ public:
         return MPI_SUCCESS;
     }
 
-    int rma_window(size_t bytes, std::vector<char*>& out) override
+    int rma_window(std::vector<char*>& out, size_t* bytes_out) override
     {
         // Collective, first passive-target window of the communicator only:
         // uncached like the engine window (peers write payloads into it)
         if (!rwin_) {
+            // ranks sharing this GPU, counted from every rank's PCI bus id
+            // (not guessed from WORLD_SIZE / device count: a launcher may show
+            // each rank only its own GPU), then the minimum size over ranks
+            char bus[64] = {0};
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev) != hipSuccess) {
+                (void)hipGetLastError();
+                snprintf(bus, sizeof(bus), "unknown-%d", rank);
+            }
+            std::vector<char> buses((size_t)size * sizeof(bus));
+            int rc = hub_.allgather(bus, sizeof(bus), buses.data());
+            if (rc != MPI_SUCCESS) return rc;
+            int share = 0;
+            for (int r = 0; r < size; ++r)
+                share += strncmp(buses.data() + (size_t)r * sizeof(bus), bus, sizeof(bus)) == 0;
+            uint64_t mine = rma_bytes_for(share), lo = mine;
+            std::vector<uint64_t> all((size_t)size);
+            if ((rc = hub_.allgather(&mine, sizeof(mine), all.data())) != MPI_SUCCESS) return rc;
+            for (uint64_t v : all) lo = std::min(lo, v);
+            const size_t bytes = (size_t)lo;
+            trace("rma window: %d rank(s) on this GPU, %zu bytes here, %zu agreed", share, (size_t)mine, bytes);
             const bool cached = getenv("MSX_WINDOW_CACHED") && atoi(getenv("MSX_WINDOW_CACHED"));
             hipError_t e = cached ? hipMalloc(&rwin_, bytes) : hipExtMallocWithFlags(&rwin_, bytes, hipDeviceMallocUncached);
             trace("rma window: %zu bytes rc=%d", bytes, (int)e);
@@ -500,10 +523,12 @@ public:
                 rwin_ = nullptr;
                 return hip_fail(e, "rma staging allocation");
             }
-            int rc = map_peers(rwin_, rwin_peers_);
+            rc = map_peers(rwin_, rwin_peers_);
             if (rc != MPI_SUCCESS) return rc;
+            rbytes_ = bytes;
         }
         out = rwin_peers_;
+        *bytes_out = rbytes_;
         return MPI_SUCCESS;
     }
 
@@ -517,6 +542,7 @@ private:
     size_t win_bytes_ = 0;
     std::vector<char*> win_peers_;
     void* rwin_ = nullptr;                // passive-target staging (rma_window)
+    size_t rbytes_ = 0;                   // its agreed size
     std::vector<char*> rwin_peers_;
 };
 
@@ -969,7 +995,7 @@ bool fault_drop_flags(int me, unsigned long long seq)
 
 int sync_stream(hipStream_t s, const char* what)
 {
-    PhaseScope ph(what);
+    PhaseScope ph(what, -1, true);
     hipError_t e = hipStreamSynchronize(s);
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
 }
@@ -1258,7 +1284,7 @@ size_t chunk_bytes()
 constexpr size_t kFlagBytes = 64 << 10;
 // Passive-target RMA staging (its own IPC allocation, created by the first
 // passive-target window of a communicator): p payload slots (written by each
-// origin) then p fetch slots (written by each target), rma_bytes() / (2p) each.
+// origin) then p fetch slots (written by each target), the agreed size / (2p) each.
 // Every slot-sized piece of a lock / PSCW operation costs one host handshake
 // with the target's service thread (~50 us), so the area is sized for large
 // pieces (MSX_RMA_BYTES, default 512 MiB), below the 2 GiB IPC limit.  256 MiB lock / PSCW accumulates, 2 ranks on one MI355X
@@ -1266,25 +1292,18 @@ constexpr size_t kFlagBytes = 64 << 10;
 // 0.53 ms with 512 MiB (= the fence epoch's 0.54 ms).
 // The area belongs to the communicator's transport: every communicator with a
 // window holds one per rank.  Without MSX_RMA_BYTES the default is capped per
-// GPU: 512 MiB divided by the ranks of the job that share this GPU (8 ranks on
-// one GPU: 64 MiB each), at least 64 MiB.
-size_t rma_bytes()
+// GPU: 512 MiB divided by the ranks that share this GPU (8 ranks on one GPU:
+// 64 MiB each), at least 64 MiB.  `share` is counted by the transport from
+// every rank's PCI bus id, and the ranks then take the minimum of their sizes
+// (IpcTransport::rma_window), so all of them address the same slots.
+size_t rma_bytes_for(int share)
 {
-    static size_t v = [] {
-        size_t b = (size_t)512 << 20;
-        const char* ws = getenv("MSX_SIZE");
-        if (!ws) ws = getenv("WORLD_SIZE");
-        const int ndev = device_count_noinit();
-        if (ws && ndev > 0) {
-            const size_t share = ((size_t)std::max(1, atoi(ws)) + (size_t)ndev - 1) / (size_t)ndev;
-            b = std::max(b / share, (size_t)64 << 20);
-        }
-        if (const char* e = getenv("MSX_RMA_BYTES")) b = (size_t)atoll(e);
-        const size_t cap = ((size_t)2 << 30) - ((size_t)1 << 20);      // IPC mapping limit
-        b = std::min(b, cap);
-        return std::max(b, (size_t)4 << 20) & ~(size_t)4095;
-    }();
-    return v;
+    size_t b = (size_t)512 << 20;
+    if (share > 1) b = std::max(b / (size_t)share, (size_t)64 << 20);
+    if (const char* e = getenv("MSX_RMA_BYTES")) b = (size_t)atoll(e);
+    const size_t cap = ((size_t)2 << 30) - ((size_t)1 << 20);      // IPC mapping limit
+    b = std::min(b, cap);
+    return std::max(b, (size_t)4 << 20) & ~(size_t)4095;
 }
 
 // Sub-slots are Q bytes long but S = Q + skew apart: the p-source tree reads
@@ -1326,7 +1345,8 @@ struct Windows {
     unsigned long long* flags(int r) const { return reinterpret_cast<unsigned long long*>(base[(size_t)r] + I + C); }
     // passive-target staging (rma_window), when the communicator has one
     std::vector<char*> rbase;
-    size_t rma_slot() const { return (rma_bytes() / (2 * rbase.size())) & ~(size_t)255; }
+    size_t rbytes = 0;                    // the agreed staging size (rma_window)
+    size_t rma_slot() const { return (rbytes / (2 * rbase.size())) & ~(size_t)255; }
     // rank r's staging: payload slot written by origin o / fetch slot written by target t
     char* rma_in(int r, int o) const { return rbase[(size_t)r] + (size_t)o * rma_slot(); }
     char* rma_fetch(int r, int t) const { return rbase[(size_t)r] + (rbase.size() + (size_t)t) * rma_slot(); }
@@ -1720,26 +1740,34 @@ int rccl_allreduce(ncclComm_t comm, Comm* c, const void* sendbuf, void* recvbuf,
     const RcclApi* api = rccl_api();
     if (rccl_native_requested() && rccl_map(op.opidx, k, &nop, &nty) &&
         (root < 0 ? api->all_reduce != nullptr : api->reduce != nullptr)) {
-        // every rank decides alike: the pair and the buffers' placement
-        // (agreed, since one rank with a host operand must not leave the others
-        // in an RCCL collective alone)
-        const int mine_dev = classify(src).place == Place::Device && (!want || classify(dst).place == Place::Device);
-        std::vector<int> all((size_t)p);
-        int rc = tp->allgather(&mine_dev, sizeof(int), all.data());
-        if (rc != MPI_SUCCESS) return rc;
-        bool all_dev = true;
-        for (int v : all) all_dev = all_dev && v;
-        if (all_dev) {
-            ncclResult_t r = root < 0 ? api->all_reduce(src, dst, count, nty, nop, comm, s)
-                                      : api->reduce(src, want ? static_cast<void*>(dst) : const_cast<char*>(src), count,
-                                                    nty, nop, root, comm, s);
-            trace("rccl native %s: count=%zu rc=%d", root < 0 ? "allreduce" : "reduce", count, (int)r);
-            if (r != ncclSuccess) {
-                set_error("%s: %s", root < 0 ? "ncclAllReduce" : "ncclReduce", api->err(r));
-                return MPI_ERR_OTHER;
-            }
-            return sync_stream(s, root < 0 ? "allreduce" : "reduce");
+        // Every rank takes this branch for a mappable pair (the pair is the
+        // same on every rank), so no per-call agreement is needed: a rank
+        // whose operands are host memory stages them through device scratch
+        // (H2D, RCCL in place on the scratch, D2H) instead of leaving the
+        // others in an RCCL collective alone.
+        const bool sdev = classify(src).place == Place::Device;
+        const bool ddev = !want || classify(dst).place == Place::Device;
+        const char* in = src;
+        char* out = want ? dst : const_cast<char*>(src);
+        char* tmp = nullptr;
+        int rc = MPI_SUCCESS;
+        if (!sdev || !ddev) {
+            tmp = dev_scratch(count * esz);
+            if (!tmp) { set_error("allreduce: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+            rc = copy_async(tmp, src, count * esz, s);
+            in = out = tmp;
         }
+        if (rc != MPI_SUCCESS) return rc;
+        ncclResult_t r = root < 0 ? api->all_reduce(in, out, count, nty, nop, comm, s)
+                                  : api->reduce(in, out, count, nty, nop, root, comm, s);
+        trace("rccl native %s: count=%zu staged=%d rc=%d", root < 0 ? "allreduce" : "reduce", count, tmp != nullptr,
+              (int)r);
+        if (r != ncclSuccess) {
+            set_error("%s: %s", root < 0 ? "ncclAllReduce" : "ncclReduce", api->err(r));
+            return MPI_ERR_OTHER;
+        }
+        if (tmp && want) rc = copy_async(dst, tmp, count * esz, s);
+        return rc == MPI_SUCCESS ? sync_stream(s, root < 0 ? "allreduce" : "reduce") : rc;
     }
     const bool is_reduce = root >= 0;
     const int gate = gate_type_size(dt, nbc);
@@ -1850,27 +1878,31 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
     if (rccl_native_requested() && api->reduce_scatter && rccl_map(op.opidx, k, &nop, &nty) &&
         maxcnt * (size_t)p == total) {
         // equal blocks (recvcounts are the same on every rank by MPI rule):
-        // ncclReduceScatter; in place, my block moves to recvbuf[0]
-        const int mine_dev = classify(src).place == Place::Device && classify(recvbuf).place == Place::Device;
-        std::vector<int> all((size_t)p);
-        int rc = tp->allgather(&mine_dev, sizeof(int), all.data());
-        if (rc != MPI_SUCCESS) return rc;
-        bool all_dev = true;
-        for (int v : all) all_dev = all_dev && v;
-        if (all_dev) {
-            void* out = recvbuf;
-            char* tmp = nullptr;
-            if (in_place && me != 0 && maxcnt) {
-                tmp = dev_scratch(maxcnt * esz);      // RCCL's in-place form wants recvbuf + rank*count
-                if (!tmp) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
-                out = tmp;
-            }
-            ncclResult_t r = api->reduce_scatter(src, out, maxcnt, nty, nop, comm, s);
-            trace("rccl native reduce_scatter: count=%zu rc=%d", maxcnt, (int)r);
-            if (r != ncclSuccess) { set_error("ncclReduceScatter: %s", api->err(r)); return MPI_ERR_OTHER; }
-            if (tmp) rc = copy_async(recvbuf, tmp, maxcnt * esz, s);
-            return rc == MPI_SUCCESS ? sync_stream(s, "reduce_scatter") : rc;
+        // ncclReduceScatter.  Taken by every rank alike (no per-call
+        // agreement): host operands are staged through device scratch, and in
+        // place my block moves to recvbuf[0]
+        const bool sdev = classify(src).place == Place::Device, ddev = classify(recvbuf).place == Place::Device;
+        const char* in = src;
+        void* out = recvbuf;
+        char* tmp = nullptr;
+        int rc = MPI_SUCCESS;
+        if (!sdev || !ddev) {
+            tmp = dev_scratch((total + maxcnt) * esz);          // [input][my block]
+            if (!tmp) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+            rc = copy_async(tmp, src, total * esz, s);
+            in = tmp;
+            out = tmp + total * esz;
+        } else if (in_place && me != 0 && maxcnt) {
+            tmp = dev_scratch(maxcnt * esz);      // RCCL's in-place form wants recvbuf + rank*count
+            if (!tmp) { set_error("reduce_scatter: scratch allocation failed"); return MPI_ERR_NO_MEM; }
+            out = tmp;
         }
+        if (rc != MPI_SUCCESS) return rc;
+        ncclResult_t r = api->reduce_scatter(in, out, maxcnt, nty, nop, comm, s);
+        trace("rccl native reduce_scatter: count=%zu staged=%d rc=%d", maxcnt, (!sdev || !ddev), (int)r);
+        if (r != ncclSuccess) { set_error("ncclReduceScatter: %s", api->err(r)); return MPI_ERR_OTHER; }
+        if (out != recvbuf) rc = copy_async(recvbuf, out, maxcnt * esz, s);
+        return rc == MPI_SUCCESS ? sync_stream(s, "reduce_scatter") : rc;
     }
     size_t qe = (chunk_bytes() / (size_t)p) / esz;
     qe -= qe % 16;
@@ -3558,7 +3590,7 @@ int passive_init(RmaWin* w)
     ps->p = c->size;
     ps->me = c->rank;
     int rc = get_windows(c->tp, &ps->win);
-    if (rc == MPI_SUCCESS) rc = c->tp->rma_window(rma_bytes(), ps->win.rbase);
+    if (rc == MPI_SUCCESS) rc = c->tp->rma_window(ps->win.rbase, &ps->win.rbytes);
     const size_t p = (size_t)ps->p;
     const size_t hdr = ((p * sizeof(std::atomic<uint32_t>) + p * sizeof(std::atomic<int32_t>)) + 63) & ~(size_t)63;
     const size_t pscw = (2 * p * p * sizeof(std::atomic<uint32_t>) + 63) & ~(size_t)63;

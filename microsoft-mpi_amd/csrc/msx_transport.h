@@ -53,9 +53,12 @@ public:
     virtual int map_peers(const void* ptr, std::vector<char*>& out) = 0;
     // Per-rank device scratch, IPC-mapped once: out[r] = rank r's window.
     virtual int window(size_t bytes, std::vector<char*>& out) = 0;
-    // Passive-target staging: a second per-rank window of `bytes`, created
-    // by the first call (collective) and kept for the transport's lifetime.
-    virtual int rma_window(size_t bytes, std::vector<char*>& out) = 0;
+    // Passive-target staging: a second per-rank window, created by the first
+    // call (collective) and kept for the transport's lifetime.  Its size is
+    // agreed by all ranks (the minimum of their rma_bytes_for(ranks sharing
+    // their GPU)) and returned in *bytes, so every rank addresses the same
+    // slots in every peer's area.
+    virtual int rma_window(std::vector<char*>& out, size_t* bytes) = 0;
     virtual hipStream_t stream() = 0;
     // Completion counters of the fused push (k_push_post, word 0) and of the
     // two-step allreduce's result flags (words 1-2): zeroed device words per

@@ -535,3 +535,22 @@ def test_alloc_mem_validation_without_gpu():
     assert L.MPI_Free_mem(ctypes.addressof(other)) == C.MPI_ERR_BASE
     assert L.MPI_Free_mem(p) == 0
     assert L.MPI_Free_mem(p) == C.MPI_ERR_BASE          # not twice
+
+
+def test_library_was_built_from_these_sources(msxlib):
+    """Build provenance: msx_version() carries the SHA-256 prefix of every
+    library source and header at build time (microsoft-mpi_amd/Makefile), so
+    a prebuilt libmsmpi_mi355x.so shipped with the tree must match it."""
+    import glob
+    import hashlib
+    pkg = os.path.join(msx.REPO_ROOT, "microsoft-mpi_amd")
+    files = sorted(glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(pkg, "csrc", "*.h")), key=lambda f: os.path.relpath(f, pkg))
+    files += [os.path.join(msx.REPO_ROOT, "include", "mpi.h"), os.path.join(msx.REPO_ROOT, "include", "msx.h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    msxlib.msx_version.restype = ctypes.c_char_p
+    v = msxlib.msx_version().decode()
+    assert v.endswith("src=" + h.hexdigest()[:16]), (v, h.hexdigest()[:16])
