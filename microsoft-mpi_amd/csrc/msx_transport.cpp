@@ -1525,6 +1525,37 @@ hipStream_t aux_stream()
     return s;
 }
 
+// Cross-stream hand-offs of the pipelined two-step allreduce (two chunks in
+// flight, so two of each); collectives are issued one at a time per process.
+struct PipeEvents {
+    hipEvent_t tree[2] = {nullptr, nullptr}, copy[2] = {nullptr, nullptr};
+    bool ok = false;
+};
+PipeEvents& pipe_events()
+{
+    static PipeEvents e = [] {
+        PipeEvents p;
+        p.ok = true;
+        for (int i = 0; i < 2; ++i)
+            p.ok = p.ok && hipEventCreateWithFlags(&p.tree[i], hipEventDisableTiming) == hipSuccess &&
+                   hipEventCreateWithFlags(&p.copy[i], hipEventDisableTiming) == hipSuccess;
+        return p;
+    }();
+    return e;
+}
+
+// The pipelined allreduce collects chunk i (result wait + OUT -> recvbuf copy)
+// on the aux stream while the engine stream pushes chunk i + 1
+// (MSX_COLLECT_OVERLAP=0: one stream).
+bool collect_overlap()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_COLLECT_OVERLAP");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 // A batch of byte ranges moved by one k_copy_segs launch (one grid row each).
 struct Segs {
     std::vector<const void*> src;
@@ -2220,6 +2251,11 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         const size_t rs = count / (size_t)pof2;
         unsigned long long seq = 0;
         size_t nranges = 0;
+        // collect stream: chunk ci's result wait and copy overlap chunk ci+1's
+        // push and trees; events order my own tree before my copy and my copy
+        // of chunk ci before my trees of chunk ci+2 (same OUT half)
+        PipeEvents& ev = pipe_events();
+        const hipStream_t sc = (want && nchunks > 1 && ev.ok && collect_overlap()) ? aux_stream() : s;
         for (size_t ci = 0; ci < nchunks && rc == MPI_SUCCESS; ++ci) {
             const size_t o = ci * pc_el, len = std::min(pc_el, count - o);
             const size_t pel = (((len + (size_t)p - 1) / (size_t)p) + 15) & ~(size_t)15;
@@ -2237,6 +2273,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, false, nullptr,
                                                 w.flags(me) + kDoneFlags, p, me, err_dev, s, 3);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce half-free wait");
+                if (rc == MPI_SUCCESS && sc != s && hipStreamWaitEvent(s, ev.copy[ci % 2], 0) != hipSuccess)
+                    rc = hip_fail(hipGetLastError(), "allreduce collect event wait");
             }
             if (rc != MPI_SUCCESS) break;
             Segs sg;
@@ -2291,25 +2329,35 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 rc = run_rank_tree(op.opidx, k, t, subs, esz, g.e0 - plo, g.e1 - g.e0,
                                    w.out(dests[0]) + obase + g.e0 * esz, s, extra, &tw);
             }
+            if (rc == MPI_SUCCESS && sc != s) {
+                if (hipEventRecord(ev.tree[ci % 2], s) != hipSuccess || hipStreamWaitEvent(sc, ev.tree[ci % 2], 0) != hipSuccess)
+                    rc = hip_fail(hipGetLastError(), "allreduce tree event");
+            }
             if (rc == MPI_SUCCESS && want) {
                 // step 3: every peer's result in my OUT half, then into recvbuf
                 e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq, false, nullptr,
-                                     w.flags(me) + kResultFlags, p, me, err_dev, s, 2);
+                                     w.flags(me) + kResultFlags, p, me, err_dev, sc, 2);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce result wait");
                 char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : dst;
-                if (rc == MPI_SUCCESS) rc = copy_async(out + o * esz, w.out(me) + obase, len * esz, s);
+                if (rc == MPI_SUCCESS) rc = copy_async(out + o * esz, w.out(me) + obase, len * esz, sc);
+                if (rc == MPI_SUCCESS && sc != s && hipEventRecord(ev.copy[ci % 2], sc) != hipSuccess)
+                    rc = hip_fail(hipGetLastError(), "allreduce collect event");
             }
             // step 4: this chunk's halves are free again (read by my trees and
-            // my copy, both earlier on the stream) -- only a later chunk of
-            // this call waits on it
+            // my copy, both earlier on the collect stream) -- only a later
+            // chunk of this call waits on it
             if (rc == MPI_SUCCESS && ci + 2 < nchunks) {
-                e = launch_post_flags(done_to.data(), (int)done_to.size(), seq, s);
+                e = launch_post_flags(done_to.data(), (int)done_to.size(), seq, sc);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce done flags");
             }
             tp->rd_parity ^= 1;
         }
         const int rsy = sync_stream(s, "allreduce two-step");
         if (rc == MPI_SUCCESS) rc = rsy;
+        if (sc != s) {
+            const int rsc = sync_stream(sc, "allreduce two-step collect");
+            if (rc == MPI_SUCCESS) rc = rsc;
+        }
         if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
             rc = flag_timeout(root < 0 ? "allreduce" : "reduce", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), seq);
         tp->post_done(seq);
