@@ -939,6 +939,30 @@ def main():
             if rank == 0 and not ok.item() and "error" not in rccl_native:
                 rccl_native["error"] = "a non-zero rank's child failed"
 
+    # SURVEY §8(e) strong-scaled local reduce on the MPI path's host buffers:
+    # one 256 MiB fp32 MPI_SUM vector split over every GPU of the node, each
+    # GPU over its own PCIe link (msx_reduce_local_multi), rank 0 after the
+    # collectives while the other ranks wait; against the same call on one GPU
+    multi_host = None
+    if world > 1 and rank == 0 and not args.no_host_path:
+        import numpy as np
+        ngpu = torch.cuda.device_count()
+        ha = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
+        hb = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
+        exp = hb + ha
+        multi_host = {"bytes_per_operand": n * 4, "gpus_visible": ngpu, "host_memory": "pageable"}
+        for g in sorted({1, ngpu}):
+            hb2 = hb.copy()
+            rc = L.msx_reduce_local_multi(ha.ctypes.data, hb2.ctypes.data, n, C.MPI_FLOAT, C.MPI_SUM, g)
+            ok = rc == 0 and hb2.tobytes() == exp.tobytes()
+            ts = []
+            for _ in range(3):
+                t1 = time.perf_counter()
+                L.msx_reduce_local_multi(ha.ctypes.data, hb2.ctypes.data, n, C.MPI_FLOAT, C.MPI_SUM, g)
+                ts.append(time.perf_counter() - t1)
+            t = sorted(ts)[1]
+            multi_host[f"{g}_gpu"] = {"ms_per_call": round(t * 1e3, 2), "payload_GiB_s": round(n * 4 / t / 2**30, 2),
+                                      "correct_first_call": ok}
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
     host = None
@@ -1049,6 +1073,8 @@ def main():
                                                    "false, 0> (the default body under its probe name)"})
         if host is not None:
             out["host_path"] = host
+        if multi_host is not None:
+            out["host_path_multi_gpu"] = multi_host
         def summarize(c):
             """c3-c5 of one data plane at a glance: correct, busBW, fractions."""
             if not c:

@@ -117,6 +117,14 @@ int msx_unpack_dev(const void* packed, int64_t count, MPI_Datatype datatype, voi
  * ((s0 op s1) op (s2 op s3)) op ((s4 op s5) op (s6 op s7)), the left operand
  * of each combine in the reference's `inout` role.  p in {1,2,4,8,16};
  * srcs is a HOST array of device pointers; out may alias srcs[0]. */
+/* SURVEY 8(e), the local reduce strong-scaled: inout[i] = inout[i] (op) in[i]
+ * over one vector split into contiguous 256-byte-aligned ranges, one per GPU
+ * of the node (ngpus <= 0: every visible GPU).  Host operands are pinned once
+ * and each GPU combines its range in place over its own PCIe link; device
+ * operands (and vectors under 1 MiB) stay on one GPU.  Blocking; MPI error
+ * classes returned.  MSX_REDUCE_LOCAL_GPUS=k routes MPI_Reduce_local here. */
+int msx_reduce_local_multi(const void* in, void* inout, int64_t count, MPI_Datatype datatype, MPI_Op op,
+                           int ngpus);
 int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count,
                         MPI_Datatype datatype, MPI_Op op, void* stream);
 

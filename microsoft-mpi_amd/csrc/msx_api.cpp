@@ -713,7 +713,17 @@ MSX_EXPORT int MPI_Reduce_local(const void* inbuf, void* inoutbuf, int count,
     if (rc == MPI_SUCCESS && inoutbuf == MPI_IN_PLACE) { set_error("inoutbuf is MPI_IN_PLACE"); rc = MPI_ERR_BUFFER; }
     if (rc == MPI_SUCCESS) rc = v_dtype_any(inbuf, count, datatype);   // :343
     if (rc == MPI_SUCCESS && inbuf == inoutbuf) { set_error("inbuf aliases inoutbuf"); rc = MPI_ERR_BUFFER; }
-    if (rc == MPI_SUCCESS) rc = local_combine(r, datatype, inbuf, inoutbuf, (size_t)count);
+    // MSX_REDUCE_LOCAL_GPUS=k (k = 0: every GPU of the node): host operands
+    // split over k GPUs' PCIe links (reduce_local_multi); for single-process
+    // use -- in a job with one rank per GPU each rank would use them all
+    static const int multi = [] {
+        const char* e = getenv("MSX_REDUCE_LOCAL_GPUS");
+        return e ? atoi(e) : 1;
+    }();
+    if (rc == MPI_SUCCESS && multi != 1 && r.opidx != O_NULL && type_info(datatype))
+        rc = reduce_local_multi(r.opidx, type_info(datatype)->kind, inbuf, inoutbuf, (size_t)count, multi);
+    else if (rc == MPI_SUCCESS)
+        rc = local_combine(r, datatype, inbuf, inoutbuf, (size_t)count);
     return err_return(nullptr, "MPI_Reduce_local", rc);
 }
 
@@ -2399,6 +2409,23 @@ MSX_EXPORT int msx_reduce_local_dev(const void* in, void* inout, int64_t count, 
     if (rc != MPI_SUCCESS) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);   // NULL = the HIP null stream
     return reduce_local_device(r.opidx, type_info(dt)->kind, in, inout, (size_t)count, s);
+}
+
+// one MPI_Reduce_local-sized vector split over the node's GPUs
+// (ngpus <= 0: all visible), host operands over each GPU's own PCIe link;
+// MPI_Reduce_local's checks, error codes returned (no error handler).
+MSX_EXPORT int msx_reduce_local_multi(const void* in, void* inout, int64_t count, MPI_Datatype dt, MPI_Op op,
+                                      int ngpus)
+{
+    if (count == 0) return MPI_SUCCESS;
+    OpRef r;
+    int rc = v_op(op, dt, &r);
+    if (rc != MPI_SUCCESS) return rc;
+    if (r.opidx == O_NULL || !type_info(dt)) { set_error("multi-GPU entry point takes builtin ops only"); return MPI_ERR_OP; }
+    if (count < 0) { set_error("negative count"); return MPI_ERR_COUNT; }
+    if (!in || !inout) { set_error("null buffer"); return MPI_ERR_BUFFER; }
+    if (in == inout) { set_error("inbuf aliases inoutbuf"); return MPI_ERR_BUFFER; }
+    return reduce_local_multi(r.opidx, type_info(dt)->kind, in, inout, (size_t)count, ngpus);
 }
 
 MSX_EXPORT int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count,

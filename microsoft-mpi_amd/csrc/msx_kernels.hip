@@ -847,11 +847,13 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
         for (int i = 0; i < 2 * t.P; ++i) a.s[i] = t.src[i];
         ns = 0;
         const int nl = (t.nleaves > 0 && t.nleaves <= t.P) ? t.nleaves : t.P;
-        for (int i = nl; i < t.P; ++i) a.s[2 * i] = a.s[2 * i + 1] = t.src[0];   // never read
+        // absent leaves read leaf 0's source (tree_fixed MASKED loads every slot; the
+        // same addresses in the same wave hit L2) and never use it
+        for (int i = nl; i < t.P; ++i) a.s[2 * i] = a.s[2 * i + 1] = t.src[0];
         for (int i = 0; i < nl; ++i) {
             if (!t.src[2 * i]) return hipErrorInvalidValue;
             if ((t.pairmask >> i) & 1u) { if (!t.src[2 * i + 1]) return hipErrorInvalidValue; }
-            else a.s[2 * i + 1] = t.src[2 * i];   // keep alignment check simple
+            else a.s[2 * i + 1] = t.src[2 * i];   // unpaired: the leaf's own source (read, not used)
         }
         ns = 2 * t.P;
     }

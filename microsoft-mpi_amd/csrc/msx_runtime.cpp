@@ -611,6 +611,88 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "host-staged combine");
 }
 
+// SURVEY §8(e), the local reduce strong-scaled: one MPI_Reduce_local-sized
+// vector split into k contiguous ranges (256-byte aligned), one per GPU of the
+// node, no exchange.  Host operands (the MPI path's send / receive buffers) are
+// pinned once for the call, portable to every device, and each GPU reads and
+// writes its range in place over its OWN PCIe link, so the host-memory rate
+// scales with the links (one GPU: ~23 GiB/s payload, PCIe-bound).  Operands in
+// HBM stay on their GPU: splitting them would move HBM bytes over xGMI, ~100x
+// below the local roofline.  Falls back to the one-GPU path when the pin is
+// refused or k = 1.
+int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t count, int ngpus)
+{
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    const int nvis = device_count_noinit();
+    int g = ngpus <= 0 || ngpus > nvis ? nvis : ngpus;
+    BufInfo bi = classify(in), bo = classify(inout);
+    const size_t esz = (size_t)kind_size(k), bytes = count * esz;
+    if (g <= 1 || bi.place == Place::Device || bo.place == Place::Device || bytes < ((size_t)1 << 20))
+        return reduce_local_any(opidx, k, in, inout, count);
+    // page-rounded registration of the operands not pinned already (one range
+    // when they share pages); pinned ones (hipHostMalloc) are used as they are
+    const uintptr_t pg = 4096;
+    uintptr_t a0 = (uintptr_t)in & ~(pg - 1), a1 = ((uintptr_t)in + bytes + pg - 1) & ~(pg - 1);
+    uintptr_t b0 = (uintptr_t)inout & ~(pg - 1), b1 = ((uintptr_t)inout + bytes + pg - 1) & ~(pg - 1);
+    std::vector<std::pair<uintptr_t, uintptr_t>> rg;
+    if (!bi.dev && !bo.dev && a0 < b1 && b0 < a1) rg.push_back({std::min(a0, b0), std::max(a1, b1)});
+    else {
+        if (!bi.dev) rg.push_back({a0, a1});
+        if (!bo.dev) rg.push_back({b0, b1});
+    }
+    size_t nreg = 0;
+    for (auto& r : rg) {
+        if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first,
+                            hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        ++nreg;
+    }
+    auto unpin = [&] {
+        for (size_t i = 0; i < nreg; ++i) (void)hipHostUnregister(reinterpret_cast<void*>(rg[i].first));
+    };
+    if (nreg != rg.size()) {
+        unpin();
+        trace("reduce_local_multi: pin refused, one GPU");
+        return reduce_local_any(opidx, k, in, inout, count);
+    }
+    static std::mutex mu;
+    static std::vector<hipStream_t> streams;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)streams.size() < nvis) streams.resize((size_t)nvis, nullptr);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    LaunchCfg cfg = g_cfg;
+    cfg.host = true;
+    hipError_t e = hipSuccess;
+    const size_t align_el = esz >= 256 ? 1 : 256 / esz;
+    for (int d = 0; d < g && e == hipSuccess; ++d) {
+        size_t lo = count * (size_t)d / (size_t)g, hi = count * (size_t)(d + 1) / (size_t)g;
+        lo -= lo % align_el;
+        if (d + 1 < g) hi -= hi % align_el;
+        if (hi <= lo) continue;
+        e = hipSetDevice(d);
+        if (e == hipSuccess && !streams[(size_t)d]) e = hipStreamCreateWithFlags(&streams[(size_t)d], hipStreamNonBlocking);
+        void *din = nullptr, *dio = nullptr;
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&din, const_cast<void*>(in), 0);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&dio, inout, 0);
+        if (e == hipSuccess)
+            e = launch_combine(opidx, k, static_cast<const char*>(din) + lo * esz, static_cast<char*>(dio) + lo * esz,
+                               hi - lo, streams[(size_t)d], cfg);
+    }
+    for (int d = 0; d < g; ++d) {
+        if (!streams[(size_t)d]) continue;
+        (void)hipSetDevice(d);
+        hipError_t e2 = hipStreamSynchronize(streams[(size_t)d]);
+        if (e == hipSuccess) e = e2;
+    }
+    (void)hipSetDevice(cur);
+    unpin();
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "multi-GPU combine");
+}
+
 namespace {
 struct Roctx {
     int (*push)(const char*) = nullptr;

@@ -108,6 +108,11 @@ int host_mode();
 // Returns an MPI error class.
 int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t count);
 
+// The same combine split over the node's GPUs (ngpus <= 0: every visible
+// one), each range over its own PCIe link; host operands only (device
+// operands and small vectors take reduce_local_any).  Blocking.
+int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t count, int ngpus);
+
 // Same, stream-ordered, both operands device-accessible.
 int reduce_local_device(int opidx, Kind k, const void* in, void* inout, size_t count,
                         hipStream_t s);

@@ -1544,14 +1544,17 @@ PipeEvents& pipe_events()
     return e;
 }
 
-// The pipelined allreduce collects chunk i (result wait + OUT -> recvbuf copy)
-// on the aux stream while the engine stream pushes chunk i + 1
-// (MSX_COLLECT_OVERLAP=0: one stream).
+// MSX_COLLECT_OVERLAP=1: the pipelined allreduce collects chunk i (result
+// wait + OUT -> recvbuf copy) on the aux stream while the engine stream
+// pushes chunk i + 1.  Off by default: 2 ranks sharing one MI355X, c3 1 GiB,
+// two interleaved rounds (scripts/c3_pipeline_ab.sh, profiles/r04/c3ab/):
+// one stream 1.87-1.96 ms, overlapped 2.18 ms -- the two streams compete for
+// the GPU with the other rank's pushes.  Worth re-measuring one rank per GPU.
 bool collect_overlap()
 {
     static const bool on = [] {
         const char* e = getenv("MSX_COLLECT_OVERLAP");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     return on;
 }

@@ -43,10 +43,23 @@ for k in range(8):
     assert L.msx_probe_hbm(4, fill.data_ptr(), ctypes.c_void_p(srcs[k]), n * 4, sp) == 0   # engine copy kernel
 torch.cuda.synchronize()
 
-cases = {
-    "p6_fold_P4_pairs2": (4, 0b11, 4, [srcs[0], srcs[1], srcs[2], srcs[3], srcs[4], srcs[4], srcs[5], srcs[5]], 6),
-    "p7_binomial_P8_leaves7": (8, 0, 7, [srcs[k // 2] if k % 2 == 0 else srcs[0] for k in range(16)], 7),
-}
+def fold(P, pm):
+    # leaf k = (slot 2k, slot 2k+1 when paired); sources numbered in slot order
+    ptrs, nsrc = [], 0
+    for k in range(P):
+        a = srcs[nsrc]; nsrc += 1
+        b = srcs[nsrc] if (pm >> k) & 1 else a
+        nsrc += (pm >> k) & 1
+        ptrs += [a, b]
+    return ptrs, nsrc
+
+
+cases = {}
+for name, P, pm in (("p3_fold_P2", 2, 0b1), ("p5_fold_P4", 4, 0b1), ("p6_fold_P4", 4, 0b11), ("p7_fold_P4", 4, 0b111)):
+    ptrs, ns = fold(P, pm)
+    cases[name] = (P, pm, P, ptrs, ns)
+for nl in (5, 6, 7):
+    cases[f"p{nl}_binomial_P8"] = (8, 0, nl, [srcs[k // 2] if k % 2 == 0 and k // 2 < nl else srcs[0] for k in range(16)], nl)
 
 
 def timed(fn, reps=10):

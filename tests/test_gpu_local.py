@@ -488,6 +488,38 @@ def test_tree_folds_dram_regime_fp32(L):
     assert torch.equal(out.view(torch.int32), exp.view(torch.int32))
 
 
+@pytest.mark.parametrize("ngpus", [0, 1, 2, 8])
+def test_reduce_local_multi_gpu_host_operands(L, ngpus):
+    """msx_reduce_local_multi (one vector split over the node's
+    GPUs, host operands over each GPU's PCIe link): bit-exact against the
+    oracle for pageable and pinned host operands, a ragged count (range ends
+    not on the 256-B grid), below and above the 1 MiB split threshold.  On a
+    one-GPU box every ngpus clamps to that GPU; the driver's 8-GPU node runs
+    the real split."""
+    rng = np.random.default_rng(77 + ngpus)
+    for n, op, dt in (((3 << 20) // 4 + 5, "MPI_SUM", "MPI_FLOAT"), (1000, "MPI_SUM", "MPI_FLOAT"),
+                      ((5 << 20) // 8 + 3, "MPI_MAX", "MPI_DOUBLE"), ((2 << 20) + 7, "MPI_BXOR", "MPI_BYTE")):
+        a, b = _raw(gen(KIND[dt], op, n, rng)), _raw(gen(KIND[dt], op, n, rng))
+        exp = _raw(b)
+        assert oracle.reduce_local(h(op), h(dt), a, exp) == 0
+        for pinned in (False, True):
+            if pinned:
+                ta = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory()
+                tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
+                pa, pb = ta.data_ptr(), tb.data_ptr()
+            else:
+                ha, hb = _raw(a), _raw(b)
+                pa, pb = ha.ctypes.data, hb.ctypes.data
+            rc = L.msx_reduce_local_multi(pa, pb, n, h(dt), h(op), ngpus)
+            assert rc == 0, msx.last_error()
+            got = tb.numpy().tobytes() if pinned else hb.tobytes()
+            assert got == exp.tobytes(), (op, dt, n, pinned, ngpus)
+    # checks as MPI_Reduce_local: aliasing, unsupported pair
+    x = np.ones(8, np.float32)
+    assert L.msx_reduce_local_multi(x.ctypes.data, x.ctypes.data, 8, C.MPI_FLOAT, C.MPI_SUM, ngpus) == C.MPI_ERR_BUFFER
+    assert L.msx_reduce_local_multi(x.ctypes.data, x.ctypes.data + 4, 1, C.MPI_BYTE, C.MPI_SUM, ngpus) == C.MPI_ERR_OP
+
+
 def test_copy_geometries_exact(L):
     # the engine's local copy in both geometries (probe modes 8 / 9: k_copy_segs'
     # XCD-contiguous tiles, k_copy_dram's one-wave dispatch order) and the
