@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-per-op", action="store_true", help="skip the per-(op, type) roofline table")
     ap.add_argument("--no-pack", action="store_true", help="skip the datatype pack/unpack table")
     ap.add_argument("--rccl-native-child", metavar="OUT", help=argparse.SUPPRESS)
+    ap.add_argument("--multi-host-child", metavar="OUT", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -190,6 +191,56 @@ def rccl_native_allreduce(world, rank, local, scale):
         except (OSError, ValueError) as e:
             return {"error": str(e)}
     return {}
+
+
+def multi_host_child_main(out, n):
+    """Child body of run_multi_host_child: one process, every visible GPU."""
+    import numpy as np
+    import torch
+    import msx
+    os.environ["MSX_SIZE"], os.environ["MSX_RANK"] = "1", "0"
+    L = msx.init(errors_return=True)
+    C = msx.C
+    ngpu = torch.cuda.device_count()
+    ha = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
+    hb = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
+    exp = hb + ha
+    res = {"bytes_per_operand": n * 4, "gpus_visible": ngpu, "host_memory": "pageable",
+           "api": "msx_reduce_local_multi (pinned for the call, each GPU over its own PCIe link)"}
+    for g in sorted({1, ngpu}):
+        hb2 = hb.copy()
+        rc = L.msx_reduce_local_multi(ha.ctypes.data, hb2.ctypes.data, n, C.MPI_FLOAT, C.MPI_SUM, g)
+        ok = rc == 0 and hb2.tobytes() == exp.tobytes()
+        ts = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            L.msx_reduce_local_multi(ha.ctypes.data, hb2.ctypes.data, n, C.MPI_FLOAT, C.MPI_SUM, g)
+            ts.append(time.perf_counter() - t1)
+        t = sorted(ts)[1]
+        res[f"{g}_gpu"] = {"ms_per_call": round(t * 1e3, 2), "payload_GiB_s": round(n * 4 / t / 2**30, 2),
+                           "correct_first_call": ok}
+    with open(out, "w") as f:
+        json.dump(res, f)
+
+
+def run_multi_host_child(n):
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"msx_multi_host_{os.getpid()}.json")
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MSX_DEVICE"):
+        env.pop(k, None)
+    try:
+        pr = subprocess.run([sys.executable, os.path.abspath(__file__), "--multi-host-child", out,
+                             "--elems", str(n)], env=env, capture_output=True, text=True, timeout=120)
+        if pr.returncode != 0:
+            return {"error": f"child rc={pr.returncode}: {pr.stderr[-600:]}"}
+        with open(out) as f:
+            return json.load(f)
+    except subprocess.TimeoutExpired:
+        return {"error": "child timed out"}
+    except (OSError, ValueError) as e:
+        return {"error": str(e)}
 
 
 def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 1, 256, true, false>"):
@@ -778,6 +829,9 @@ def main():
     if args.rccl_native_child:
         rccl_native_child_main(args.rccl_native_child, args.coll_scale)
         return
+    if args.multi_host_child:
+        multi_host_child_main(args.multi_host_child, args.elems)
+        return
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args))
@@ -941,28 +995,13 @@ def main():
 
     # SURVEY §8(e) strong-scaled local reduce on the MPI path's host buffers:
     # one 256 MiB fp32 MPI_SUM vector split over every GPU of the node, each
-    # GPU over its own PCIe link (msx_reduce_local_multi), rank 0 after the
-    # collectives while the other ranks wait; against the same call on one GPU
+    # GPU over its own PCIe link (msx_reduce_local_multi), against the same call
+    # on one GPU -- rank 0, after the collectives while the other ranks wait,
+    # in a child process with a time limit (like the collectives) so a failure
+    # there can never take this JSON line down
     multi_host = None
     if world > 1 and rank == 0 and not args.no_host_path:
-        import numpy as np
-        ngpu = torch.cuda.device_count()
-        ha = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
-        hb = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
-        exp = hb + ha
-        multi_host = {"bytes_per_operand": n * 4, "gpus_visible": ngpu, "host_memory": "pageable"}
-        for g in sorted({1, ngpu}):
-            hb2 = hb.copy()
-            rc = L.msx_reduce_local_multi(ha.ctypes.data, hb2.ctypes.data, n, C.MPI_FLOAT, C.MPI_SUM, g)
-            ok = rc == 0 and hb2.tobytes() == exp.tobytes()
-            ts = []
-            for _ in range(3):
-                t1 = time.perf_counter()
-                L.msx_reduce_local_multi(ha.ctypes.data, hb2.ctypes.data, n, C.MPI_FLOAT, C.MPI_SUM, g)
-                ts.append(time.perf_counter() - t1)
-            t = sorted(ts)[1]
-            multi_host[f"{g}_gpu"] = {"ms_per_call": round(t * 1e3, 2), "payload_GiB_s": round(n * 4 / t / 2**30, 2),
-                                      "correct_first_call": ok}
+        multi_host = run_multi_host_child(n)
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
     host = None
