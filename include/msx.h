@@ -202,6 +202,12 @@ int msx_schedule_algo_dt(int which, int p, int64_t count, MPI_Datatype dt, int n
 int msx_schedule_ireduce_tree(int p, int n, int root, int* src32, int* P, unsigned* pairmask,
                               int* chain);
 int msx_schedule_newrank(int rank, int p);
+/* the pipelined two-step allreduce's chunk plan for `rank` (tests): *chunk_el
+ * elements per chunk; out[3i], out[3i+1], out[3i+2] = first element, end
+ * element and owner newrank of each range of the rank's pieces over all
+ * chunks; returns the range count, -1 if cap triples do not suffice */
+int64_t msx_schedule_two_step(int p, int64_t count, int esz, int rank, int64_t* chunk_el, int64_t* out,
+                              int64_t cap);
 int msx_schedule_block(int p, int64_t count, int n, int64_t* start, int64_t* len);
 
 #ifdef __cplusplus

@@ -2609,6 +2609,33 @@ MSX_EXPORT int msx_schedule_ireduce_tree(int p, int n, int root, int* src32, int
 
 // newrank of `rank`, and the allreduce block owned by newrank n
 MSX_EXPORT int msx_schedule_newrank(int rank, int p) { return newrank_of(rank, p); }
+// The pipelined two-step allreduce / reduce's plan for one rank (tests): the
+// chunk length in elements, and every range of that rank's pieces over all
+// chunks as (first element, end element, owner newrank) triples in out[3i..];
+// returns the number of ranges, or -1 when `cap` triples do not suffice.
+MSX_EXPORT int64_t msx_schedule_two_step(int p, int64_t count, int esz, int rank, int64_t* chunk_el, int64_t* out,
+                                         int64_t cap)
+{
+    if (p < 2 || p > 32 || count <= 0 || esz <= 0 || rank < 0 || rank >= p || !chunk_el || !out) return -1;
+    const size_t pc = two_step_chunk_el(p, (size_t)esz);
+    *chunk_el = (int64_t)pc;
+    if (pc == 0) return 0;
+    std::vector<TwoStepRange> ranges;
+    int64_t n = 0;
+    for (size_t ci = 0; ci * pc < (size_t)count; ++ci) {
+        size_t plo, phi, len;
+        two_step_plan(p, (size_t)count, pc, ci, rank, &ranges, &plo, &phi, &len);
+        for (const TwoStepRange& g : ranges) {
+            if (n >= cap) return -1;
+            out[3 * n] = (int64_t)(ci * pc + g.e0);
+            out[3 * n + 1] = (int64_t)(ci * pc + g.e1);
+            out[3 * n + 2] = g.owner;
+            ++n;
+        }
+    }
+    return n;
+}
+
 MSX_EXPORT int msx_schedule_block(int p, int64_t count, int n, int64_t* start, int64_t* len)
 {
     size_t s, l;

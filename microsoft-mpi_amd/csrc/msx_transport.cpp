@@ -1988,6 +1988,50 @@ int rccl_reduce_scatter(ncclComm_t comm, Comm* c, const void* sendbuf, void* rec
     return rc == MPI_SUCCESS ? sync_stream(s, "reduce_scatter") : rc;
 }
 
+}  // namespace
+
+// Elements per chunk of the pipelined two-step allreduce / reduce for p ranks
+// and elements of esz bytes: p pieces of at most half an IN sub-slot each, the
+// whole chunk within half the OUT area above the recursive-doubling results,
+// whole 16-element pieces (0: the window is too small).
+size_t two_step_chunk_el(int p, size_t esz)
+{
+    const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
+    const size_t qh_el = (Qh / esz) & ~(size_t)15;
+    const size_t out_half = ((chunk_bytes() - Qh) / 2) & ~(size_t)255;
+    size_t pc_el = std::min((size_t)p * qh_el, out_half / esz);
+    return pc_el - pc_el % ((size_t)p * 16);
+}
+
+// Rank me's part of chunk ci: its piece [plo, phi) of the chunk (16-element
+// granules) cut where the owner tree changes -- the owner of an element is
+// that of its block in the WHOLE vector (allreduce_block, reduce.cpp:3927-
+// 4066), so the chunking never changes a result.  Offsets are relative to
+// the chunk start o = ci * pc_el.
+void two_step_plan(int p, size_t count, size_t pc_el, size_t ci, int me, std::vector<TwoStepRange>* ranges,
+                   size_t* plo, size_t* phi, size_t* len_out)
+{
+    const int pof2 = pof2_floor(p);
+    const size_t o = ci * pc_el, len = std::min(pc_el, count - o);
+    const size_t pel = (((len + (size_t)p - 1) / (size_t)p) + 15) & ~(size_t)15;
+    *plo = std::min(len, (size_t)me * pel);
+    *phi = std::min(len, (size_t)(me + 1) * pel);
+    *len_out = len;
+    ranges->clear();
+    const size_t rs = count / (size_t)pof2;
+    for (size_t e0 = *plo; e0 < *phi;) {
+        const size_t ge = o + e0;
+        const int j = rs ? (int)std::min((size_t)pof2 - 1, ge / rs) : pof2 - 1;
+        size_t bst, bl;
+        allreduce_block(p, count, j, &bst, &bl);
+        const size_t e1 = std::min(*phi, bst + bl - o);
+        ranges->push_back({e0, e1, allreduce_block_owner(p, j)});
+        e0 = e1;
+    }
+}
+
+namespace {
+
 // root < 0: allreduce; root >= 0: only `root` receives the result (MPI_Reduce).
 int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
                  const OpRef& op, int root = -1, bool nbc = false)
@@ -2024,10 +2068,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     // OUT area above the recursive-doubling results; a longer message runs as
     // a pipeline of such chunks.  Only count, type, p and the environment
     // decide, so every rank takes the same branch and the same chunks.
-    const size_t qh_el = (Qh / esz) & ~(size_t)15;
     const size_t out_half = ((chunk_bytes() - Qh) / 2) & ~(size_t)255;
-    size_t pc_el = std::min((size_t)p * qh_el, out_half / esz);
-    pc_el -= pc_el % ((size_t)p * 16);                         // whole 16-element pieces
+    const size_t pc_el = two_step_chunk_el(p, esz);
     const bool two_step = algo == A_RABENSEIFNER && p >= 2 && p <= 32 && rd_flags() && tp->has_done() &&
                           count * esz <= two_step_max() && pc_el > 0;
     Windows w;
@@ -2251,7 +2293,6 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         for (int r = 0; r < p; ++r)
             if (r != me) done_to.push_back(w.flags(r) + kDoneFlags + me);
         const size_t nchunks = (count + pc_el - 1) / pc_el;
-        const size_t rs = count / (size_t)pof2;
         unsigned long long seq = 0;
         size_t nranges = 0;
         // collect stream: chunk ci's result wait and copy overlap chunk ci+1's
@@ -2259,8 +2300,11 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // of chunk ci before my trees of chunk ci+2 (same OUT half)
         PipeEvents& ev = pipe_events();
         const hipStream_t sc = (want && nchunks > 1 && ev.ok && collect_overlap()) ? aux_stream() : s;
+        std::vector<TwoStepRange> ranges;
         for (size_t ci = 0; ci < nchunks && rc == MPI_SUCCESS; ++ci) {
-            const size_t o = ci * pc_el, len = std::min(pc_el, count - o);
+            const size_t o = ci * pc_el;
+            size_t plo, phi, len;
+            two_step_plan(p, count, pc_el, ci, me, &ranges, &plo, &phi, &len);
             const size_t pel = (((len + (size_t)p - 1) / (size_t)p) + 15) & ~(size_t)15;
             auto lo_of = [&](int r) { return std::min(len, (size_t)r * pel); };
             auto hi_of = [&](int r) { return std::min(len, (size_t)(r + 1) * pel); };
@@ -2289,20 +2333,6 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             }
             for (int d : dests)
                 if (d != me) done.push_back(w.flags(d) + kResultFlags + me);
-            // my piece, cut where the owner tree changes (block boundaries of
-            // the whole vector)
-            const size_t plo = lo_of(me), phi = hi_of(me);
-            struct Range { size_t e0, e1; int owner; };
-            std::vector<Range> ranges;
-            for (size_t e0 = plo; e0 < phi;) {
-                const size_t ge = o + e0;
-                const int j = rs ? (int)std::min((size_t)pof2 - 1, ge / rs) : pof2 - 1;
-                size_t bst, bl;
-                allreduce_block(p, count, j, &bst, &bl);
-                const size_t e1 = std::min(phi, bst + bl - o);
-                ranges.push_back({e0, e1, allreduce_block_owner(p, j)});
-                e0 = e1;
-            }
             nranges += ranges.size();
             for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
             subs[(size_t)me] = const_cast<char*>(mine) + plo * esz;
@@ -2319,7 +2349,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce result flags");
             }
             for (size_t i = 0; i < ranges.size() && rc == MPI_SUCCESS; ++i) {
-                const Range& g = ranges[i];
+                const TwoStepRange& g = ranges[i];
                 const RankTree t = !is_reduce ? tree_allreduce(p, g.owner)
                                               : (nbc ? tree_ireduce_rsag(p, g.owner, root) : tree_reduce_rsag(p, g.owner));
                 std::vector<char*> extra;

@@ -115,6 +115,11 @@ int reduce_scatter_algo(int p, size_t total_count, int type_size, bool commutati
 int reduce_algo(int p, size_t count, int type_size, bool builtin);
 // allreduce Rabenseifner blocks: block j = [start, start+len), computed at newrank owner
 void allreduce_block(int p, size_t count, int j, size_t* start, size_t* len);
+// the pipelined two-step allreduce's chunk plan (msx_transport.cpp)
+struct TwoStepRange { size_t e0, e1; int owner; };
+size_t two_step_chunk_el(int p, size_t esz);
+void two_step_plan(int p, size_t count, size_t pc_el, size_t ci, int me, std::vector<TwoStepRange>* ranges,
+                   size_t* plo, size_t* phi, size_t* len);
 int allreduce_block_owner(int p, int j);           // newrank that owns block j
 int allreduce_block_of_newrank(int p, int n);
 // Tree spec (in real ranks) for the value newrank n computes:

@@ -165,6 +165,7 @@ def lib():
         "msx_last_error": (ctypes.c_char_p, []),
         "msx_op_check": (i, [i, i]),
         "msx_operands_on_device": (i, [p, p]),
+        "msx_schedule_two_step": (i64, [i, i64, i, i, ctypes.POINTER(i64), ctypes.POINTER(i64), i64]),
         "msx_reduce_local_multi": (i, [p, p, i64, i, i, i]),
         "msx_reduce_tree_spec_dev": (i, [ctypes.POINTER(p), i, ctypes.c_uint, i, i, p, i64, i, i, p]),
         "msx_type_size": (i, [i]),

@@ -784,3 +784,38 @@ def test_intercommunicators_six_processes():
         assert d["errs"] == [C.MPI_ERR_COMM, C.MPI_ERR_COMM, C.MPI_ERR_COMM, C.MPI_ERR_COMM, C.MPI_ERR_COMM,
                              C.MPI_ERR_RANK, C.MPI_ERR_BUFFER, C.MPI_ERR_ROOT, C.MPI_SUCCESS]
         assert d["ic2_remote"] == {0: [2, 3], 1: [2, 3], 2: [0, 1], 3: [0, 1], 4: [5], 5: [4]}[rank]
+
+
+@pytest.mark.parametrize("p", [2, 3, 5, 6, 7, 8, 9, 16, 32])
+def test_two_step_chunk_plan_covers_and_keeps_owners(p):
+    """The pipelined two-step allreduce's chunk plan (msx_schedule_two_step,
+    the function do_allreduce itself runs): over all ranks and chunks the
+    ranges cover [0, count) exactly once, and each lies inside the block of
+    the owner it is evaluated with (reduce.cpp:3927-4066's block of newrank
+    `owner`) -- so cutting a message into chunks changes the work split, never
+    the tree an element gets."""
+    import msx
+    L = msx.lib()
+    i64 = ctypes.c_int64
+    for esz in (4, 8):
+        ce = i64()
+        L.msx_schedule_two_step(p, 1000, esz, 0, ctypes.byref(ce), (i64 * 3)(), 1)
+        pc = ce.value
+        assert pc > 0 and pc % (p * 16) == 0
+        for count in (p, 1001, 300001, pc - 1, pc, pc + 1, 3 * pc + 12345):
+            cover = []
+            for r in range(p):
+                cap = 4096
+                out = (i64 * (3 * cap))()
+                n = L.msx_schedule_two_step(p, count, esz, r, ctypes.byref(ce), out, cap)
+                assert n >= 0
+                for k in range(n):
+                    e0, e1, owner = out[3 * k], out[3 * k + 1], out[3 * k + 2]
+                    assert 0 <= e0 < e1 <= count
+                    st, ln = i64(), i64()
+                    L.msx_schedule_block(p, count, owner, ctypes.byref(st), ctypes.byref(ln))
+                    assert st.value <= e0 and e1 <= st.value + ln.value, (p, count, r, e0, e1, owner)
+                    cover.append((e0, e1))
+            cover.sort()
+            assert cover[0][0] == 0 and cover[-1][1] == count
+            assert all(a[1] == b[0] for a, b in zip(cover, cover[1:])), (p, count)
