@@ -58,15 +58,26 @@ def parse():
     return ap.parse_args()
 
 
-def run_collectives_child(world, rank, local, scale, transport="ipc"):
+# c3 engine settings timed at N = 8 (one GPU per rank) for the next round's
+# tuning, each in its own child job: the round-3 host-barrier chunks, the
+# default pipeline, the pipeline with the collect overlapped, a 960 MiB window
+C3_VARIANTS = (("host_barrier_chunks_r03", {"MSX_TWO_STEP_MAX": str(256 << 20)}),
+               ("pipeline_default", {}),
+               ("pipeline_collect_overlap", {"MSX_COLLECT_OVERLAP": "1"}),
+               ("pipeline_window_960MiB", {"MSX_CHUNK_BYTES": str(960 << 20)}))
+
+
+def run_collectives_child(world, rank, local, scale, transport="ipc", extra_env=None, tag="", port_off=0):
     """c3-c5 in a child MPI process per rank (isolated from the headline line).
     transport "ipc": IPC windows + xGMI remote writes; "rccl": RCCL send/recv;
     "rccl_native": RCCL's own collectives where the (op, type) pair maps."""
     import subprocess
     import tempfile
-    out = os.path.join(tempfile.gettempdir(), f"msx_coll_{transport}_{os.environ.get('MASTER_PORT', '0')}.json")
+    out = os.path.join(tempfile.gettempdir(),
+                       f"msx_coll_{transport}{tag}_{os.environ.get('MASTER_PORT', '0')}.json")
     env = dict(os.environ)
-    off = {"ipc": 113, "rccl": 127, "rccl_native": 139}[transport]
+    env.update(extra_env or {})
+    off = {"ipc": 113, "rccl": 127, "rccl_native": 139}[transport] + port_off   # same on every rank
     env.update({"MSX_SIZE": str(world), "MSX_RANK": str(rank), "MSX_DEVICE": str(local),
                 "MSX_TRANSPORT": transport,
                 "MSX_BOOTSTRAP_ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
@@ -965,7 +976,7 @@ def main():
 
     # N > 1: the collective configs c3-c5 in child MPI processes (not part of
     # `value`); each rank reports whether its child succeeded.
-    coll = coll_rccl = coll_native = rccl_native = None
+    coll = coll_rccl = coll_native = rccl_native = c3_variants = None
     distinct = torch.cuda.device_count() >= world      # one GPU per rank (RCCL needs it)
     if world > 1 and not args.no_collectives:
         def collect(transport):
@@ -992,6 +1003,21 @@ def main():
             rccl_native = mine if rank == 0 else None
             if rank == 0 and not ok.item() and "error" not in rccl_native:
                 rccl_native["error"] = "a non-zero rank's child failed"
+            if world == 8:
+                c3_variants = {}
+                for vi, (name, extra) in enumerate(C3_VARIANTS):
+                    mine = run_collectives_child(world, rank, local, args.coll_scale, "ipc",
+                                                 dict(extra, MSX_COLL_ONLY="c3"), tag="_" + name,
+                                                 port_off=200 + 11 * vi)
+                    errs = [None] * world
+                    dist.all_gather_object(errs, mine.get("error"))
+                    if rank == 0:
+                        c3 = mine.get("c3_allreduce_sum_f32") or {}
+                        c3_variants[name] = {k: c3.get(k) for k in ("seconds", "busbw_GB_s", "correct",
+                                                                   "chunks_per_call") if k in c3}
+                        c3_variants[name]["env"] = extra
+                        if any(errs):
+                            c3_variants[name]["errors"] = [e for e in errs if e]
 
     # SURVEY §8(e) strong-scaled local reduce on the MPI path's host buffers:
     # one 256 MiB fp32 MPI_SUM vector split over every GPU of the node, each
@@ -1141,6 +1167,8 @@ def main():
             out["collectives_rccl_native_transport"] = coll_native
         if rccl_native is not None:
             out["rccl_native_allreduce_f32"] = rccl_native
+        if c3_variants:
+            out["c3_engine_variants"] = c3_variants
         if per_op is not None:
             out["per_op_roofline_hbm"] = per_op
         if pack is not None:

@@ -95,7 +95,7 @@ def main(out_path, scale):
     # measured link roofline: every rank writes into all peers' windows at once
     # (the scatter step's pattern); busBW is also reported against it
     xgmi_meas = None
-    if p > 1 and res["transport_requested"] == "ipc":
+    if p > 1 and res["transport_requested"] == "ipc" and os.environ.get("MSX_COLL_ONLY") != "c3":
         sec, used = ctypes.c_double(), ctypes.c_int64()
         rc = L.msx_peer_write_bandwidth(max(1 << 20, int((64 << 20) * scale)), 5, ctypes.byref(sec),
                                         ctypes.byref(used))
@@ -138,6 +138,16 @@ def main(out_path, scale):
                 enumerate(("stage_scatter", "collect_wait_barrier_a", "reduce_push", "barrier_b",
                            "final_collect"))}
             res["c3_allreduce_sum_f32"]["chunks_per_call"] = stats[5] / calls
+    if os.environ.get("MSX_COLL_ONLY") == "c3":
+        # one engine setting of c3 only (bench.py's variant sweep at N = 8)
+        barrier()
+        L.msx_engine_transport.restype = ctypes.c_char_p
+        res["transport_used"] = L.msx_engine_transport().decode()
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump(res, f)
+        L.MPI_Finalize()
+        return
     # allreduce latency / bandwidth curve (fp32 SUM, exact integer data)
     curve = {}
     for nbytes in (4 << 10, 256 << 10, 4 << 20, 64 << 20):
