@@ -58,10 +58,12 @@ def parse():
     return ap.parse_args()
 
 
-# c3 engine settings timed at N = 8 (one GPU per rank) for the next round's
-# tuning, each in its own child job: the round-3 host-barrier chunks, the
-# default pipeline, the pipeline with the collect overlapped, a 960 MiB window
+# c3 / c4 engine settings timed at N = 8 (one GPU per rank) for the next
+# round's tuning, each in its own child job: the round-3 host-barrier chunks,
+# the default pipeline, the pipeline with the collect overlapped, a 960 MiB
+# window (2 ranks sharing one GPU: profiles/r04/c3ab/)
 C3_VARIANTS = (("host_barrier_chunks_r03", {"MSX_TWO_STEP_MAX": str(256 << 20)}),
+               ("host_barrier_window_960MiB", {"MSX_TWO_STEP_MAX": str(256 << 20), "MSX_CHUNK_BYTES": str(960 << 20)}),
                ("pipeline_default", {}),
                ("pipeline_collect_overlap", {"MSX_COLLECT_OVERLAP": "1"}),
                ("pipeline_window_960MiB", {"MSX_CHUNK_BYTES": str(960 << 20)}))
@@ -1007,17 +1009,18 @@ def main():
                 c3_variants = {}
                 for vi, (name, extra) in enumerate(C3_VARIANTS):
                     mine = run_collectives_child(world, rank, local, args.coll_scale, "ipc",
-                                                 dict(extra, MSX_COLL_ONLY="c3"), tag="_" + name,
+                                                 dict(extra, MSX_COLL_ONLY="c3c4"), tag="_" + name,
                                                  port_off=200 + 11 * vi)
                     errs = [None] * world
                     dist.all_gather_object(errs, mine.get("error"))
                     if rank == 0:
-                        c3 = mine.get("c3_allreduce_sum_f32") or {}
-                        c3_variants[name] = {k: c3.get(k) for k in ("seconds", "busbw_GB_s", "correct",
-                                                                   "chunks_per_call") if k in c3}
-                        c3_variants[name]["env"] = extra
+                        ent = {"env": extra}
+                        for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4")):
+                            v = mine.get(key) or {}
+                            ent[tag] = {k: v.get(k) for k in ("seconds", "busbw_GB_s", "correct") if k in v}
                         if any(errs):
-                            c3_variants[name]["errors"] = [e for e in errs if e]
+                            ent["errors"] = [e for e in errs if e]
+                        c3_variants[name] = ent
 
     # SURVEY §8(e) strong-scaled local reduce on the MPI path's host buffers:
     # one 256 MiB fp32 MPI_SUM vector split over every GPU of the node, each
@@ -1168,7 +1171,7 @@ def main():
         if rccl_native is not None:
             out["rccl_native_allreduce_f32"] = rccl_native
         if c3_variants:
-            out["c3_engine_variants"] = c3_variants
+            out["c3_c4_engine_variants"] = c3_variants
         if per_op is not None:
             out["per_op_roofline_hbm"] = per_op
         if pack is not None:

@@ -95,7 +95,7 @@ def main(out_path, scale):
     # measured link roofline: every rank writes into all peers' windows at once
     # (the scatter step's pattern); busBW is also reported against it
     xgmi_meas = None
-    if p > 1 and res["transport_requested"] == "ipc" and os.environ.get("MSX_COLL_ONLY") != "c3":
+    if p > 1 and res["transport_requested"] == "ipc" and os.environ.get("MSX_COLL_ONLY") != "c3c4":
         sec, used = ctypes.c_double(), ctypes.c_int64()
         rc = L.msx_peer_write_bandwidth(max(1 << 20, int((64 << 20) * scale)), 5, ctypes.byref(sec),
                                         ctypes.byref(used))
@@ -138,8 +138,48 @@ def main(out_path, scale):
                 enumerate(("stage_scatter", "collect_wait_barrier_a", "reduce_push", "barrier_b",
                            "final_collect"))}
             res["c3_allreduce_sum_f32"]["chunks_per_call"] = stats[5] / calls
-    if os.environ.get("MSX_COLL_ONLY") == "c3":
-        # one engine setting of c3 only (bench.py's variant sweep at N = 8)
+    # ---- c4: reduce_scatter MAX fp64, 4 GiB per rank sendbuf ----------------
+    def c4_section():
+        per = int((512 << 20) * scale) // p                  # recvcount per rank (c4: 2^29 / p)
+        tot = per * p
+        i = torch.arange(tot, device=dev, dtype=torch.int64)
+        send = ((i * 2654435761 + rank * 40503) % 1000003).to(torch.float64)
+        recv = torch.empty(per, device=dev, dtype=torch.float64)
+        counts = (ctypes.c_int * p)(*([per] * p))
+        lo, hi = rank * per, (rank + 1) * per
+        ii = i[lo:hi]
+        exp = torch.full((per,), -1.0, device=dev, dtype=torch.float64)
+        for r in range(p):
+            exp = torch.maximum(exp, ((ii * 2654435761 + r * 40503) % 1000003).to(torch.float64))
+        del i, ii
+        torch.cuda.synchronize()
+        times = []
+        for it in range(3):
+            barrier()
+            t0 = time.perf_counter()
+            rc = L.MPI_Reduce_scatter(send.data_ptr(), recv.data_ptr(), counts, C.MPI_DOUBLE, C.MPI_MAX,
+                                      C.MPI_COMM_WORLD)
+            times.append(time.perf_counter() - t0)
+            log(f"c4 iter {it} rc={rc} {times[-1]:.4f}s")
+            if rc:
+                fail("c4", rc)
+                break
+        if "c4_error" not in res:
+            t = sorted(times[1:])[len(times[1:]) // 2]
+            S = tot * 8
+            res["c4_reduce_scatter_max_f64"] = {
+                "bytes_per_rank": S, "seconds": round(t, 5), "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 2),
+                "busbw_frac_xgmi": round(S / t / 1e9 * (p - 1) / p / XGMI, 3),
+                "busbw_frac_measured_links": (round(S / t / 1e9 * (p - 1) / p / xgmi_meas, 3) if xgmi_meas else None),
+                "correct": bool(torch.equal(recv, exp))}
+        del send, recv, exp
+        torch.cuda.empty_cache()
+
+    if os.environ.get("MSX_COLL_ONLY") == "c3c4":
+        # one engine setting of c3 and c4 only (bench.py's variant sweep at N = 8)
+        del send, recv, exp
+        torch.cuda.empty_cache()
+        c4_section()
         barrier()
         L.msx_engine_transport.restype = ctypes.c_char_p
         res["transport_used"] = L.msx_engine_transport().decode()
@@ -284,41 +324,7 @@ def main(out_path, scale):
     log(f"c5 host done {res.get('c5_host_pageable_iallreduce_band_u64', res.get('c5_host_error'))}")
     del hs5, hr5, he5
 
-    # ---- c4: reduce_scatter MAX fp64, 4 GiB per rank sendbuf ----------------
-    per = int((512 << 20) * scale) // p                  # recvcount per rank (c4: 2^29 / p)
-    tot = per * p
-    i = torch.arange(tot, device=dev, dtype=torch.int64)
-    send = ((i * 2654435761 + rank * 40503) % 1000003).to(torch.float64)
-    recv = torch.empty(per, device=dev, dtype=torch.float64)
-    counts = (ctypes.c_int * p)(*([per] * p))
-    lo, hi = rank * per, (rank + 1) * per
-    ii = i[lo:hi]
-    exp = torch.full((per,), -1.0, device=dev, dtype=torch.float64)
-    for r in range(p):
-        exp = torch.maximum(exp, ((ii * 2654435761 + r * 40503) % 1000003).to(torch.float64))
-    del i, ii
-    torch.cuda.synchronize()
-    times = []
-    for it in range(3):
-        barrier()
-        t0 = time.perf_counter()
-        rc = L.MPI_Reduce_scatter(send.data_ptr(), recv.data_ptr(), counts, C.MPI_DOUBLE, C.MPI_MAX,
-                                  C.MPI_COMM_WORLD)
-        times.append(time.perf_counter() - t0)
-        log(f"c4 iter {it} rc={rc} {times[-1]:.4f}s")
-        if rc:
-            fail("c4", rc)
-            break
-    if "c4_error" not in res:
-        t = sorted(times[1:])[len(times[1:]) // 2]
-        S = tot * 8
-        res["c4_reduce_scatter_max_f64"] = {
-            "bytes_per_rank": S, "seconds": round(t, 5), "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 2),
-            "busbw_frac_xgmi": round(S / t / 1e9 * (p - 1) / p / XGMI, 3),
-            "busbw_frac_measured_links": (round(S / t / 1e9 * (p - 1) / p / xgmi_meas, 3) if xgmi_meas else None),
-            "correct": bool(torch.equal(recv, exp))}
-    del send, recv, exp
-    torch.cuda.empty_cache()
+    c4_section()
 
     # ---- c5: iallreduce BAND u64, 512 MiB, overlapped with host compute ------
     n = int((64 << 20) * scale)

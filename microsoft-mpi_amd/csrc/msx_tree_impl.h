@@ -38,10 +38,10 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
     return hipGetLastError();
 }
 
-// The compile-time-source kernel for every tree of up to 8 leaves and every
-// chain of 2-8 sources: full power-of-two trees, non-power-of-two folds and
-// binomial trees with absent leaves (MASKED, round 4); the generic kernel
-// only beyond 8 (p >= 9) and for the tuning modes.
+// The compile-time-source kernel for every tree of up to 8 leaves without
+// absent leaves -- full power-of-two trees and non-power-of-two folds (MASKED,
+// round 4) -- and every chain of 2-8 sources; the generic kernel for binomial
+// trees with absent leaves, p >= 9, and the tuning modes.
 // DRAM-regime geometry of the compile-time-source kernel (NT: the sources
 // exceed the Infinity Cache): one-wave workgroups in dispatch order, as
 // k_combine_dram, so the eight XCDs read neighbouring tiles of every source.
@@ -86,10 +86,14 @@ hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hi
         case 8: return run_tree_fixed<OP, T, VT, NT, 8, U, false>(a, nsrc, out, count, s);
         default: break;
         }
-    } else {
-        // non-power-of-two folds (p = 3, 5, 6, 7: leaf pairs) and binomial
-        // trees with absent leaves: the leaf count compile-time, the pattern
-        // at run time (tree_fixed MASKED)
+    } else if (a.nleaves == a.P) {
+        // non-power-of-two folds (p = 3, 5, 6, 7: leaf pairs): the leaf count
+        // compile-time, the pattern at run time (tree_fixed MASKED).  Binomial
+        // trees with ABSENT leaves keep the generic kernel: the masked form
+        // loads leaf 0's vectors again for them, which at DRAM sizes costs
+        // more than the generic kernel's leaf tests (p = 5/6/7 over 8 leaves,
+        // 128 MiB per source: 185/199/215 us masked vs 141/163/179 us generic,
+        // scripts/tree_fold_probe.py, profiles/r04/tree_fold_probe.log)
         switch (a.P) {
         case 2: return run_tree_fixed<OP, T, VT, NT, 2, U, false, true>(a, nsrc, out, count, s);
         case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, false, true>(a, nsrc, out, count, s);

@@ -9,7 +9,7 @@ OUT=${1:-gpurun_out/c3ab}
 mkdir -p "$OUT"
 cd "$(dirname "$0")/.." || exit 2
 for round in 1 2; do
-  for cfg in "r03|MSX_TWO_STEP_MAX=268435456" "pipe|MSX_NOTHING=0" "overlap|MSX_COLLECT_OVERLAP=1" "r03_c960|MSX_TWO_STEP_MAX=268435456 MSX_CHUNK_BYTES=1006632960" "pipe_c960|MSX_CHUNK_BYTES=1006632960"; do
+  for cfg in ${CONFIGS:-"r03|MSX_TWO_STEP_MAX=268435456" "pipe|MSX_NOTHING=0" "overlap|MSX_COLLECT_OVERLAP=1" "r03_c960|MSX_TWO_STEP_MAX=268435456 MSX_CHUNK_BYTES=1006632960" "pipe_c960|MSX_CHUNK_BYTES=1006632960"}; do
     name=${cfg%%|*}; kv=${cfg#*|}
     PORT=$((20000 + RANDOM % 20000))
     pids=()
