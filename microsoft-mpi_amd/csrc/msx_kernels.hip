@@ -1016,20 +1016,21 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     f.n = nflags;
     f.seq = seq;
     for (int i = 0; i < nflags; ++i) f.dst[i] = flags[i];
-    // MSX_PUSH_VECS 16-byte granules per workgroup and pass (default 1024:
-    // four per lane) and at most MSX_PUSH_GRID_CAP pushing workgroups in all
-    // (default 2048).  One granule per lane with up to 16384 workgroups (the
-    // copy kernel's geometry) measured no different on the shared GPU
-    // (scripts/push_cmp.sh, profiles/r02/copy/push_cmp.log).
+    // MSX_PUSH_VECS 16-byte granules per workgroup and pass (default 256:
+    // one per lane) and at most MSX_PUSH_GRID_CAP pushing workgroups in all
+    // (default 65536), the copy kernel's geometry.  Rounds 1-3 used 1024 and
+    // 2048, which measured no different up to 64 MiB (profiles/r02/copy/
+    // push_cmp.log) but 4-7% slower at c3/c4 sizes once the chunks were
+    // pipelined (scripts/push_geometry_ab.sh, profiles/r04/pushab/).
     static const size_t per_wg = [] {
         const char* e = getenv("MSX_PUSH_VECS");
-        const long long v = e ? atoll(e) : 1024;
+        const long long v = e ? atoll(e) : 256;
         return v >= 256 ? (size_t)v : (size_t)256;
     }();
     static const size_t grid_cap = [] {
         const char* e = getenv("MSX_PUSH_GRID_CAP");
-        const long long v = e ? atoll(e) : 2048;
-        return v >= 1 ? (size_t)v : (size_t)2048;
+        const long long v = e ? atoll(e) : 65536;
+        return v >= 1 ? (size_t)v : (size_t)65536;
     }();
     size_t gx = (maxb / 16 + per_wg - 1) / per_wg;
     const size_t cap = nseg > 0 ? std::max<size_t>(1, grid_cap / (size_t)nseg) : 1;
