@@ -30,15 +30,15 @@ import test_gpu_multirank as T  # noqa: E402  (the WORKER text, not the tests)
 def main():
     p, passes = int(sys.argv[1]), int(sys.argv[2])
     extra = dict(kv.split("=", 1) for kv in sys.argv[3:])
-    tag = f"p{p}_x{passes}" + "".join(f"_{k}-{v}" for k, v in extra.items())
-    out = os.path.join(REPO, "gpurun_out", "repro", tag)
-    os.makedirs(out, exist_ok=True)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    pq = int(os.environ.get("REPRO_PARENT_QUEUES", "0"))
-    busy = os.environ.get("REPRO_PARENT_BUSY", "0") == "1"
+    # parent settings, from the command line (not passed on to the ranks)
+    pq = int(extra.pop("REPRO_PARENT_QUEUES", os.environ.get("REPRO_PARENT_QUEUES", "0")))
+    busy = extra.pop("REPRO_PARENT_BUSY", os.environ.get("REPRO_PARENT_BUSY", "0")) == "1"
+    tag = f"p{p}_x{passes}" + "".join(f"_{k}-{v}" for k, v in extra.items())
+    out = os.path.join(REPO, "gpurun_out", "repro", tag)
     if pq > 0:
         import torch
         streams = [torch.cuda.Stream() for _ in range(pq)]
@@ -50,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         tag += f"_parentq{pq}" + ("_busy" if busy else "")
         out = os.path.join(REPO, "gpurun_out", "repro", tag)
-        os.makedirs(out, exist_ok=True)
+    os.makedirs(out, exist_ok=True)
     procs, files = [], []
     for r in range(p):
         env = dict(os.environ)
