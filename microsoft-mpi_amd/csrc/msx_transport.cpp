@@ -1323,17 +1323,28 @@ size_t sub_skew(size_t per_rank)
 // 1.88 ms on the shared-GPU rehearsal -- and reverted it: the only wrong
 // results seen in round 3, in the 8-ranks-on-one-GPU stress, appeared after
 // that change; DESIGN.md §2 "Open issue".)
+// MSX_WINDOW_LAYOUT=1 selects that late-round-3 layout again (sub-slots of
+// the whole C/p, the skew on top, an IN area of p * (C/p + skew)), only to
+// rerun the round-3 whole-suite stress under it with the round-4 diagnostics.
+bool skew_on_top()
+{
+    static const bool on = [] {
+        const char* e = getenv("MSX_WINDOW_LAYOUT");
+        return e && atoi(e) == 1;
+    }();
+    return on;
+}
+
 size_t sub_len(size_t C, int p)
 {
     const size_t per = C / (size_t)p;
-    return (per - sub_skew(per)) & ~(size_t)255;
+    return (skew_on_top() ? per : per - sub_skew(per)) & ~(size_t)255;
 }
 
 // IN area of a window: p sub-slots sub_skew apart, C bytes in all
 size_t in_bytes(size_t C, int p)
 {
-    (void)p;
-    return C;
+    return skew_on_top() ? (size_t)p * (sub_len(C, p) + sub_skew(C / (size_t)p)) : C;
 }
 
 struct Windows {
