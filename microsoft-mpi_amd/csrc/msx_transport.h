@@ -40,6 +40,10 @@ public:
     // area after its last barrier, so the first two-step call after one
     // barriers first.  Cleared by every host-barrier window user.
     bool out_quiet = false;
+    // Whether two or more ranks of this communicator run on one GPU (their
+    // PCI bus ids, allgathered at init, so every rank holds the same value).
+    // The GPU-flag Rabenseifner schedules default off there (two_step_max).
+    bool gpu_shared = false;
     // lock-step host collectives over the bootstrap hub (all ranks, same n)
     virtual int allgather(const void* mine, size_t n, void* all) = 0;
     virtual int barrier() = 0;

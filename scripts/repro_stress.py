@@ -57,6 +57,7 @@ def main():
         env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
                     "MSX_BOOTSTRAP_TIMEOUT": "180", "MSX_STRESS_PASSES": str(passes)})
+        env.setdefault("MSX_TWO_STEP_MAX", str(1 << 62))   # the GPU-flag schedules the round-3 failure ran
         env.update(extra)
         f = open(os.path.join(out, f"rank{r}.log"), "w")
         files.append(f)

@@ -141,7 +141,7 @@ def _free_port():
     return port
 
 
-def _run(cfg, p, one_per_gpu=False, transport=None):
+def _run(cfg, p, one_per_gpu=False, transport=None, extra=None):
     port = _free_port()
     procs = []
     for r in range(p):
@@ -152,6 +152,7 @@ def _run(cfg, p, one_per_gpu=False, transport=None):
         if transport:
             env["MSX_TRANSPORT"] = transport
             env["MSX_FLAG_TIMEOUT_MS"] = "60000"
+        env.update(extra or {})
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
@@ -177,12 +178,20 @@ def _run(cfg, p, one_per_gpu=False, transport=None):
     return [[l.split()[1] for l in o.splitlines() if l.startswith("TRANSPORT")] for _, o, _ in results]
 
 
-@pytest.mark.parametrize("cfg,p", [("c3", 2), ("c3", 3), ("c4", 2), ("c5", 2), ("c3", 8), ("c4", 8), ("c5", 8)])
-def test_baseline_config_full_size(cfg, p):
+# Ranks sharing the one GPU take the host-barrier schedules by default since
+# round 4; `flags` forces the GPU-flag ones (the pipelined
+# two-step allreduce, pipelined reduce_scatter rounds) that one rank per GPU
+# runs by default.
+@pytest.mark.parametrize("cfg,p,sched", [("c3", 2, "default"), ("c3", 3, "default"), ("c4", 2, "default"),
+                                         ("c5", 2, "default"), ("c3", 8, "default"), ("c4", 8, "default"),
+                                         ("c5", 8, "default"), ("c3", 2, "flags"), ("c3", 3, "flags"),
+                                         ("c4", 2, "flags"), ("c5", 2, "flags"), ("c3", 8, "flags"),
+                                         ("c4", 8, "flags")])
+def test_baseline_config_full_size(cfg, p, sched):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run(cfg, p)
+    _run(cfg, p, extra={"MSX_TWO_STEP_MAX": str(1 << 62)} if sched == "flags" else None)
 
 
 # The configs at their own layout: 8 ranks, ONE PER GPU (MSX_DEVICE = rank),

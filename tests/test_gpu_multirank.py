@@ -469,12 +469,20 @@ def _free_port():
                                                         (7, 1 << 20, None, None), (3, None, None, "0"),
                                                         (4, 65536, None, "0"), (3, None, None, "unfused"),
                                                         (4, None, None, "ts512k"), (6, None, None, None),
-                                                        (3, None, None, "plain_stores"), (4, None, None, "switch0"),
+                                                        (3, None, None, "plain_stores+ts"), (4, None, None, "switch0"),
                                                         (3, None, None, "switch0"), (5, None, None, "switchmax"),
                                                         (5, 65536, None, "switch0"), (7, None, None, "switchmax"),
                                                         (8, None, None, "switch0"), (3, None, None, "staged"),
-                                                        (4, 1 << 20, None, "cached"), (3, None, "rccl_native", None)])
+                                                        (4, 1 << 20, None, "cached"), (3, None, "rccl_native", None),
+                                                        (2, None, None, "+ts"), (5, None, None, "+ts"),
+                                                        (8, None, None, "+ts"), (3, 65536, None, "+ts"),
+                                                        (8, None, None, "switch0+ts")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
+    """`+ts`: the GPU-flag Rabenseifner schedules (two-step allreduce / reduce,
+    one-step reduce_scatter, flag scan) forced on.  Ranks that share a GPU
+    default to the host-barrier schedules since round 4, so the
+    flag schedules the one-rank-per-GPU deployment runs are tested here by
+    asking for them."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -485,34 +493,38 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
         env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
                     "MSX_BOOTSTRAP_TIMEOUT": "180"})
+        mode = rd_flags
+        if mode and mode.endswith("+ts"):
+            env["MSX_TWO_STEP_MAX"] = str(1 << 62)
+            mode = mode[:-3] or None
         if chunk:
             env["MSX_CHUNK_BYTES"] = str(chunk)     # many chunks, pieces across block edges
         if transport:
             env["MSX_TRANSPORT"] = transport
-        if rd_flags == "unfused":
+        if mode == "unfused":
             env["MSX_FUSED_PUSH"] = "0"             # flag path with a separate push launch
-        elif rd_flags in ("switch0", "switchmax"):
+        elif mode in ("switch0", "switchmax"):
             # the reference's flat switch points moved (mpid/env.cpp:514-608): at 0
             # every allreduce of >= pof2 elements is Rabenseifner (blocks of a few
             # elements) and every reduce_scatter pairwise; the oracle simulation
             # in the worker reads the same variables
-            v = "0" if rd_flags == "switch0" else "2147483647"
+            v = "0" if mode == "switch0" else "2147483647"
             for k in ("ALLREDUCE_SHORT_MSG", "REDUCE_SHORT_MSG", "REDSCAT_COMMUTATIVE_LONG_MSG"):
                 env["MPICH_DEFAULT_" + k] = v
-        elif rd_flags == "cached":
+        elif mode == "cached":
             # the documented fallback: cached windows, every engine kernel with
             # system-scope acquire / release fences
             env["MSX_WINDOW_CACHED"] = "1"
-        elif rd_flags == "staged":
+        elif mode == "staged":
             # host buffers staged through HBM: no call-scoped pinning, no bounce buffers
             env["MSX_HOST_PIN_MIN"] = str(1 << 40)
             env["MSX_HOST_BOUNCE_MAX"] = "0"
-        elif rd_flags == "plain_stores":
+        elif mode == "plain_stores":
             env["MSX_WT_STORES"] = "0"              # two-step pushes / results with plain stores
-        elif rd_flags == "ts512k":
+        elif mode == "ts512k":
             env["MSX_TWO_STEP_MAX"] = str(512 << 10)   # two-step and host-barrier Rabenseifner alternate
-        elif rd_flags is not None:
-            env["MSX_RD_FLAGS"] = rd_flags          # host-barrier small allreduce / reduce
+        elif mode is not None:
+            env["MSX_RD_FLAGS"] = mode          # host-barrier small allreduce / reduce
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
