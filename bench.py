@@ -64,9 +64,9 @@ def parse():
 # window (2 ranks sharing one GPU: profiles/r04/c3ab/)
 C3_VARIANTS = (("host_barrier_chunks_r03", {"MSX_TWO_STEP_MAX": str(256 << 20)}),
                ("host_barrier_window_960MiB", {"MSX_TWO_STEP_MAX": str(256 << 20), "MSX_CHUNK_BYTES": str(960 << 20)}),
-               ("pipeline_default", {}),
-               ("pipeline_collect_overlap", {"MSX_COLLECT_OVERLAP": "1"}),
-               ("pipeline_window_960MiB", {"MSX_CHUNK_BYTES": str(960 << 20)}))
+               ("pipeline", {"MSX_TWO_STEP_MAX": str(1 << 62)}),
+               ("pipeline_collect_overlap", {"MSX_TWO_STEP_MAX": str(1 << 62), "MSX_COLLECT_OVERLAP": "1"}),
+               ("pipeline_window_960MiB", {"MSX_TWO_STEP_MAX": str(1 << 62), "MSX_CHUNK_BYTES": str(960 << 20)}))
 
 
 def run_collectives_child(world, rank, local, scale, transport="ipc", extra_env=None, tag="", port_off=0):
@@ -1005,22 +1005,24 @@ def main():
             rccl_native = mine if rank == 0 else None
             if rank == 0 and not ok.item() and "error" not in rccl_native:
                 rccl_native["error"] = "a non-zero rank's child failed"
-            if world == 8:
-                c3_variants = {}
-                for vi, (name, extra) in enumerate(C3_VARIANTS):
-                    mine = run_collectives_child(world, rank, local, args.coll_scale, "ipc",
-                                                 dict(extra, MSX_COLL_ONLY="c3c4"), tag="_" + name,
-                                                 port_off=200 + 11 * vi)
-                    errs = [None] * world
-                    dist.all_gather_object(errs, mine.get("error"))
-                    if rank == 0:
-                        ent = {"env": extra}
-                        for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4")):
-                            v = mine.get(key) or {}
-                            ent[tag] = {k: v.get(k) for k in ("seconds", "busbw_GB_s", "correct") if k in v}
-                        if any(errs):
-                            ent["errors"] = [e for e in errs if e]
-                        c3_variants[name] = ent
+        # the engine-variant sweep (IPC plane only) at N = 8, or at the N that
+        # MSX_BENCH_VARIANTS_AT names (a rehearsal of this code on fewer GPUs)
+        if world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")):
+            c3_variants = {}
+            for vi, (name, extra) in enumerate(C3_VARIANTS):
+                mine = run_collectives_child(world, rank, local, args.coll_scale, "ipc",
+                                             dict(extra, MSX_COLL_ONLY="c3c4"), tag="_" + name,
+                                             port_off=200 + 11 * vi)
+                errs = [None] * world
+                dist.all_gather_object(errs, mine.get("error"))
+                if rank == 0:
+                    ent = {"env": extra}
+                    for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4")):
+                        v = mine.get(key) or {}
+                        ent[tag] = {k: v.get(k) for k in ("seconds", "busbw_GB_s", "correct") if k in v}
+                    if any(errs):
+                        ent["errors"] = [e for e in errs if e]
+                    c3_variants[name] = ent
 
     # SURVEY §8(e) strong-scaled local reduce on the MPI path's host buffers:
     # one 256 MiB fp32 MPI_SUM vector split over every GPU of the node, each
