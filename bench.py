@@ -59,14 +59,16 @@ def parse():
 
 
 # c3 / c4 engine settings timed at N = 8 (one GPU per rank) for the next
-# round's tuning, each in its own child job: the round-3 host-barrier chunks,
-# the default pipeline, the pipeline with the collect overlapped, a 960 MiB
-# window (2 ranks sharing one GPU: profiles/r04/c3ab/)
-C3_VARIANTS = (("host_barrier_chunks_r03", {"MSX_TWO_STEP_MAX": str(256 << 20)}),
-               ("host_barrier_window_960MiB", {"MSX_TWO_STEP_MAX": str(256 << 20), "MSX_CHUNK_BYTES": str(960 << 20)}),
-               ("pipeline", {"MSX_TWO_STEP_MAX": str(1 << 62)}),
+# round's tuning, each in its own child job: the round-3 host-barrier chunks
+# (512 MiB window), host-barrier chunks in the default 960 MiB window, the
+# pipeline in the round-4 512 MiB window, the pipeline with the collect
+# overlapped, the default pipeline (2 ranks sharing one GPU:
+# profiles/r04/c3ab/, profiles/r04/bench_n2_variants.json)
+C3_VARIANTS = (("host_barrier_chunks_r03", {"MSX_TWO_STEP_MAX": str(256 << 20), "MSX_CHUNK_BYTES": str(512 << 20)}),
+               ("host_barrier_window_960MiB", {"MSX_TWO_STEP_MAX": str(256 << 20)}),
+               ("pipeline_window_512MiB", {"MSX_TWO_STEP_MAX": str(1 << 62), "MSX_CHUNK_BYTES": str(512 << 20)}),
                ("pipeline_collect_overlap", {"MSX_TWO_STEP_MAX": str(1 << 62), "MSX_COLLECT_OVERLAP": "1"}),
-               ("pipeline_window_960MiB", {"MSX_TWO_STEP_MAX": str(1 << 62), "MSX_CHUNK_BYTES": str(960 << 20)}))
+               ("pipeline", {"MSX_TWO_STEP_MAX": str(1 << 62)}))
 
 
 def run_collectives_child(world, rank, local, scale, transport="ipc", extra_env=None, tag="", port_off=0):

@@ -1283,10 +1283,15 @@ char* dev_scratch(size_t bytes)
 // only after barrier A of chunk i+1 (I collected chunk i before it).  After a
 // collective's last barrier B no peer touches my window, so the next
 // collective needs no extra barrier.
+// Default C = 960 MiB, the largest whose window (2 C + flags) stays below the
+// 2 GiB IPC mapping limit: 1.9 GB of each rank's 288 GB.  Rounds 1-4 used
+// 512 MiB; with the larger window c3 takes 3 pipelined chunks instead of 5 at
+// p = 8, and 2 ranks on one MI355X measured c3 1.87 -> 1.77 ms and c4 3.80 ->
+// 3.60 ms (bench.py's engine-variant sweep, profiles/r04/bench_n2_variants.json).
 size_t chunk_bytes()
 {
     static size_t c = [] {
-        size_t v = (size_t)512 << 20;
+        size_t v = (size_t)960 << 20;
         if (const char* e = getenv("MSX_CHUNK_BYTES")) v = (size_t)atoll(e);
         if (v < ((size_t)1 << 16)) v = (size_t)1 << 16;
         if (v > ((size_t)960 << 20)) v = (size_t)960 << 20;   // whole window < 2 GiB (IPC limit)
