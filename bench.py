@@ -412,7 +412,7 @@ def _mem_available():
     return 16 << 30
 
 
-def cpu_baseline_collectives(p=8, reps=3):
+def cpu_baseline_collectives(p=8, reps=20, warmup=3):
     """The reference's collective schedules on the host CPU with p THREADS as
     the p ranks (oracle/msx_oracle_threads.c, restated from mpid/reduce.cpp:
     Rabenseifner allreduce :3927-4066, recursive-halving reduce_scatter
@@ -423,7 +423,8 @@ def cpu_baseline_collectives(p=8, reps=3):
     per-rank sizes (c3 1 GiB fp32 SUM, c4 4 GiB MAX fp64 send buffer, c5
     512 MiB BAND u64) unless host memory is short, then halved until the
     footprint (send + recv + tmp per rank) fits half of MemAvailable; the
-    median of `reps` calls (inputs refilled outside the timed region),
+    median of `reps` calls after `warmup` untimed ones (>= 20
+    after 3; inputs refilled outside the timed region),
     checked against the closed form.  busBW uses the GPU formulas
     (S/t*2(p-1)/p for allreduce, S/t*(p-1)/p for reduce_scatter)."""
     import oracle
@@ -441,12 +442,12 @@ def cpu_baseline_collectives(p=8, reps=3):
         per_rank_vec = count * (p if which == 1 else 1) * esz          # S: the rank's input bytes
         while count > 1024 and p * foot * (count * (p if which == 1 else 1) * esz) > avail / 2:
             count //= 2
-        rc, ts = oracle.coll_threads(which, op, dt, p, count, reps)
-        ts = sorted(ts)
+        rc, ts = oracle.coll_threads(which, op, dt, p, count, reps + warmup)
+        ts = sorted(ts[warmup:])
         t = ts[len(ts) // 2]
         S = count * (p if which == 1 else 1) * esz
         out[name] = {"bytes_per_rank": S, "config_bytes_per_rank": per_rank_vec,
-                     "scaled": count != full, "seconds": round(t, 5), "calls": reps,
+                     "scaled": count != full, "seconds": round(t, 5), "calls": reps, "warmup_calls": warmup,
                      "correct": rc == 0,
                      "busbw_GB_s": round(S / t / 1e9 * bus * (p - 1) / p, 3)}
         if rc:

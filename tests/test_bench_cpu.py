@@ -53,7 +53,7 @@ def test_cpu_baseline_collectives_scales_to_memory(monkeypatch):
     sys.path.insert(0, REPO)
     import bench
     monkeypatch.setattr(bench, "_mem_available", lambda: 3 << 30)   # force scaling on this host
-    out = bench.cpu_baseline_collectives(8, reps=1)
+    out = bench.cpu_baseline_collectives(8, reps=1, warmup=1)
     assert out["threads"] == 8 and out["kind"] == "port"
     for k in ("c3_allreduce_sum_f32", "c4_reduce_scatter_max_f64", "c5_allreduce_band_u64"):
         e = out[k]
