@@ -984,10 +984,14 @@ def main():
     coll = coll_rccl = coll_native = rccl_native = c3_variants = None
     distinct = torch.cuda.device_count() >= world      # one GPU per rank (RCCL needs it)
     if world > 1 and not args.no_collectives:
+        ipc_failed = [False]
+
         def collect(transport):
             mine = run_collectives_child(world, rank, local, args.coll_scale, transport)
             errs = [None] * world
             dist.all_gather_object(errs, mine.get("error"))      # every rank's structured error
+            if transport == "ipc":
+                ipc_failed[0] = any(e is not None for e in errs)   # the same on every rank
             res = mine if rank == 0 else None
             if rank == 0 and any(e is not None for e in errs):
                 res["errors"] = [dict(e, rank=r) if isinstance(e, dict) else {"rank": r, "text": e}
@@ -1010,7 +1014,11 @@ def main():
                 rccl_native["error"] = "a non-zero rank's child failed"
         # the engine-variant sweep (IPC plane only) at N = 8, or at the N that
         # MSX_BENCH_VARIANTS_AT names (a rehearsal of this code on fewer GPUs)
-        if world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")):
+        # (skipped when the default IPC run failed: its variants would only
+        # repeat the failure, each up to its child's time limit)
+        if world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")) and ipc_failed[0]:
+            c3_variants = {"skipped": "the default IPC collectives child failed (see collectives.error)"}
+        elif world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")):
             c3_variants = {}
             for vi, (name, extra) in enumerate(C3_VARIANTS):
                 mine = run_collectives_child(world, rank, local, args.coll_scale, "ipc",
