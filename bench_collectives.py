@@ -260,7 +260,26 @@ def main(out_path, scale):
             "busbw_GB_s": round(nh * 4 / t / 1e9 * 2 * (p - 1) / p, 2),
             "correct": bool(np.array_equal(hrecv, hexp))}
     log(f"c3 host done {res.get('c3_host_pageable_allreduce_sum_f32', res.get('c3_host_error'))}")
-    del hsend, hrecv, hexp
+    # the same on pinned (page-locked) host buffers, SURVEY 8(d)'s other host variant
+    psend = torch.from_numpy(hsend).pin_memory()
+    precv = torch.empty(nh, dtype=torch.float32).pin_memory()
+    ts = []
+    for it in range(4):
+        barrier()
+        t0 = time.perf_counter()
+        rc = L.MPI_Allreduce(psend.data_ptr(), precv.data_ptr(), nh, C.MPI_FLOAT, C.MPI_SUM, C.MPI_COMM_WORLD)
+        ts.append(time.perf_counter() - t0)
+        if rc:
+            fail("c3_host_pinned", rc)
+            break
+    if "c3_host_pinned_error" not in res:
+        t = sorted(ts[1:])[len(ts[1:]) // 2]
+        res["c3_host_pinned_allreduce_sum_f32"] = {
+            "bytes_per_rank": nh * 4, "seconds": round(t, 5), "algbw_GB_s": round(nh * 4 / t / 1e9, 2),
+            "busbw_GB_s": round(nh * 4 / t / 1e9 * 2 * (p - 1) / p, 2),
+            "correct": bool(np.array_equal(precv.numpy(), hexp))}
+    log(f"c3 pinned done {res.get('c3_host_pinned_allreduce_sum_f32', res.get('c3_host_pinned_error'))}")
+    del hsend, hrecv, hexp, psend, precv
 
     # ---- c4 / c5 on host memory (the host variant of every GPU
     # config), at bounded sizes: a 512 MiB send buffer per rank for the
