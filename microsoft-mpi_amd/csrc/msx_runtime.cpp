@@ -630,6 +630,18 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
     const size_t esz = (size_t)kind_size(k), bytes = count * esz;
     if (g <= 1 || bi.place == Place::Device || bo.place == Place::Device || bytes < ((size_t)1 << 20))
         return reduce_local_any(opidx, k, in, inout, count);
+    // an operand the caller pinned already is mapped on other GPUs only if it
+    // was pinned portable; otherwise the one-GPU path (no kernel on a device
+    // that cannot address it)
+    for (const void* p : {in, static_cast<const void*>(inout)}) {
+        const BufInfo& b = p == in ? bi : bo;
+        unsigned flags = 0;
+        if (b.dev && (hipHostGetFlags(&flags, const_cast<void*>(p)) != hipSuccess || !(flags & hipHostMallocPortable))) {
+            (void)hipGetLastError();
+            trace("reduce_local_multi: caller-pinned operand not portable, one GPU");
+            return reduce_local_any(opidx, k, in, inout, count);
+        }
+    }
     // page-rounded registration of the operands not pinned already (one range
     // when they share pages); pinned ones (hipHostMalloc) are used as they are
     const uintptr_t pg = 4096;
