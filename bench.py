@@ -258,7 +258,7 @@ def run_multi_host_child(n):
         return {"error": str(e)}
 
 
-def traffic_from_profiles(kernel_substr="k_combine<3, float, float, 1, 256, true, false>"):
+def traffic_from_profiles(kernel_substr="k_combine_dram<3, float, float, 64, true, false>"):
     """Per-launch HBM bytes of the default fp32 SUM kernel from the newest
     committed rocprofv3 PMC collection (profiles/<round>/pmc_*counter_collection.csv,
     FETCH_SIZE and WRITE_SIZE collected in separate passes)."""
@@ -673,8 +673,9 @@ def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12, mixes=True):
     cold method gives the copy-like stream mix is what the kernel does without
     the cache.  Reported beside `value`, never part of it."""
     sp = ctypes.c_void_p(stream.cuda_stream)
-    # the default kernel body under its probe symbol (k_combine_rr<..., 0>), so
-    # these single launches stay out of the headline symbol's rocprof average
+    # the default kernel body under its probe symbol (k_combine_rr<..., 64, ...,
+    # -2>, the body of k_combine_dram), so these single launches stay out of
+    # the headline symbol's rocprof average
     L.msx_tune_variant_name.restype = ctypes.c_char_p
     probe_v = [v for v in range(L.msx_tune_variant_count())
                if L.msx_tune_variant_name(v).decode() == "default_body_probe"]
@@ -705,7 +706,8 @@ def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12, mixes=True):
     a2.random_(0, 256)
     b2.random_(0, 256)
     torch.cuda.synchronize()
-    kinds, mixes = (((2, "copy_r1w1", 2), (0, "read2", 2)) if mixes else ()), {}
+    kinds, mixes = (((2, "copy_r1w1", 2), (9, "copy_r1w1_dispatch_order", 2), (0, "read2", 2))
+                    if mixes else ()), {}
     for mode, name, streams in kinds:
         pt = []
         for _ in range(reps):
@@ -727,17 +729,19 @@ def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12, mixes=True):
             "warm_single_us": round(wms * 1e3, 1), "cold_probe_GB_s": mixes,
             "method": "median of 12 single launches, each after a 1 GiB read + write pass over other data "
                       "(cold) or right after the previous launch (warm); HIP events on the launch stream; "
-                      "the default kernel body under its probe symbol k_combine_rr<3, float, float, 1, 256, "
-                      "true, false, 0>"}
+                      "the default kernel body under its probe symbol k_combine_rr<3, float, float, 1, 64, "
+                      "true, false, -2>"}
 
 
 def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
-    """What this GPU's HBM delivers for other stream mixes under the combine's
-    own launch geometry (k_probe: 16 B per lane, 256-lane workgroups, one tile
-    each, XCD-contiguous, non-temporal loads), on the same 2 x 256 MiB
-    operands: 2 reads, 1 read, 1 write, 1 read + 1 write.  Median of 3 rounds
-    of 10 launches, HIP events on the launch stream.  Context for the
-    roofline's `frac` (which stays against the 8 TB/s spec peak)."""
+    """What this GPU's HBM delivers for other stream mixes on the same
+    2 x 256 MiB operands, in the tile geometry (k_probe: 16 B per lane,
+    256-lane workgroups, one tile each, XCD-contiguous, non-temporal loads):
+    2 reads, 1 read, 1 write, 1 read + 1 write; and the copy in the combine's
+    default geometry at this size (k_copy_dram: one-wave workgroups in
+    dispatch order).  Median of 3 rounds of 10 launches, HIP events on the
+    launch stream.  Context for the roofline's `frac` (which stays against
+    the 8 TB/s spec peak)."""
     sp = ctypes.c_void_p(stream.cuda_stream)
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -746,6 +750,7 @@ def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
         b.random_(0, 256)
     out = {}
     for mode, name, streams in ((0, "read2", 2), (3, "read1", 1), (1, "write1", 1), (2, "copy_r1w1", 2),
+                                (9, "copy_r1w1_dispatch_order", 2),
                                 (6, "write_16of32B", 0.5), (7, "read_16of32B", 0.5)):
         ts = []
         for _ in range(3):
@@ -1150,8 +1155,9 @@ def main():
                                     "kernel_us_cold": cold["cold_us"],
                                     "cold_method": "median of 12 single launches, each after a 1 GiB read + "
                                                    "write pass over other data (flushes the 256 MiB MALL); "
-                                                   "kernel symbol k_combine_rr<3, float, float, 1, 256, true, "
-                                                   "false, 0> (the default body under its probe name)"})
+                                                   "kernel symbol k_combine_rr<3, float, float, 1, 64, true, "
+                                                   "false, -2> (the default body, k_combine_dram's, under its "
+                                                   "probe name)"})
         if host is not None:
             out["host_path"] = host
         if multi_host is not None:

@@ -489,11 +489,23 @@ inline void split(const void* in, const void* io, size_t count, size_t& head, si
 }
 
 // Bytes per operand above which the device combine takes k_combine_dram
-// (MSX_COMBINE_DRAM_MIN overrides; the Infinity Cache is 256 MiB).
+// (MSX_COMBINE_DRAM_MIN overrides): 16 MiB, where the two operands outgrow the
+// chip's L2 (8 x 4 MiB).  Rounds 1-4 switched only above the 256 MiB Infinity
+// Cache.  fp32 SUM, HIP events, interleaved (scripts/combine_size_sweep.py,
+// profiles/r04/combine_geometry/), XCD-contiguous tiles -> dispatch order,
+// GB/s back to back / with the Infinity Cache flushed first:
+//    16 MiB 7077 -> 6560 / 4309 -> 4280 (L2-resident: tiles stay)
+//    32 MiB 6357 -> 6614 / 4954 -> 5287     64 MiB 6221 -> 6458 / 5216 -> 5599
+//   128 MiB 6639 -> 6742 / 5298 -> 6031    192 MiB 6926 -> 6864 / 5609 -> 6106
+//   256 MiB 7114 -> 6999 / 5751 -> 6097
+// Dispatch order wins cold at every size above L2 (+5-14 %) and back to back
+// up to 128 MiB; from 160 MiB, back to back on the same operands, the
+// Infinity Cache replays part of each launch and the tiles are 0.4-1.6 %
+// ahead.  Operands that size are rarely still cached when a reduction comes.
 size_t combine_dram_min()
 {
     static const size_t v = [] {
-        size_t b = (size_t)256 << 20;
+        size_t b = (size_t)16 << 20;
         if (const char* e = getenv("MSX_COMBINE_DRAM_MIN")) b = (size_t)atoll(e);
         return b;
     }();
@@ -648,7 +660,7 @@ struct Variant {
     hipError_t (*fn)(const void*, void*, size_t, hipStream_t, const LaunchCfg&);
 };
 const Variant kF32SumVariants[] = {
-    {"u1_b256_ntld", run_combine<O_SUM, float, float, 1, 256, true, false>},
+    {"default", run_combine<O_SUM, float, float, 1, 256, true, false>},
     {"u1_b128_ntld", run_combine<O_SUM, float, float, 1, 128, true, false>},
     {"u1_b512_ntld", run_combine<O_SUM, float, float, 1, 512, true, false>},
     {"u1_b1024_ntld", run_combine<O_SUM, float, float, 1, 1024, true, false>},
@@ -678,10 +690,14 @@ const Variant kF32SumVariants[] = {
     {"u1_b512_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 512, true, false, -1>},
     {"u1_b256_ntall_rr", run_combine_rr<O_SUM, float, float, 1, 256, true, true, -1>},
     {"u4_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 4, 256, true, false, -1>},
-    // the default kernel's exact body under another symbol (k_combine_rr<..., 0>):
-    // bench.py times its single cold-cache launches with it, so the rocprof
-    // statistics of the headline symbol hold only the back-to-back launches
-    {"default_body_probe", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 0>},
+    // rounds 1-4's default below 256 MiB: XCD-contiguous 256-thread tiles
+    {"u1_b256_ntld_tiles", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 0>},
+    // the default kernel's exact body above 16 MiB per operand (k_combine_dram:
+    // one-wave workgroups in dispatch order) under another symbol
+    // (k_combine_rr<..., 64, ..., -2>): bench.py times its single cold-cache
+    // launches with it, so the rocprof statistics of the headline symbol hold
+    // only the back-to-back launches
+    {"default_body_probe", run_combine_rr<O_SUM, float, float, 1, 64, true, false, -2>},
 };
 constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
 

@@ -32,7 +32,7 @@ with open(os.path.join(SRC, "bench.log")) as f:
 with open(os.path.join(DST, "bench_sweep.log"), "w") as f:
     f.writelines(sweep)
 shutil.copy(os.path.join(SRC, "prof_trace", "trace_kernel_stats.csv"), DST)
-keep = ("k_combine<3, float, float, 1, 256, true, false>", "k_dt_", "k_tree<3, float, float, 256, false, false, 8, 1, false>")
+keep = ("k_combine_dram<3, float, float, 64, true, false>", "k_combine<3, float, float, 1, 256, true, false>", "k_dt_", "k_tree<3, float, float, 256, false, false, 8, 1, false>")
 with open(os.path.join(SRC, "prof_trace", "trace_kernel_trace.csv")) as fi, \
         open(os.path.join(DST, "trace_kernel_trace.csv"), "w", newline="") as fo:
     r, w = csv.reader(fi), csv.writer(fo)

@@ -3,7 +3,7 @@
 # two PMC passes (FETCH_SIZE, WRITE_SIZE; one counter group each), smoke.
 # Stops at the first failing step.
 cd "$(dirname "$0")/.." || exit 2
-OUT=gpurun_out/r04
+OUT=${OUT:-gpurun_out/r04}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 set -o pipefail
