@@ -55,6 +55,7 @@ for mib in [int(x) for x in os.environ.get("SIZES", "16,32,64,128,256").split(",
             row.setdefault(name + "/warm", []).append(round(2 * nb / warm / 1e6, 1))
             row.setdefault(name + "/cold", []).append(round(2 * nb / cms / 1e6, 1))
             b.zero_()
+            torch.cuda.synchronize()      # the library's stream does not order after torch's
     out[str(mib)] = {k: sorted(v)[len(v) // 2] for k, v in row.items()}
     print(json.dumps({mib: out[str(mib)]}), file=sys.stderr, flush=True)
     del a, b
