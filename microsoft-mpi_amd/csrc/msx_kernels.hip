@@ -1071,12 +1071,17 @@ hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned lon
     return hipGetLastError();
 }
 
-// Bytes of one local copy above which it takes k_copy_dram (MSX_COPY_DRAM_MIN,
-// default the combine's 256 MiB, see combine_dram_min).
+// Bytes of one local copy above which it takes k_copy_dram (MSX_COPY_DRAM_MIN):
+// 16 MiB, as the combine (combine_dram_min).  Rounds 1-4 switched above
+// 256 MiB.  HIP events, interleaved (scripts/copy_geometry_probe.py,
+// profiles/r04/combine_geometry/copy.json), tiles -> dispatch order, GB/s back
+// to back / cache flushed: 16 MiB 4637 -> 4284 / 3277 -> 3452 (tiles stay),
+// 32 MiB 4981 -> 5384 / 4153 -> 4427, 64 MiB 5696 -> 6025 / 4706 -> 5335,
+// 128 MiB 6475 -> 6822 / 5247 -> 5780, 256 MiB 7150 -> 7259 / 5836 -> 6237.
 size_t copy_dram_min()
 {
     static const size_t v = [] {
-        size_t b = (size_t)256 << 20;
+        size_t b = (size_t)16 << 20;
         if (const char* e = getenv("MSX_COPY_DRAM_MIN")) b = (size_t)atoll(e);
         return b;
     }();
