@@ -690,6 +690,10 @@ const Variant kF32SumVariants[] = {
     {"u1_b512_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 512, true, false, -1>},
     {"u1_b256_ntall_rr", run_combine_rr<O_SUM, float, float, 1, 256, true, true, -1>},
     {"u4_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 4, 256, true, false, -1>},
+    // round 4: around the dispatch-order default (k_combine_dram = u1_b64_ntld_rr)
+    {"u2_b64_ntld_rr", run_combine_rr<O_SUM, float, float, 2, 64, true, false, -1>},
+    {"u1_b64_ntall_rr", run_combine_rr<O_SUM, float, float, 1, 64, true, true, -1>},
+    {"u1_b64_plain_rr", run_combine_rr<O_SUM, float, float, 1, 64, false, false, -1>},
     // rounds 1-4's default below 256 MiB: XCD-contiguous 256-thread tiles
     {"u1_b256_ntld_tiles", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 0>},
     // the default kernel's exact body above 16 MiB per operand (k_combine_dram:
