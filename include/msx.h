@@ -47,7 +47,9 @@ int msx_device_count(void);
 const char* msx_engine_transport(void);
 /* phase timers of the window allreduce since the last reset (seconds):
  * out[0] stage+scatter, [1] collect wait + barrier A, [2] reduce + push,
- * [3] barrier B, [4] final collect, [5] chunks, [6] calls; returns 7 */
+ * [3] barrier B, [4] final collect, [5] chunks, [6] calls, [7] calls that
+ * took the GPU-flag Rabenseifner schedules (two-step allreduce / reduce,
+ * flag reduce_scatter); returns 8 */
 int msx_engine_stats(double* out, int n, int reset);
 /* link roofline probe over MPI_COMM_WORLD (collective): every rank writes
  * bytes_per_peer (capped at the window sub-slot) into each peer's window at

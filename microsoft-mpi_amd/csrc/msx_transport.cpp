@@ -1545,6 +1545,7 @@ int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
 struct EngineStats {
     double t[5] = {0, 0, 0, 0, 0};
     long chunks = 0, calls = 0;
+    long flag_calls = 0;   // GPU-flag Rabenseifner calls (two-step allreduce / reduce, flag reduce_scatter)
 };
 EngineStats g_stats;
 
@@ -2419,6 +2420,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             }
             tp->rd_parity ^= 1;
         }
+        ++g_stats.flag_calls;
         const int rsy = sync_stream(s, "allreduce two-step");
         if (rc == MPI_SUCCESS) rc = rsy;
         if (sc != s) {
@@ -2663,6 +2665,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
             tp->rd_parity ^= 1;
         }
         if (rc == MPI_SUCCESS && mycnt && in_place) rc = copy_async(dst, out, mycnt * esz, s);
+        ++g_stats.flag_calls;
         const int rs = sync_stream(s, "reduce_scatter one-step");
         if (rc == MPI_SUCCESS) rc = rs;
         if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
@@ -3887,11 +3890,11 @@ int engine_rma_fence(RmaWin* w)
 int engine_stats(double* out, int n, int reset)
 {
     return worker().submit([out, n, reset]() -> int {
-        const double v[7] = {g_stats.t[0], g_stats.t[1], g_stats.t[2], g_stats.t[3], g_stats.t[4],
-                             (double)g_stats.chunks, (double)g_stats.calls};
-        for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+        const double v[8] = {g_stats.t[0], g_stats.t[1], g_stats.t[2], g_stats.t[3], g_stats.t[4],
+                             (double)g_stats.chunks, (double)g_stats.calls, (double)g_stats.flag_calls};
+        for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
         if (reset) g_stats = EngineStats();
-        return 7;
+        return 8;
     }).get();
 }
 

@@ -431,6 +431,9 @@ for it in range(240 * passes):
 
 L.msx_engine_transport.restype = ctypes.c_char_p
 print("TRANSPORT", L.msx_engine_transport().decode(), flush=True)
+st = (ctypes.c_double * 8)()
+L.msx_engine_stats(st, 8, 0)
+print("FLAGCALLS", int(st[7]), flush=True)       # GPU-flag Rabenseifner calls of this rank
 print("RESULT", rank, p, len(fails), fails[:12], flush=True)
 L.MPI_Finalize()
 '''
@@ -541,6 +544,15 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
         # RCCL needs one GPU per rank: ranks sharing a GPU keep the IPC engine
         n_dev = torch.cuda.device_count()
         assert used == [transport if transport in ("rccl", "rccl_native") and n_dev >= p else "ipc"], used
+        # ranks sharing the GPU run the GPU-flag Rabenseifner schedules only
+        # when asked: the stress loop's 100,003- and
+        # 300,001-int calls take them with `+ts` / `ts512k`, never by default
+        flag_calls = [int(l.split()[1]) for l in o.splitlines() if l.startswith("FLAGCALLS")]
+        if transport is None:
+            if rd_flags and (rd_flags.endswith("+ts") or rd_flags == "ts512k"):
+                assert flag_calls and flag_calls[0] > 0, (rd_flags, flag_calls)
+            else:
+                assert flag_calls == [0], (rd_flags, flag_calls)
 
 
 # One rank per GPU -- the deployment the north star names.  The one-GPU box
