@@ -41,6 +41,10 @@ extern "C" {
 const char* msx_version(void);
 /* number of visible GPUs (0 on a host without one); never aborts */
 int msx_device_count(void);
+/* diagnosis only (MSX_PUSH_VERIFY=1): out[0..3] = the push re-check counters
+ * (destination mismatches, source mismatches, all-zero loaded vectors, last
+ * mismatching vector + 1); -1 when the checks are off */
+int msx_push_verify_counts(unsigned* out);
 /* data plane of the collective engine for MPI_COMM_WORLD: "rccl" (RCCL
  * send/recv over xGMI, MSX_TRANSPORT=rccl and one GPU per rank), "ipc" (IPC
  * windows + remote writes) or "self" (one rank) */

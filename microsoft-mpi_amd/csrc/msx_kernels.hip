@@ -1015,6 +1015,21 @@ unsigned long long flag_wait_ticks()
 
 double flag_wait_seconds() { return (double)flag_wait_ticks() / 1e8; }
 
+// MSX_PUSH_VERIFY=1 (diagnosis only): the device counter block of
+// copy_post_body's store / source re-checks (CopySegs::dbg); nullptr otherwise.
+unsigned* push_verify_counts()
+{
+    static unsigned* d = [] {
+        unsigned* p = nullptr;
+        const char* e = getenv("MSX_PUSH_VERIFY");
+        if (!e || atoi(e) == 0) return p;
+        if (hipMalloc(reinterpret_cast<void**>(&p), 64) != hipSuccess) return (unsigned*)nullptr;
+        if (hipMemset(p, 0, 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return (unsigned*)nullptr;
+        return p;
+    }();
+    return d;
+}
+
 hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
                             unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,
@@ -1027,6 +1042,7 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     PostFlags f{};
     size_t maxb = 0;
     c.n = nseg > 0 ? nseg : 1;
+    c.dbg = push_verify_counts();
     for (int i = 0; i < nseg; ++i) {
         c.src[i] = src[i];
         c.dst[i] = dst[i];

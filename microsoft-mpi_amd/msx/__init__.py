@@ -162,6 +162,7 @@ def lib():
         "MPI_Wtime": (ctypes.c_double, []),
         "msx_version": (ctypes.c_char_p, []),
         "msx_device_count": (i, []),
+        "msx_push_verify_counts": (i, [ctypes.POINTER(ctypes.c_uint)]),
         "msx_last_error": (ctypes.c_char_p, []),
         "msx_op_check": (i, [i, i]),
         "msx_operands_on_device": (i, [p, p]),
