@@ -380,6 +380,20 @@ def stress_diag(it, n, got, tot):
     return (f"[{bad.size} differ, first {bad[0]} last {bad[-1]}; got/exp {sample}; "
             f"explained by: {', '.join(hyp[:8]) or 'none of the tested'}]")
 
+def upload_check(tag, t, a):
+    # the device copy of a send buffer really holds what was uploaded (a
+    # host-to-device copy that lost bytes would look like a wrong reduction)
+    back = fromdev(t, a)
+    if back.tobytes() != a.tobytes():
+        bad = np.nonzero(back != a)[0]
+        fails.append(f"{tag} upload mismatch [{bad.size} differ, first {bad[0]} last {bad[-1]}]")
+
+def reread(tag, t, exp):
+    # a mismatch read a second time: clean now = the first device-to-host
+    # readback was wrong, not the device buffer
+    again = fromdev(t, exp)
+    return f"{tag}: second readback {'clean' if again.tobytes() == exp.tobytes() else 'same error'}"
+
 passes = int(os.environ.get("MSX_STRESS_PASSES", "1"))
 for it in range(240 * passes):
     # recursive doubling / binomial (GPU flags) up to 64 Ki ints, the two-step
@@ -389,6 +403,8 @@ for it in range(240 * passes):
         print("PASS", it // 240, len(fails), flush=True)
     tot = sum(ivec(it, r, n).astype(np.int64) for r in range(p)).astype(np.int32)
     sb = todev(ivec(it, rank, n))
+    if n >= 100003:
+        upload_check(f"stress {it}", sb, ivec(it, rank, n))
     if it % 7 == 3:                        # rooted reduce: arrival flags, push to the root only
         root = it % p
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
@@ -402,12 +418,17 @@ for it in range(240 * passes):
         full = [ivec(it, r, n * p) for r in range(p)]
         mine_tot = sum(f[rank * n:(rank + 1) * n].astype(np.int64) for f in full).astype(np.int32)
         sb = todev(full[rank])
+        if n >= 100003:
+            upload_check(f"stress rsb {it}", sb, full[rank])
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
         rc = L.MPI_Reduce_scatter_block(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD)
         if rc:
             fails.append(f"stress rsb {it} rc={rc} {msx.last_error()}")
             break
-        check(f"stress rsb {it} n={n}", fromdev(rb, mine_tot), mine_tot)
+        got_rs = fromdev(rb, mine_tot)
+        check(f"stress rsb {it} n={n}", got_rs, mine_tot)
+        if got_rs.tobytes() != mine_tot.tobytes():
+            fails.append(reread(f"stress rsb {it}", rb, mine_tot))
         continue
     if it % 11 == 5:                       # non-blocking, through the worker
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
@@ -428,6 +449,7 @@ for it in range(240 * passes):
     got = fromdev(rb, tot)
     if got.tobytes() != tot.tobytes():
         fails.append(f"stress allreduce {it} n={n} {stress_diag(it, n, got, tot)}")
+        fails.append(reread(f"stress allreduce {it}", rb, tot))
 
 L.msx_engine_transport.restype = ctypes.c_char_p
 print("TRANSPORT", L.msx_engine_transport().decode(), flush=True)
@@ -438,7 +460,7 @@ if os.environ.get("MSX_PUSH_VERIFY"):              # diagnosis runs only (DESIGN
     pv = (ctypes.c_uint * 4)()
     if L.msx_push_verify_counts(pv) == 0 and any(pv):
         fails.append(f"push re-check: dst {pv[0]} src {pv[1]} zero {pv[2]} last {pv[3]}")
-print("RESULT", rank, p, len(fails), fails[:12], flush=True)
+print("RESULT", rank, p, len(fails), fails[:16], flush=True)
 L.MPI_Finalize()
 '''
 
