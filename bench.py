@@ -325,6 +325,14 @@ def host_cpu_info():
     except OSError:
         pass
     info["numa_nodes"] = len(glob.glob("/sys/devices/system/node/node[0-9]*")) or None
+    # the cgroup's CPU-time quota (cgroup v2 cpu.max "quota period"): cores'
+    # worth of CPU time the job may burn, whatever its affinity mask allows
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        info["cpu_quota_cores"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return info
 
 
@@ -361,17 +369,33 @@ def cpu_baseline(seconds, elems):
            "sample": f"median of {k1} calls (after 3 warm-ups) of oracle Op<float>::Sum over 2 x {n * 4 >> 20} MiB "
                      f"host buffers, 1 thread = one MS-MPI rank",
            "payload_GiB_s": round(n * 4 / t1 / 2**30, 3), "ms_per_call": round(t1 * 1e3, 3), "cpu": cpu}
-    # every host core of this job, elements sharded across
-    # threads (the box allots 16 cores to a one-GPU job)
-    cores = min(16, cpu.get("cores_allowed") or os.cpu_count() or 1)
-    if cores > 1:
-        tN, kN = _median_rate(lambda: oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=cores),
+    # every host core this job may use (its affinity mask,
+    # `cores_allowed`), elements sharded across threads; beside it the rate by
+    # thread count, which shows where the host's memory bandwidth (or the
+    # job's cgroup CPU quota, `cpu_quota_cores`) stops adding threads paying.
+    allowed = max(1, cpu.get("cores_allowed") or os.cpu_count() or 1)
+    curve = {}
+    for t in sorted({2, 4, 8, 16, 32, 64, 128, allowed}):
+        if t > allowed:
+            continue
+        tt, _ = _median_rate(lambda: oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=t),
+                             n * BYTES_PER_ELEM, 0.3, min_iters=5, warmup=2)
+        curve[str(t)] = round(n * BYTES_PER_ELEM / tt / 2**30, 3)
+    if curve:
+        out["threads_curve_GiB_s"] = curve
+    best = int(max(curve, key=curve.get)) if curve else 1
+    if allowed > 1:
+        tN, kN = _median_rate(lambda: oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, a, b, nthreads=allowed),
                               n * BYTES_PER_ELEM, seconds / 3)
-        out["all_cores"] = {"value": round(n * BYTES_PER_ELEM / tN / 2**30, 3), "unit": "GiB/s", "cores": cores,
+        out["all_cores"] = {"value": round(n * BYTES_PER_ELEM / tN / 2**30, 3), "unit": "GiB/s", "cores": allowed,
                             "payload_GiB_s": round(n * 4 / tN / 2**30, 3), "ms_per_call": round(tN * 1e3, 3),
-                            "sample": f"median of {kN} calls after 3 warm-ups, {cores} threads"}
+                            "sample": f"median of {kN} calls after 3 warm-ups, {allowed} threads "
+                                      f"(every core of the affinity mask)",
+                            "best_threads": best, "best_value": curve.get(str(best))}
     # the same loop by operand size (the host-operand crossover table beside
-    # host_path.pageable_by_size_fp32_sum); one thread and every core
+    # host_path.pageable_by_size_fp32_sum); one thread and the best thread
+    # count of the curve
+    cores = best
     by = {}
     for nb in HOST_SIZES:
         m = max(1, nb // 4)

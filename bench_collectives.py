@@ -43,8 +43,21 @@ def main(out_path, scale):
     # per direction per link; busBW (bytes each GPU moves per direction) is
     # compared with the 7-link per-direction aggregate
     XGMI = 7 * 76.8
+    # Ranks sharing one GPU move every byte through that GPU's HBM: their busBW
+    # is an HBM-plane figure, and no fraction of a link it never used is
+    # emitted for them (the xGMI fields appear only with one rank per GPU).
+    shared = L.msx_engine_gpu_shared() == 1
     res = {"ranks": p, "transport_requested": os.environ.get("MSX_TRANSPORT", "ipc"),
-           "xgmi_aggregate_GB_s_per_direction": XGMI}
+           "gpu_shared": shared, "plane": "hbm (ranks share one GPU)" if shared else "xgmi"}
+    if not shared:
+        res["xgmi_aggregate_GB_s_per_direction"] = XGMI
+
+    def link_fracs(busbw, meas):
+        """xGMI fractions of a busBW figure, for distinct GPUs only."""
+        if shared:
+            return {}
+        return {"busbw_frac_xgmi": round(busbw / XGMI, 3),
+                "busbw_frac_measured_links": round(busbw / meas, 3) if meas else None}
     logf = open(os.environ.get("MSX_BENCH_LOG", os.devnull), "a")
 
     def log(msg):
@@ -102,7 +115,8 @@ def main(out_path, scale):
         if rc == 0 and sec.value > 0:
             xgmi_meas = (p - 1) * used.value / sec.value / 1e9
             res["peer_write_probe"] = {"bytes_per_peer": used.value, "seconds": round(sec.value, 6),
-                                       "outbound_GB_s_per_gpu": round(xgmi_meas, 1)}
+                                       "outbound_GB_s_per_gpu": round(xgmi_meas, 1),
+                                       "plane": res["plane"]}
         else:
             res["peer_write_probe"] = {"error": f"rc={rc} {msx.last_error()}"}
         log(f"peer write probe {res['peer_write_probe']}")
@@ -126,9 +140,7 @@ def main(out_path, scale):
         res["c3_allreduce_sum_f32"] = {
             "bytes_per_rank": S, "seconds": round(t, 5), "algbw_GB_s": round(S / t / 1e9, 2),
             "busbw_GB_s": round(S / t / 1e9 * 2 * (p - 1) / p, 2),
-            "busbw_frac_xgmi": round(S / t / 1e9 * 2 * (p - 1) / p / XGMI, 3),
-            "busbw_frac_measured_links": (round(S / t / 1e9 * 2 * (p - 1) / p / xgmi_meas, 3)
-                                          if xgmi_meas else None),
+            **link_fracs(S / t / 1e9 * 2 * (p - 1) / p, xgmi_meas),
             "correct": bool(torch.equal(recv, exp))}
         L.msx_engine_stats(stats, 7, 1)
         calls = max(stats[6], 1.0)
@@ -169,8 +181,7 @@ def main(out_path, scale):
             S = tot * 8
             res["c4_reduce_scatter_max_f64"] = {
                 "bytes_per_rank": S, "seconds": round(t, 5), "busbw_GB_s": round(S / t / 1e9 * (p - 1) / p, 2),
-                "busbw_frac_xgmi": round(S / t / 1e9 * (p - 1) / p / XGMI, 3),
-                "busbw_frac_measured_links": (round(S / t / 1e9 * (p - 1) / p / xgmi_meas, 3) if xgmi_meas else None),
+                **link_fracs(S / t / 1e9 * (p - 1) / p, xgmi_meas),
                 "correct": bool(torch.equal(recv, exp))}
         del send, recv, exp
         torch.cuda.empty_cache()
@@ -408,8 +419,8 @@ def main(out_path, scale):
             "bytes_per_rank": S, "t_comm_s": round(t_comm, 5), "t_host_s": round(t_host, 5),
             "t_overlapped_s": round(t_total, 5),
             "busbw_GB_s": round(S / t_comm / 1e9 * 2 * (p - 1) / p, 2),
-            "busbw_frac_measured_links": (round(S / t_comm / 1e9 * 2 * (p - 1) / p / xgmi_meas, 3)
-                                          if xgmi_meas else None),
+            **{k: v for k, v in link_fracs(S / t_comm / 1e9 * 2 * (p - 1) / p, xgmi_meas).items()
+               if k == "busbw_frac_measured_links"},
             "overlap_efficiency": round((t_comm + t_host - t_total) / min(t_comm, t_host), 3),
             "correct": bool(torch.equal(recv, exp))}
     del send, recv, exp

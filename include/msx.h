@@ -41,14 +41,14 @@ extern "C" {
 const char* msx_version(void);
 /* number of visible GPUs (0 on a host without one); never aborts */
 int msx_device_count(void);
-/* diagnosis only (MSX_PUSH_VERIFY=1): out[0..3] = the push re-check counters
- * (destination mismatches, source mismatches, all-zero loaded vectors, last
- * mismatching vector + 1); -1 when the checks are off */
-int msx_push_verify_counts(unsigned* out);
 /* data plane of the collective engine for MPI_COMM_WORLD: "rccl" (RCCL
  * send/recv over xGMI, MSX_TRANSPORT=rccl and one GPU per rank), "ipc" (IPC
  * windows + remote writes) or "self" (one rank) */
 const char* msx_engine_transport(void);
+/* 1 when two or more ranks of MPI_COMM_WORLD run on one GPU (their PCI bus ids
+ * agree), 0 when every rank has its own GPU, -1 before MPI_Init; the same on
+ * every rank.  Link fractions (xGMI) mean nothing when it is 1. */
+int msx_engine_gpu_shared(void);
 /* phase timers of the window allreduce since the last reset (seconds):
  * out[0] stage+scatter, [1] collect wait + barrier A, [2] reduce + push,
  * [3] barrier B, [4] final collect, [5] chunks, [6] calls, [7] calls that

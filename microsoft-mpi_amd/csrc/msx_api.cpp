@@ -2288,6 +2288,12 @@ MSX_EXPORT const char* msx_engine_transport(void)
     Comm* c = world();
     return engine_transport_name(c ? c->tp : nullptr);
 }
+MSX_EXPORT int msx_engine_gpu_shared(void)
+{
+    Comm* c = world();
+    if (!c) return -1;
+    return c->tp && c->tp->gpu_shared ? 1 : 0;
+}
 MSX_EXPORT int msx_engine_stats(double* out, int n, int reset)
 {
     if (!out || n < 0) return -1;
@@ -2301,15 +2307,6 @@ MSX_EXPORT int msx_peer_write_bandwidth(int64_t bytes_per_peer, int reps, double
     return engine_peer_write_probe(c, (size_t)bytes_per_peer, reps, seconds, bytes_used);
 }
 MSX_EXPORT int msx_device_count(void) { return device_count_noinit(); }
-// Diagnosis only (MSX_PUSH_VERIFY=1): out[0..3] = the push re-check counters
-// (destination mismatches, source mismatches, all-zero loaded vectors, last
-// mismatching vector + 1); -1 when the checks are off.
-MSX_EXPORT int msx_push_verify_counts(unsigned* out)
-{
-    unsigned* d = push_verify_counts();
-    if (!d || !out) return -1;
-    return hipMemcpy(out, d, 4 * sizeof(unsigned), hipMemcpyDeviceToHost) == hipSuccess ? 0 : MPI_ERR_OTHER;
-}
 MSX_EXPORT const char* msx_last_error(void) { return last_error(); }
 
 MSX_EXPORT int msx_op_check(MPI_Op op, MPI_Datatype dt)

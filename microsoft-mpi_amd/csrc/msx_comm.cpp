@@ -139,9 +139,7 @@ int copy_any(void* dst, const void* src, size_t bytes)
     }
     int rc = ensure_device();
     if (rc != MPI_SUCCESS) return rc;
-    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, internal_stream());
-    if (e == hipSuccess) e = hipStreamSynchronize(internal_stream());
-    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy");
+    return xfer_sync(dst, src, bytes, internal_stream());   // pageable sides through the page-locked ring
 }
 
 // A derived datatype reaches only user functions (the builtin ops' check

@@ -980,10 +980,10 @@ int build_dev_layout(Dtype* t)
         host[2 * n] = acc;
         void* mem = nullptr;
         hipError_t e = hipMalloc(&mem, host.size() * sizeof(int64_t));
-        if (e == hipSuccess) e = hipMemcpy(mem, host.data(), host.size() * sizeof(int64_t), hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            if (mem) (void)hipFree(mem);
-            return hip_fail(e, "datatype layout upload");
+        if (e != hipSuccess) return hip_fail(e, "datatype layout allocation");
+        if ((rc = xfer_sync(mem, host.data(), host.size() * sizeof(int64_t), internal_stream())) != MPI_SUCCESS) {
+            (void)hipFree(mem);
+            return rc;
         }
         t->dev_mem = mem;
         L.disp = static_cast<const int64_t*>(mem);
@@ -1208,7 +1208,7 @@ int dt_pack_any(const Dtype* t, int64_t count, const void* typed, void* packed)
         // keep the user's address modulo 16 so the kernel's granule choice holds
         const uintptr_t mis = (uintptr_t)(static_cast<const char*>(typed) + lo) & 15;
         char* base = st + mis;
-        e = hipMemcpyAsync(base, static_cast<const char*>(typed) + lo, span, hipMemcpyHostToDevice, s);
+        if ((rc = xfer_sync(base, static_cast<const char*>(typed) + lo, span, s)) != MPI_SUCCESS) return rc;
         tdev = base - lo;
         st += span + 16;
     } else {
@@ -1218,8 +1218,7 @@ int dt_pack_any(const Dtype* t, int64_t count, const void* typed, void* packed)
     else pdev = static_cast<char*>(bp.dev);
     if (e != hipSuccess) return hip_fail(e, "datatype pack staging");
     rc = dt_pack_dev(t, count, tdev, pdev, s);
-    if (rc == MPI_SUCCESS && stage_p)
-        e = hipMemcpyAsync(packed, pdev, pbytes, hipMemcpyDeviceToHost, s);
+    if (rc == MPI_SUCCESS && stage_p) return xfer_sync(packed, pdev, pbytes, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     return rc != MPI_SUCCESS ? rc : (e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "datatype pack"));
 }
@@ -1249,7 +1248,7 @@ int dt_unpack_any(const Dtype* t, int64_t count, const void* packed, void* typed
         // the gaps between runs must keep the caller's bytes: stage the whole
         // span in, unpack into it, copy it back
         tbase = st + ((uintptr_t)user_lo & 15);
-        e = hipMemcpyAsync(tbase, user_lo, span, hipMemcpyHostToDevice, s);
+        if ((rc = xfer_sync(tbase, user_lo, span, s)) != MPI_SUCCESS) return rc;
         tdev = tbase - lo;
         st += span + 16;
     } else {
@@ -1257,14 +1256,14 @@ int dt_unpack_any(const Dtype* t, int64_t count, const void* packed, void* typed
     }
     if (e == hipSuccess && stage_p) {
         char* pb = st + ((uintptr_t)packed & 15);
-        e = hipMemcpyAsync(pb, packed, pbytes, hipMemcpyHostToDevice, s);
+        if ((rc = xfer_sync(pb, packed, pbytes, s)) != MPI_SUCCESS) return rc;
         pdev = pb;
     } else {
         pdev = static_cast<const char*>(bp.dev);
     }
     if (e != hipSuccess) return hip_fail(e, "datatype unpack staging");
     rc = dt_unpack_dev(t, count, pdev, tdev, s);
-    if (rc == MPI_SUCCESS && stage_t) e = hipMemcpyAsync(user_lo, tbase, span, hipMemcpyDeviceToHost, s);
+    if (rc == MPI_SUCCESS && stage_t) return xfer_sync(user_lo, tbase, span, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     return rc != MPI_SUCCESS ? rc : (e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "datatype unpack"));
 }

@@ -112,9 +112,6 @@ hipError_t launch_push_post(const void* const* src, void* const* dst, const size
 // wait_flags[r] >= seq for r < wait_n, r != wait_skip (flag_wait_seconds()
 // bound, then wait_tag * 65536 + 1 + r -> *wait_err).  Launches after it on
 // `s` read what the flags announce.
-// MSX_PUSH_VERIFY=1 (diagnosis only): device counters of the push re-checks
-// (CopySegs::dbg in msx_tree_dev.h), nullptr when off.
-unsigned* push_verify_counts();
 hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
                             unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,

@@ -930,7 +930,7 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.wait_flags && !t.push_nseg &&
         !t.done_counter) {
         if (t.src[0] == out) return hipSuccess;
-        return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);
+        return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);   // xfer: device/pinned
     }
     if (opidx == O_SUM && k == K_F32 && g_tree_tune.mode != 0) return tree_tune_f32_sum(g_tree_tune.mode, a, ns, out, n, s);
     switch (opidx) {
@@ -955,7 +955,7 @@ hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStrea
     if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 9) return hipErrorInvalidValue;
     if (mode == 4) return launch_copy_segs(&a, &b, &bytes, 1, false, s);      // the engine's copy kernel
     if (mode == 8 || mode == 9) return launch_copy_one(a, b, bytes, s, mode == 8 ? 0 : 1);   // forced geometry
-    if (mode == 5) return hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, s);   // HIP's blit
+    if (mode == 5) return hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, s);   // HIP's blit; xfer: device/pinned
     // modes 6 / 7 touch every other 16-B vector of `bytes`: nvec = bytes / 32
     const size_t nvec = (mode >= 6) ? bytes / 32 : bytes / 16;
     const size_t grid = (nvec + 255) / 256;
@@ -1015,21 +1015,6 @@ unsigned long long flag_wait_ticks()
 
 double flag_wait_seconds() { return (double)flag_wait_ticks() / 1e8; }
 
-// MSX_PUSH_VERIFY=1 (diagnosis only): the device counter block of
-// copy_post_body's store / source re-checks (CopySegs::dbg); nullptr otherwise.
-unsigned* push_verify_counts()
-{
-    static unsigned* d = [] {
-        unsigned* p = nullptr;
-        const char* e = getenv("MSX_PUSH_VERIFY");
-        if (!e || atoi(e) == 0) return p;
-        if (hipMalloc(reinterpret_cast<void**>(&p), 64) != hipSuccess) return (unsigned*)nullptr;
-        if (hipMemset(p, 0, 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return (unsigned*)nullptr;
-        return p;
-    }();
-    return d;
-}
-
 hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
                             unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
                             unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,
@@ -1042,7 +1027,6 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     PostFlags f{};
     size_t maxb = 0;
     c.n = nseg > 0 ? nseg : 1;
-    c.dbg = push_verify_counts();
     for (int i = 0; i < nseg; ++i) {
         c.src[i] = src[i];
         c.dst[i] = dst[i];

@@ -281,7 +281,7 @@ public:
     CallPin& operator=(const CallPin&) = delete;
     ~CallPin() { release(); }
 
-    bool pin(uintptr_t a, uintptr_t b)
+    bool pin(uintptr_t a, uintptr_t b, unsigned flags = hipHostRegisterMapped)
     {
         lo_ = page_down(a);
         hi_ = page_up(b);
@@ -297,7 +297,7 @@ public:
             t.n.fetch_add(1, std::memory_order_release);
         }
         listed_ = true;
-        hipError_t e = hipHostRegister(reinterpret_cast<void*>(lo_), hi_ - lo_, hipHostRegisterMapped);
+        hipError_t e = hipHostRegister(reinterpret_cast<void*>(lo_), hi_ - lo_, flags);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             trace("call pin of %zu bytes refused: %s", (size_t)(hi_ - lo_), hipGetErrorString(e));
@@ -316,6 +316,18 @@ public:
     }
     // device alias of host address p (inside the pinned range)
     void* dev(const void* p) const { return dev_ + ((uintptr_t)p - lo_); }
+    // the same for the CURRENT device of a portable pin: the registered base's
+    // alias there plus p's offset (interior pointers are never queried)
+    void* dev_here(const void* p) const
+    {
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(lo_), 0) != hipSuccess || !d) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return static_cast<char*>(d) + ((uintptr_t)p - lo_);
+    }
+    bool covers(const void* p) const { return dev_ && (uintptr_t)p >= lo_ && (uintptr_t)p < hi_; }
     bool active() const { return dev_ != nullptr; }
     void release()
     {
@@ -472,6 +484,96 @@ BufInfo classify(const void* p)
     return b;
 }
 
+// ---- page-locked staging ring for pageable transfers (xfer_sync) -------------
+namespace {
+constexpr size_t kXferChunk = (size_t)8 << 20;
+struct XferRing {
+    std::mutex mu;
+    char* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool ok = false;
+    bool init()
+    {
+        if (ok) return true;
+        for (int i = 0; i < 2; ++i) {
+            if (!buf[i] && hipHostMalloc(reinterpret_cast<void**>(&buf[i]), kXferChunk, hipHostMallocPortable) != hipSuccess) {
+                (void)hipGetLastError();
+                buf[i] = nullptr;
+                return false;
+            }
+            if (!ev[i] && hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) {
+                (void)hipGetLastError();
+                ev[i] = nullptr;
+                return false;
+            }
+        }
+        ok = true;
+        return true;
+    }
+};
+XferRing& xring()
+{
+    static XferRing r;
+    return r;
+}
+}  // namespace
+
+bool host_pageable(const void* p)
+{
+    const BufInfo b = classify(p);
+    return b.place == Place::Host && !b.dev;
+}
+
+int xfer_sync(void* dst, const void* src, size_t bytes, hipStream_t s)
+{
+    if (!bytes) return MPI_SUCCESS;
+    const bool pd = host_pageable(dst), ps = host_pageable(src);
+    hipError_t e = hipSuccess;
+    if (pd && ps) {
+        memcpy(dst, src, bytes);
+        return MPI_SUCCESS;
+    }
+    if (!pd && !ps) {
+        e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s);   // xfer: device/pinned
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy");
+    }
+    XferRing& r = xring();
+    std::lock_guard<std::mutex> g(r.mu);
+    if (!r.init()) return hip_fail(hipErrorOutOfMemory, "page-locked staging ring");
+    const size_t nch = (bytes + kXferChunk - 1) / kXferChunk;
+    auto len = [&](size_t k) { return std::min(kXferChunk, bytes - k * kXferChunk); };
+    if (ps) {
+        // host -> device: fill a ring slot on the CPU, DMA it; a slot is
+        // refilled only after its previous DMA completed
+        for (size_t k = 0; k < nch && e == hipSuccess; ++k) {
+            const int sl = (int)(k & 1);
+            if (k >= 2) e = hipEventSynchronize(r.ev[sl]);
+            if (e != hipSuccess) break;
+            memcpy(r.buf[sl], static_cast<const char*>(src) + k * kXferChunk, len(k));
+            e = hipMemcpyAsync(static_cast<char*>(dst) + k * kXferChunk, r.buf[sl], len(k), hipMemcpyHostToDevice,
+                               s);   // xfer: device/pinned
+            if (e == hipSuccess) e = hipEventRecord(r.ev[sl], s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+    } else {
+        // device -> host: DMA chunk k + 1 while the CPU drains chunk k
+        auto issue = [&](size_t k) {
+            const int sl = (int)(k & 1);
+            hipError_t x = hipMemcpyAsync(r.buf[sl], static_cast<const char*>(src) + k * kXferChunk, len(k),
+                                          hipMemcpyDeviceToHost, s);   // xfer: device/pinned
+            return x == hipSuccess ? hipEventRecord(r.ev[sl], s) : x;
+        };
+        e = issue(0);
+        for (size_t k = 0; k < nch && e == hipSuccess; ++k) {
+            if (k + 1 < nch) e = issue(k + 1);
+            if (e == hipSuccess) e = hipEventSynchronize(r.ev[k & 1]);
+            if (e == hipSuccess) memcpy(static_cast<char*>(dst) + k * kXferChunk, r.buf[k & 1], len(k));
+        }
+    }
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "page-locked staged copy");
+}
+
 int reduce_local_device(int opidx, Kind k, const void* in, void* inout, size_t count,
                         hipStream_t s)
 {
@@ -582,22 +684,29 @@ int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t coun
         char* src_io = static_cast<char*>(inout) + off * esz;
         const void* din;
         void* dio;
+        // page-locked operands (host modes 1 / 2) are copied by DMA on the
+        // slot's stream; pageable ones through the page-locked ring (xfer_sync)
+        auto h2d = [&](void* d, const void* h, const BufInfo& b) {
+            if (!b.dev) return xfer_sync(d, h, bytes, st) == MPI_SUCCESS ? hipSuccess : hipErrorUnknown;
+            return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);   // xfer: device/pinned
+        };
         if (bi.place == Place::Device) {
             din = static_cast<const char*>(bi.dev) + off * esz;
         } else {
-            e = hipMemcpyAsync(s.stage_in[slot], src_in, bytes, hipMemcpyHostToDevice, st);
+            e = h2d(s.stage_in[slot], src_in, bi);
             din = s.stage_in[slot];
         }
         if (bo.place == Place::Device) {
             dio = static_cast<char*>(bo.dev) + off * esz;
         } else {
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(s.stage_io[slot], src_io, bytes, hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = h2d(s.stage_io[slot], src_io, bo);
             dio = s.stage_io[slot];
         }
         if (e == hipSuccess) e = launch_combine(opidx, k, din, dio, n, st, host_cfg);
-        if (e == hipSuccess && bo.place == Place::Host)
-            e = hipMemcpyAsync(src_io, dio, bytes, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && bo.place == Place::Host) {
+            if (bo.dev) e = hipMemcpyAsync(src_io, dio, bytes, hipMemcpyDeviceToHost, st);   // xfer: device/pinned
+            else e = xfer_sync(src_io, dio, bytes, st) == MPI_SUCCESS ? hipSuccess : hipErrorUnknown;
+        }
         off += n;
         slot ^= 1;
         // Before re-using the other slot's staging buffers, its previous chunk
@@ -642,34 +751,37 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
             return reduce_local_any(opidx, k, in, inout, count);
         }
     }
-    // page-rounded registration of the operands not pinned already (one range
-    // when they share pages); pinned ones (hipHostMalloc) are used as they are
-    const uintptr_t pg = 4096;
-    uintptr_t a0 = (uintptr_t)in & ~(pg - 1), a1 = ((uintptr_t)in + bytes + pg - 1) & ~(pg - 1);
-    uintptr_t b0 = (uintptr_t)inout & ~(pg - 1), b1 = ((uintptr_t)inout + bytes + pg - 1) & ~(pg - 1);
-    std::vector<std::pair<uintptr_t, uintptr_t>> rg;
-    if (!bi.dev && !bo.dev && a0 < b1 && b0 < a1) rg.push_back({std::min(a0, b0), std::max(a1, b1)});
-    else {
-        if (!bi.dev) rg.push_back({a0, a1});
-        if (!bo.dev) rg.push_back({b0, b1});
+    // Call-scoped pins (CallPin: listed in temp_pins, so classify() on other
+    // threads sees these pages as pageable and never launches on them), portable
+    // to every device, of the operands not pinned already (one range when they
+    // share pages); caller-pinned ones (hipHostMalloc) are used as they are.
+    // UNVERIFIED above one GPU: the one-GPU box clamps g to 1 and returns above.
+    CallPin pins[2];
+    const unsigned pflags = hipHostRegisterPortable | hipHostRegisterMapped;
+    const uintptr_t a0 = (uintptr_t)in, a1 = a0 + bytes, b0 = (uintptr_t)inout, b1 = b0 + bytes;
+    bool ok = true;
+    if (!bi.dev && !bo.dev && page_down(a0) < page_up(b1) && page_down(b0) < page_up(a1)) {
+        ok = pins[0].pin(std::min(a0, b0), std::max(a1, b1), pflags);
+    } else {
+        if (!bi.dev) ok = pins[0].pin(a0, a1, pflags);
+        if (ok && !bo.dev) ok = pins[1].pin(b0, b1, pflags);
     }
-    size_t nreg = 0;
-    for (auto& r : rg) {
-        if (hipHostRegister(reinterpret_cast<void*>(r.first), r.second - r.first,
-                            hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
-            (void)hipGetLastError();
-            break;
-        }
-        ++nreg;
-    }
-    auto unpin = [&] {
-        for (size_t i = 0; i < nreg; ++i) (void)hipHostUnregister(reinterpret_cast<void*>(rg[i].first));
-    };
-    if (nreg != rg.size()) {
-        unpin();
-        trace("reduce_local_multi: pin refused, one GPU");
+    if (!ok) {
+        pins[0].release();
+        pins[1].release();
+        trace("reduce_local_multi: pin refused or range in use, one GPU");
         return reduce_local_any(opidx, k, in, inout, count);
     }
+    auto alias = [&](const void* p) -> void* {
+        for (const CallPin& c : pins)
+            if (c.covers(p)) return c.dev_here(p);
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return d;
+    };
     static std::mutex mu;
     static std::vector<hipStream_t> streams;
     std::lock_guard<std::mutex> lk(mu);
@@ -687,9 +799,9 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
         if (hi <= lo) continue;
         e = hipSetDevice(d);
         if (e == hipSuccess && !streams[(size_t)d]) e = hipStreamCreateWithFlags(&streams[(size_t)d], hipStreamNonBlocking);
-        void *din = nullptr, *dio = nullptr;
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&din, const_cast<void*>(in), 0);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&dio, inout, 0);
+        void* din = e == hipSuccess ? alias(in) : nullptr;
+        void* dio = e == hipSuccess ? alias(inout) : nullptr;
+        if (e == hipSuccess && (!din || !dio)) e = hipErrorInvalidValue;
         if (e == hipSuccess)
             e = launch_combine(opidx, k, static_cast<const char*>(din) + lo * esz, static_cast<char*>(dio) + lo * esz,
                                hi - lo, streams[(size_t)d], cfg);
@@ -701,8 +813,7 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
         if (e == hipSuccess) e = e2;
     }
     (void)hipSetDevice(cur);
-    unpin();
-    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "multi-GPU combine");
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "multi-GPU combine");   // pins released after the syncs
 }
 
 namespace {

@@ -117,6 +117,20 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
 int reduce_local_device(int opidx, Kind k, const void* in, void* inout, size_t count,
                         hipStream_t s);
 
+// Host <-> device copy that never hands PAGEABLE host memory to the HIP
+// runtime's copy path: a pageable side goes through the library's own
+// page-locked staging ring (CPU memcpy + DMA from hipHostMalloc'd memory);
+// device and page-locked memory are copied directly.  DESIGN.md §2: the
+// wrong results of rounds 3-4 were 256-byte holes in pageable transfers of
+// the test harness, so the product keeps its own bytes off that path.
+// Stream-ordered after earlier work on s, and synchronous: returns after the
+// bytes have arrived (the pageable copies it replaces were synchronous too).
+// Every hipMemcpy* call site of the product is either this helper or marked
+// `// xfer: device/pinned` (tests/test_abi.py audits it).
+int xfer_sync(void* dst, const void* src, size_t bytes, hipStream_t s);
+// true when p is host memory HIP would treat as pageable (not page-locked)
+bool host_pageable(const void* p);
+
 // hipError_t -> MPI error class with the HIP error text recorded.
 int hip_fail(hipError_t e, const char* what);
 

@@ -650,7 +650,16 @@ int transport_create(int rank, int size, Transport** out)
     return MPI_SUCCESS;
 }
 
-void transport_destroy(Transport* t) { delete t; }
+void transport_destroy(Transport* t)
+{
+    if (!t) return;
+    for (int i = 0; i < 2; ++i) {
+        if (t->pipe_tree[i]) (void)hipEventDestroy(t->pipe_tree[i]);
+        if (t->pipe_copy[i]) (void)hipEventDestroy(t->pipe_copy[i]);
+    }
+    if (t->aux) (void)hipStreamDestroy(t->aux);
+    delete t;
+}
 
 // ===========================================================================
 // schedules
@@ -1340,33 +1349,16 @@ size_t sub_skew(size_t per_rank)
 
 // usable bytes of one sub-slot of a window with chunk C over p ranks: C/p
 // minus the skew, so the IN area is exactly C.  (Late round 3 tried the whole
-// C/p with the skew on top -- c3's 1 GiB in 2 chunks instead of 3, 1.93 ->
-// 1.88 ms on the shared-GPU rehearsal -- and reverted it: the only wrong
-// results seen in round 3, in the 8-ranks-on-one-GPU stress, appeared after
-// that change; DESIGN.md §2 "Open issue".)
-// MSX_WINDOW_LAYOUT=1 selects that late-round-3 layout again (sub-slots of
-// the whole C/p, the skew on top, an IN area of p * (C/p + skew)), only to
-// rerun the round-3 whole-suite stress under it with the round-4 diagnostics.
-bool skew_on_top()
-{
-    static const bool on = [] {
-        const char* e = getenv("MSX_WINDOW_LAYOUT");
-        return e && atoi(e) == 1;
-    }();
-    return on;
-}
-
+// C/p with the skew on top and reverted it; round 4 re-ran that layout to
+// rule it out for the wrong results DESIGN.md §2 explains.)
 size_t sub_len(size_t C, int p)
 {
     const size_t per = C / (size_t)p;
-    return (skew_on_top() ? per : per - sub_skew(per)) & ~(size_t)255;
+    return (per - sub_skew(per)) & ~(size_t)255;
 }
 
 // IN area of a window: p sub-slots sub_skew apart, C bytes in all
-size_t in_bytes(size_t C, int p)
-{
-    return skew_on_top() ? (size_t)p * (sub_len(C, p) + sub_skew(C / (size_t)p)) : C;
-}
+size_t in_bytes(size_t C, int /*p*/) { return C; }
 
 struct Windows {
     std::vector<char*> base;
@@ -1404,16 +1396,21 @@ constexpr size_t kDoneFlags = 6144;
 // one MI355X (scripts/allreduce_probe.sh, profiles/r02/two_step_*) measured
 // 1 MiB 62.6 -> 28.5 us, 4 MiB 64.3 -> 32.5, 16 MiB 75.6 -> 45.8,
 // 64 MiB 154.8 -> 133.0, 128 MiB 265 -> 249; 4 ranks 64 MiB 310 -> 254.
-// Except where ranks share a GPU: the only wrong result ever seen on this
-// path (8 ranks on one GPU, round 3) has no established cause,
-// so there the default is the host-barrier schedule and the GPU-flag one runs
-// only when MSX_TWO_STEP_MAX asks for it (the tests do).  One rank per GPU,
-// the deployment, keeps it.  Same value on every rank (gpu_shared is agreed).
+// Defaults (round 5; same value on every rank, gpu_shared is agreed):
+//  * ranks sharing a GPU: 0, the host-barrier schedules (round 4's default
+//    there; the flag schedules run when MSX_TWO_STEP_MAX asks, as the tests
+//    do).  The wrong results recorded on this path in rounds 3-4 were the test
+//    harness's own pageable transfers, not the schedule.
+//  * one rank per GPU: 256 MiB, the rounds 1-3 cap -- a single chunk of the
+//    two-step schedule; longer messages run the host-barrier pipeline.  The
+//    cross-GPU data plane has not run on hardware yet (no multi-GPU box has
+//    been available to the tests), so the multi-chunk GPU-flag pipeline is
+//    opt-in (MSX_TWO_STEP_MAX) until the one-rank-per-GPU suites pass.
 size_t two_step_max(const Transport* tp)
 {
     static const char* e = getenv("MSX_TWO_STEP_MAX");
     if (e) return (size_t)atoll(e);
-    return tp->gpu_shared ? 0 : ~(size_t)0;
+    return tp->gpu_shared ? 0 : (size_t)256 << 20;
 }
 
 // Pinned bounce buffers of the engine (engine worker, or the one inline
@@ -1535,7 +1532,9 @@ int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
             return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy kernel");
         }
     }
-    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s);
+    // a pageable host side never goes to HIP's copy path (xfer_sync)
+    if (host_pageable(dst) || host_pageable(src)) return xfer_sync(dst, src, bytes, s);
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s);   // xfer: device/pinned
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "stage copy");
 }
 
@@ -1549,34 +1548,32 @@ struct EngineStats {
 };
 EngineStats g_stats;
 
-// Second engine stream (engine worker only): local copies that overlap xGMI work.
-hipStream_t aux_stream()
+// The communicator's second engine stream: local copies that overlap xGMI
+// work.  Created on first use; nullptr (callers then stay on their stream)
+// if HIP refuses.
+hipStream_t aux_stream(Transport* tp)
 {
-    static hipStream_t s = [] {
-        hipStream_t t = nullptr;
-        (void)hipStreamCreateWithFlags(&t, hipStreamNonBlocking);
-        return t;
-    }();
-    return s;
+    if (!tp->aux && hipStreamCreateWithFlags(&tp->aux, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        tp->aux = nullptr;
+    }
+    return tp->aux;
 }
 
 // Cross-stream hand-offs of the pipelined two-step allreduce (two chunks in
-// flight, so two of each); collectives are issued one at a time per process.
-struct PipeEvents {
-    hipEvent_t tree[2] = {nullptr, nullptr}, copy[2] = {nullptr, nullptr};
-    bool ok = false;
-};
-PipeEvents& pipe_events()
+// flight, so two of each), per communicator: one collective at a time per
+// communicator is MPI's ordering rule, not one per process.
+bool pipe_events(Transport* tp)
 {
-    static PipeEvents e = [] {
-        PipeEvents p;
-        p.ok = true;
+    if (tp->pipe_ok < 0) {
+        bool ok = true;
         for (int i = 0; i < 2; ++i)
-            p.ok = p.ok && hipEventCreateWithFlags(&p.tree[i], hipEventDisableTiming) == hipSuccess &&
-                   hipEventCreateWithFlags(&p.copy[i], hipEventDisableTiming) == hipSuccess;
-        return p;
-    }();
-    return e;
+            ok = ok && hipEventCreateWithFlags(&tp->pipe_tree[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&tp->pipe_copy[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) (void)hipGetLastError();
+        tp->pipe_ok = ok ? 1 : 0;
+    }
+    return tp->pipe_ok == 1;
 }
 
 // MSX_COLLECT_OVERLAP=1: the pipelined allreduce collects chunk i (result
@@ -2113,7 +2110,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     BufInfo bs = classify(src), bd = classify(dst);
     PinHold pins;
     pins.sync_before_release(s);
-    pins.sync_before_release(aux_stream());
+    if (hipStream_t a = aux_stream(tp)) pins.sync_before_release(a);
     alias_host_operands(pins, true, src, count * esz, &bs, want ? dst : nullptr, want ? count * esz : 0, &bd);
     // elements per sub-slot, whole 16-element granules
     size_t qmax = w.Q / esz;
@@ -2333,8 +2330,8 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // collect stream: chunk ci's result wait and copy overlap chunk ci+1's
         // push and trees; events order my own tree before my copy and my copy
         // of chunk ci before my trees of chunk ci+2 (same OUT half)
-        PipeEvents& ev = pipe_events();
-        const hipStream_t sc = (want && nchunks > 1 && ev.ok && collect_overlap()) ? aux_stream() : s;
+        const bool ovl = want && nchunks > 1 && collect_overlap() && pipe_events(tp) && aux_stream(tp);
+        const hipStream_t sc = ovl ? aux_stream(tp) : s;
         std::vector<TwoStepRange> ranges;
         for (size_t ci = 0; ci < nchunks && rc == MPI_SUCCESS; ++ci) {
             const size_t o = ci * pc_el;
@@ -2355,7 +2352,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, false, nullptr,
                                                 w.flags(me) + kDoneFlags, p, me, err_dev, s, 3);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce half-free wait");
-                if (rc == MPI_SUCCESS && sc != s && hipStreamWaitEvent(s, ev.copy[ci % 2], 0) != hipSuccess)
+                if (rc == MPI_SUCCESS && sc != s && hipStreamWaitEvent(s, tp->pipe_copy[ci % 2], 0) != hipSuccess)
                     rc = hip_fail(hipGetLastError(), "allreduce collect event wait");
             }
             if (rc != MPI_SUCCESS) break;
@@ -2398,7 +2395,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                                    w.out(dests[0]) + obase + g.e0 * esz, s, extra, &tw);
             }
             if (rc == MPI_SUCCESS && sc != s) {
-                if (hipEventRecord(ev.tree[ci % 2], s) != hipSuccess || hipStreamWaitEvent(sc, ev.tree[ci % 2], 0) != hipSuccess)
+                if (hipEventRecord(tp->pipe_tree[ci % 2], s) != hipSuccess || hipStreamWaitEvent(sc, tp->pipe_tree[ci % 2], 0) != hipSuccess)
                     rc = hip_fail(hipGetLastError(), "allreduce tree event");
             }
             if (rc == MPI_SUCCESS && want) {
@@ -2408,7 +2405,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce result wait");
                 char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : dst;
                 if (rc == MPI_SUCCESS) rc = copy_async(out + o * esz, w.out(me) + obase, len * esz, sc);
-                if (rc == MPI_SUCCESS && sc != s && hipEventRecord(ev.copy[ci % 2], sc) != hipSuccess)
+                if (rc == MPI_SUCCESS && sc != s && hipEventRecord(tp->pipe_copy[ci % 2], sc) != hipSuccess)
                     rc = hip_fail(hipGetLastError(), "allreduce collect event");
             }
             // step 4: this chunk's halves are free again (read by my trees and
@@ -2442,7 +2439,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     // pieces (work balance only, 16-element granules); each element of a piece
     // is evaluated with the tree of its block's owner.
     const size_t ce = (size_t)p * qmax;
-    hipStream_t s2 = aux_stream();
+    hipStream_t s2 = aux_stream(tp) ? aux_stream(tp) : s;
     for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += ce) {
         const double t0 = now_s();
         const size_t len = std::min(ce, count - o);

@@ -21,13 +21,6 @@ struct CopySegs {
     int n;
     int sys;
     int wt;    // copy_post_body: write-through stores (st_wt), see there
-    // diagnosis only (MSX_PUSH_VERIFY=1): copy_post_body's
-    // unrolled write-through path re-reads each vector it stored, from the
-    // destination with system-scope loads and from the source, and counts
-    // mismatches: [0] destination != value stored, [1] source != value
-    // loaded, [2] value loaded was all zero, [3] last vector index that
-    // mismatched + 1.  nullptr: no checks.
-    unsigned* dbg;
 };
 
 struct PostFlags {
@@ -199,26 +192,6 @@ __device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlag
                 const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
                 st_wt_at(r, 16 * i, a0); st_wt_at(r, 16 * (i + stride), a1);
                 st_wt_at(r, 16 * (i + 2 * stride), a2); st_wt_at(r, 16 * (i + 3 * stride), a3);
-                if (c.dbg) {
-                    stores_done();
-                    const u32x4 av[4] = {a0, a1, a2, a3};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const size_t v = i + (size_t)k * stride;
-                        const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(unsigned)(16 * v), 0, 17);
-                        const u32x4 s2 = s4[v];
-                        const u32x4 a = av[k];
-                        const bool dbad = d.x != a.x || d.y != a.y || d.z != a.z || d.w != a.w;
-                        const bool sbad = s2.x != a.x || s2.y != a.y || s2.z != a.z || s2.w != a.w;
-                        if (dbad) __hip_atomic_fetch_add(c.dbg + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        if (sbad) __hip_atomic_fetch_add(c.dbg + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        if ((a.x | a.y | a.z | a.w) == 0)
-                            __hip_atomic_fetch_add(c.dbg + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        if (dbad || sbad)
-                            __hip_atomic_fetch_max(c.dbg + 3, (unsigned)v + 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                }
             }
             for (; i < nv; i += stride) st_wt_at(r, 16 * i, s4[i]);
         } else {
@@ -493,12 +466,13 @@ template <int OP, class VT> struct VecFn {
 // 55 us generic vs 44.6 us here, scripts/tree_probe.py).
 //
 // MASKED (trees only): the same NL-leaf tree with the non-power-of-two fold's
-// leaf pairs (pairmask: leaf k = f(s[2k], s[2k+1])) and absent leaves (k >=
-// nleaves: a binomial tree over p < NL ranks) taken at run time -- NL, the
-// unrolling and the up-front loads stay compile-time, the pattern is a
+// leaf pairs (pairmask: leaf k = f(s[2k], s[2k+1])) taken at run time -- NL,
+// the unrolling and the up-front loads stay compile-time, the pattern is a
 // wave-uniform test per leaf (scalar branches, no divergence), so p = 3, 5, 6,
-// 7 and the rooted binomial trees run the fixed form instead of the generic
-// kernel's 16-leaf loop.
+// 7 run the fixed form instead of the generic kernel's 16-leaf loop.
+// run_tree_sel (msx_tree_impl.h) sends it only full-leaf trees (nleaves ==
+// P); trees with absent leaves (the rooted binomial trees) keep the generic
+// kernel, which measured faster for them.
 template <class F, int NL, int U, int BLOCK, bool NT, bool CHAIN, bool MASKED = false>
 __device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict__ out, size_t nvec, size_t bid,
                                            size_t nb)

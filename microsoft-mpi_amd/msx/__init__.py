@@ -156,13 +156,13 @@ def lib():
         "MPI_Pack_size": (i, [i, i, i, p]),
         "msx_engine_transport": (ctypes.c_char_p, []),
         "msx_engine_stats": (i, [ctypes.POINTER(ctypes.c_double), i, i]),
+        "msx_engine_gpu_shared": (i, []),
         "msx_peer_write_bandwidth": (i, [i64, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]),
         "MPI_Wait": (i, [ctypes.POINTER(i), p]),
         "MPI_Test": (i, [ctypes.POINTER(i), ctypes.POINTER(i), p]),
         "MPI_Wtime": (ctypes.c_double, []),
         "msx_version": (ctypes.c_char_p, []),
         "msx_device_count": (i, []),
-        "msx_push_verify_counts": (i, [ctypes.POINTER(ctypes.c_uint)]),
         "msx_last_error": (ctypes.c_char_p, []),
         "msx_op_check": (i, [i, i]),
         "msx_operands_on_device": (i, [p, p]),

@@ -228,13 +228,19 @@ static void* rank_main(void* v)
         for (int k = 0; k < j->p; ++k)
             if (!j->send[k] || !j->rb[k] || !j->tmp[k]) rc = MPI_ERR_NO_MEM;
     }
+    /* Every thread leaves the loop at the same rep: a failing call publishes
+     * its error in the shared word before the closing barrier, and each thread
+     * reads that word only after it (no thread writes it again before all
+     * have read it), so none is left waiting at a barrier the others skip. */
     for (int rep = 0; rep < j->reps && rc == 0; ++rep) {
         fill(j, r, j->send[r], elems);                           /* outside the timed region */
         pthread_barrier_wait(&j->bar);
         const double t0 = now_s();
-        rc |= j->which == 0 ? allreduce_rank(j, r) : reduce_scatter_rank(j, r);
+        const int rc1 = j->which == 0 ? allreduce_rank(j, r) : reduce_scatter_rank(j, r);
+        if (rc1) __atomic_fetch_or(&j->rc, rc1, __ATOMIC_RELAXED);
         pthread_barrier_wait(&j->bar);
         if (r == 0) j->t[rep] = now_s() - t0;
+        rc = __atomic_load_n(&j->rc, __ATOMIC_RELAXED);
     }
     if (rc == 0) {
         const int bad = j->which == 0 ? check(j, j->rb[r], 0, j->count)

@@ -554,3 +554,28 @@ def test_library_was_built_from_these_sources(msxlib):
     msxlib.msx_version.restype = ctypes.c_char_p
     v = msxlib.msx_version().decode()
     assert v.endswith("src=" + h.hexdigest()[:16]), (v, h.hexdigest()[:16])
+
+
+def test_no_pageable_memory_reaches_hip_copies():
+    """the wrong results of rounds 3-4 were 256-byte holes in
+    pageable host transfers (the test harness's).  The product keeps user
+    bytes off HIP's pageable-copy path: every hipMemcpy* call in csrc/ is
+    either inside xfer_sync's page-locked ring or marked as a device / page-
+    locked copy (`xfer: device/pinned`); pageable sides go through xfer_sync."""
+    import re
+    csrc = os.path.join(msx.REPO_ROOT, "microsoft-mpi_amd", "csrc")
+    unmarked = []
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".cpp", ".hip", ".h")):
+            continue
+        text = open(os.path.join(csrc, f)).read()
+        for m in re.finditer(r"\bhipMemcpy\w*\s*\(", text):
+            line_start = text.rfind("\n", 0, m.start()) + 1
+            if text[line_start:m.start()].lstrip().startswith("//"):
+                continue                                  # a comment mentioning it
+            end = text.find(";", m.end())
+            stmt_end = text.find("\n", end)
+            stmt = text[m.start():stmt_end if stmt_end >= 0 else len(text)]
+            if "xfer: device/pinned" not in stmt:
+                unmarked.append(f"{f}:{text.count(chr(10), 0, m.start()) + 1}")
+    assert not unmarked, unmarked

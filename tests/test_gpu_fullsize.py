@@ -199,13 +199,23 @@ def test_baseline_config_full_size(cfg, p, sched):
 # reduce.cpp:3973,4047 for c3, :1126 for c4, :4421-4472,4549-4577 for c5) and
 # RCCL send/recv -- checked against the same 8-leaf reference trees.  Skipped
 # below 8 GPUs (the one-GPU box); the driver's 8-GPU node runs them.
+# `sched`: the default for distinct GPUs (GPU-flag two-step up to 256 MiB,
+# host barriers above), the host-barrier schedules only (MSX_TWO_STEP_MAX=0)
+# and the opt-in GPU-flag pipeline at every size, so a failure tells the
+# schedule from the data plane.
+SCHED_ENV = {"default": None, "host_barrier": {"MSX_TWO_STEP_MAX": "0"},
+             "pipeline": {"MSX_TWO_STEP_MAX": str(1 << 62)}}
+
+
+@pytest.mark.parametrize("sched", ["default", "host_barrier", "pipeline"])
 @pytest.mark.parametrize("transport", ["ipc", "rccl"])
 @pytest.mark.parametrize("cfg", ["c3", "c4", "c5"])
-def test_baseline_config_one_rank_per_gpu(cfg, transport):
+def test_baseline_config_one_rank_per_gpu(cfg, transport, sched):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if torch.cuda.device_count() < 8:
         pytest.skip("needs 8 GPUs (one rank per GPU, the configs' layout)")
-    used = _run(cfg, 8, one_per_gpu=True, transport=transport)
+    used = _run(cfg, 8, one_per_gpu=True, transport=transport,
+                extra=SCHED_ENV[sched])
     assert all(u == [transport] for u in used), used

@@ -41,24 +41,62 @@ def dzeros(*a, **k):
     torch.cuda.synchronize()      # the library's streams do not order after torch's
     return t
 
-PINNED = os.environ.get("MSX_TEST_PINNED") == "1"   # diagnosis: transfers from / to page-locked memory
+# The harness's own transfers.  Pageable (MSX_TEST_PINNED=0) they take HIP's
+# pageable-copy path; DESIGN.md §2 shows that the wrong results of rounds 3-4
+# were bytes that path did not deliver, so each pageable transfer lands on a
+# prefilled sentinel: bytes a transfer leaves unwritten then read as the
+# sentinel instead of as whatever the buffer held before.
+PINNED = os.environ.get("MSX_TEST_PINNED", "1") != "0"
+from _stress import SENT_HOST
+SENT_DEV = 0x5A
 
 def todev(a):
     t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
     if a.nbytes:
         h = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy())
+        if not PINNED:
+            t.fill_(SENT_DEV)
         t.copy_(h.pin_memory() if PINNED else h)
     torch.cuda.synchronize()      # the library's streams do not order after torch's
     return t
 
 def fromdev(t, like, n=None):
     n = like.size if n is None else n
+    h = torch.empty(n * like.dtype.itemsize, dtype=torch.uint8)
     if PINNED:
-        h = torch.empty(n * like.dtype.itemsize, dtype=torch.uint8).pin_memory()
-        h.copy_(t[: n * like.dtype.itemsize])
-        torch.cuda.synchronize()
-        return np.frombuffer(bytearray(h.numpy().tobytes()), like.dtype)
-    return np.frombuffer(bytearray(t[: n * like.dtype.itemsize].cpu().numpy().tobytes()), like.dtype)
+        h = h.pin_memory()
+    else:
+        h.fill_(SENT_HOST)
+    h.copy_(t[: n * like.dtype.itemsize])
+    torch.cuda.synchronize()
+    return np.frombuffer(bytearray(h.numpy().tobytes()), like.dtype)
+
+def pinned_dev(a):
+    # an independent upload (page-locked source, direct DMA) to compare on the GPU
+    return torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory().to("cuda")
+
+def where_wrong(tag, got, exp, dev_res, dev_in=None, own=None):
+    # Which copy holds the wrong bytes (DESIGN.md §2): the device result
+    # compared on the GPU with an independent upload of the expected bytes;
+    # host elements still holding the readback sentinel (never written by the
+    # device-to-host copy); the rank's own send buffer on the GPU against its
+    # input (an upload that lost bytes).  Reported, never retried.
+    ne = exp.size * exp.dtype.itemsize
+    bad = np.nonzero(got != exp)[0]
+    sent = np.frombuffer(np.full(exp.dtype.itemsize, SENT_HOST, np.uint8).tobytes(), exp.dtype)[0]
+    unwritten = int(np.count_nonzero(got[bad] == sent))
+    d = dev_res[:ne].view(torch.uint8) != pinned_dev(exp)
+    dbad = torch.nonzero(d.view(-1, exp.dtype.itemsize).any(1)).flatten().cpu().numpy()
+    msg = (f"{tag}: host {bad.size} wrong ({unwritten} hold the readback sentinel); "
+           f"device result {dbad.size} wrong" + (f" [{dbad[0]}..{dbad[-1]}]" if dbad.size else ""))
+    if dev_in is not None:
+        u = dev_in[:own.nbytes].view(torch.uint8) != pinned_dev(own)
+        ubad = torch.nonzero(u.view(-1, own.dtype.itemsize).any(1)).flatten().cpu().numpy()
+        sd = int((dev_in[:own.nbytes][u] == SENT_DEV).sum().item())
+        msg += f"; own send buffer {ubad.size} wrong" + (
+            f" [{ubad[0]}..{ubad[-1]}, {sd} bytes sentinel]" if ubad.size else "")
+    again = fromdev(dev_res, exp)
+    return msg + f"; second readback {'clean' if again.tobytes() == exp.tobytes() else 'same error'}"
 
 def check(tag, got, exp):
     if got.tobytes() != exp.tobytes():
@@ -333,76 +371,15 @@ else: check("testall allreduce int", fromdev(ra, xa[rank]), ea[rank])
 # arrival-flag path, non-roots push to the root only), a chunked large
 # allreduce (full barrier first), non-blocking calls through the engine
 # worker, in-place calls.
-def ivec(it, r, n):
-    # the high term differs per (call, rank), so a wrong value names its source
-    hi = (((it * 2654435761) ^ (r * 40503)) % 4093) << 17
-    return ((np.arange(n, dtype=np.int64) * 7 + it * 31 + r * 1009) % 100003 + hi).astype(np.int32)
-
-def stress_n(it):
-    return (1 << 18) if it % 50 == 49 else (1, 5, 64, 1000, 4096, 65536, 100003, 300001)[it % 8]
-
-def stress_input(it, r):
-    # what rank r sent in iteration `it` (element k of it sits at byte 4k of the
-    # receiver's IN sub-slot r: every path pushes rank 0's piece / block / the
-    # whole vector from element 0)
-    n = stress_n(it)
-    return ivec(it, r, n * p if it % 9 == 4 and it % 7 != 3 else n)
+from _stress import ivec, stress_n, classify
 
 def stress_diag(it, n, got, tot):
-    # Which mechanism explains the wrong elements (DESIGN.md §2): zeros (a
-    # result store lost), one peer's contribution missing, one peer's
-    # contribution from an EARLIER call (a stale IN sub-slot), or an earlier
-    # call's result (a stale OUT half; with alternating halves the previous
-    # writer of a half can be 16 iterations back).  Wrapping int32
-    # arithmetic.  A hypothesis that explains only part of the wrong elements
-    # is reported with its count.
+    # which mechanism explains the wrong elements (tests/_stress.py, DESIGN.md §2)
     bad = np.nonzero(got != tot)[0]
-    e = bad
-    g, t = got[e].astype(np.int64), tot[e].astype(np.int64)
-    w = lambda v: (v.astype(np.int64) & 0xFFFFFFFF)
-    hyp = []
-    def note(name, ok):
-        k = int(np.count_nonzero(ok))
-        if k == e.size:
-            hyp.append(name)
-        elif k:
-            hyp.append(f"{name} ({k} of {e.size})")
-    note("zero", got[e] == 0)
-    for r in range(p):
-        x = ivec(it, r, n)[e].astype(np.int64)
-        note(f"missing r{r}", w(t - x) == w(g))
-        for back in range(1, 25):
-            i2 = it - back
-            if i2 < 0:
-                break
-            old = stress_input(i2, r)
-            if e.max() < old.size:
-                note(f"stale r{r} from it{i2}", w(t - x + old[e]) == w(g))
-    for back in range(1, 25):
-        i2 = it - back
-        n2 = stress_n(i2) if i2 >= 0 else 0
-        if i2 >= 0 and e.max() < n2:
-            t2 = sum(ivec(i2, r, n2)[e].astype(np.int64) for r in range(p))
-            note(f"result of it{i2}", w(t2) == w(g))
-    sample = ", ".join(f"{int(k)}:{int(a)}/{int(b)}" for k, a, b in zip(e[:3], got[e[:3]], tot[e[:3]]))
+    hyp = classify(it, n, bad, got[bad], tot[bad], p, rank)
+    sample = ", ".join(f"{int(k)}:{int(a)}/{int(b)}" for k, a, b in zip(bad[:3], got[bad[:3]], tot[bad[:3]]))
     return (f"[{bad.size} differ, first {bad[0]} last {bad[-1]}; got/exp {sample}; "
             f"explained by: {', '.join(hyp[:8]) or 'none of the tested'}]")
-
-CHECKS = os.environ.get("MSX_STRESS_CHECKS", "1") != "0"
-
-def upload_check(tag, t, a):
-    # the device copy of a send buffer really holds what was uploaded (a
-    # host-to-device copy that lost bytes would look like a wrong reduction)
-    back = fromdev(t, a)
-    if back.tobytes() != a.tobytes():
-        bad = np.nonzero(back != a)[0]
-        fails.append(f"{tag} upload mismatch [{bad.size} differ, first {bad[0]} last {bad[-1]}]")
-
-def reread(tag, t, exp):
-    # a mismatch read a second time: clean now = the first device-to-host
-    # readback was wrong, not the device buffer
-    again = fromdev(t, exp)
-    return f"{tag}: second readback {'clean' if again.tobytes() == exp.tobytes() else 'same error'}"
 
 passes = int(os.environ.get("MSX_STRESS_PASSES", "1"))
 for it in range(240 * passes):
@@ -413,8 +390,6 @@ for it in range(240 * passes):
         print("PASS", it // 240, len(fails), flush=True)
     tot = sum(ivec(it, r, n).astype(np.int64) for r in range(p)).astype(np.int32)
     sb = todev(ivec(it, rank, n))
-    if n >= 100003 and CHECKS:
-        upload_check(f"stress {it}", sb, ivec(it, rank, n))
     if it % 7 == 3:                        # rooted reduce: arrival flags, push to the root only
         root = it % p
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
@@ -428,8 +403,6 @@ for it in range(240 * passes):
         full = [ivec(it, r, n * p) for r in range(p)]
         mine_tot = sum(f[rank * n:(rank + 1) * n].astype(np.int64) for f in full).astype(np.int32)
         sb = todev(full[rank])
-        if n >= 100003 and CHECKS:
-            upload_check(f"stress rsb {it}", sb, full[rank])
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
         rc = L.MPI_Reduce_scatter_block(sb.data_ptr(), rb.data_ptr(), n, C.MPI_INT, C.MPI_SUM, C.MPI_COMM_WORLD)
         if rc:
@@ -438,7 +411,7 @@ for it in range(240 * passes):
         got_rs = fromdev(rb, mine_tot)
         check(f"stress rsb {it} n={n}", got_rs, mine_tot)
         if got_rs.tobytes() != mine_tot.tobytes():
-            fails.append(reread(f"stress rsb {it}", rb, mine_tot))
+            fails.append(where_wrong(f"stress rsb {it}", got_rs, mine_tot, rb, sb, full[rank]))
         continue
     if it % 11 == 5:                       # non-blocking, through the worker
         rb = dzeros(n * 4, dtype=torch.uint8, device="cuda")
@@ -459,17 +432,15 @@ for it in range(240 * passes):
     got = fromdev(rb, tot)
     if got.tobytes() != tot.tobytes():
         fails.append(f"stress allreduce {it} n={n} {stress_diag(it, n, got, tot)}")
-        fails.append(reread(f"stress allreduce {it}", rb, tot))
+        inplace = rb is sb
+        fails.append(where_wrong(f"stress allreduce {it}", got, tot, rb, None if inplace else sb,
+                                 None if inplace else ivec(it, rank, n)))
 
 L.msx_engine_transport.restype = ctypes.c_char_p
 print("TRANSPORT", L.msx_engine_transport().decode(), flush=True)
 st = (ctypes.c_double * 8)()
 L.msx_engine_stats(st, 8, 0)
 print("FLAGCALLS", int(st[7]), flush=True)       # GPU-flag Rabenseifner calls of this rank
-if os.environ.get("MSX_PUSH_VERIFY"):              # diagnosis runs only
-    pv = (ctypes.c_uint * 4)()
-    if L.msx_push_verify_counts(pv) == 0 and (pv[0] or pv[1]):   # [2] counts legitimately zero data too
-        fails.append(f"push re-check: dst {pv[0]} src {pv[1]} zero {pv[2]} last {pv[3]}")
 print("RESULT", rank, p, len(fails), fails[:16], flush=True)
 L.MPI_Finalize()
 '''
@@ -596,8 +567,9 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
 # paths that the shared-GPU cases above cannot: IPC windows opened on another
 # device (xGMI remote writes, system-scope write-through, peer flag polls) and
 # the RCCL send/recv plane, each checked bit for bit against the oracle.
+@pytest.mark.parametrize("sched", ["default", "host_barrier", "pipeline"])
 @pytest.mark.parametrize("transport", ["ipc", "rccl"])
-def test_collectives_one_rank_per_gpu(transport):
+def test_collectives_one_rank_per_gpu(transport, sched):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -613,6 +585,10 @@ def test_collectives_one_rank_per_gpu(transport):
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
                     "MSX_BOOTSTRAP_TIMEOUT": "180", "MSX_TRANSPORT": transport,
                     "MSX_FLAG_TIMEOUT_MS": "60000"})
+        if sched == "host_barrier":
+            env["MSX_TWO_STEP_MAX"] = "0"       # the host-barrier Rabenseifner schedules only
+        elif sched == "pipeline":
+            env["MSX_TWO_STEP_MAX"] = str(1 << 62)   # the opt-in GPU-flag pipeline at every size
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
