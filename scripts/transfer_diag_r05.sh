@@ -6,6 +6,8 @@
 # Each pageable transfer lands on a sentinel and every stress mismatch is
 # located (device result, readback, the rank's own upload) by the worker's
 # where_wrong().  Evidence collection, read once; not a rate estimate.
+# (Run on the tree of commit ddc45df's parent; MSX_WINDOW_LAYOUT was removed
+# from the library after this run and is ignored since.)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 export TMPDIR=/tmp
