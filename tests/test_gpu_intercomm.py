@@ -51,16 +51,8 @@ def ok(rc, tag):
 def raw(a):
     return np.frombuffer(bytearray(a.tobytes()), dtype=a.dtype)
 
-def todev(a):
-    t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
-    if a.nbytes:
-        t.copy_(torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()))
-    torch.cuda.synchronize()      # the library's streams do not order after torch's
-    return t
+from _xfer import todev, fromdev   # page-locked transfers (tests/_xfer.py, DESIGN.md §2)
 
-def fromdev(t, like, n=None):
-    n = like.size if n is None else n
-    return np.frombuffer(bytearray(t[: n * like.dtype.itemsize].cpu().numpy().tobytes()), like.dtype)
 
 def check(tag, got, exp):
     print("step", tag, file=sys.stderr, flush=True)

@@ -41,39 +41,8 @@ def dzeros(*a, **k):
     torch.cuda.synchronize()      # the library's streams do not order after torch's
     return t
 
-# The harness's own transfers.  Pageable (MSX_TEST_PINNED=0) they take HIP's
-# pageable-copy path; DESIGN.md §2 shows that the wrong results of rounds 3-4
-# were bytes that path did not deliver, so each pageable transfer lands on a
-# prefilled sentinel: bytes a transfer leaves unwritten then read as the
-# sentinel instead of as whatever the buffer held before.
-PINNED = os.environ.get("MSX_TEST_PINNED", "1") != "0"
-from _stress import SENT_HOST
-SENT_DEV = 0x5A
-
-def todev(a):
-    t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
-    if a.nbytes:
-        h = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy())
-        if not PINNED:
-            t.fill_(SENT_DEV)
-        t.copy_(h.pin_memory() if PINNED else h)
-    torch.cuda.synchronize()      # the library's streams do not order after torch's
-    return t
-
-def fromdev(t, like, n=None):
-    n = like.size if n is None else n
-    h = torch.empty(n * like.dtype.itemsize, dtype=torch.uint8)
-    if PINNED:
-        h = h.pin_memory()
-    else:
-        h.fill_(SENT_HOST)
-    h.copy_(t[: n * like.dtype.itemsize])
-    torch.cuda.synchronize()
-    return np.frombuffer(bytearray(h.numpy().tobytes()), like.dtype)
-
-def pinned_dev(a):
-    # an independent upload (page-locked source, direct DMA) to compare on the GPU
-    return torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory().to("cuda")
+# the harness's own transfers: page-locked by default (tests/_xfer.py, DESIGN.md §2)
+from _xfer import todev, fromdev, pinned_dev, SENT_DEV, SENT_HOST
 
 def where_wrong(tag, got, exp, dev_res, dev_in=None, own=None):
     # Which copy holds the wrong bytes (DESIGN.md §2): the device result

@@ -43,20 +43,13 @@ IN_PLACE = ctypes.c_void_p(-1 & 0xffffffffffffffff)
 def raw(a):
     return np.frombuffer(bytearray(a.tobytes()), dtype=a.dtype)
 
-def todev(a):
-    t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, device="cuda")
-    t.copy_(torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()))
-    torch.cuda.synchronize()
-    return t
+from _xfer import todev, fromdev   # page-locked transfers (tests/_xfer.py, DESIGN.md §2)
 
 def dzeros(n):
     t = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     return t
 
-def fromdev(t, like, n=None):
-    n = like.size if n is None else n
-    return np.frombuffer(bytearray(t[: n * like.dtype.itemsize].cpu().numpy().tobytes()), like.dtype)
 
 def inputs(opn, dtn, count, seed):
     rng = np.random.default_rng(seed)
