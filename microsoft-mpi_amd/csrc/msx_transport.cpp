@@ -1757,8 +1757,17 @@ ncclComm_t rccl_comm(Transport* tp)
     ncclComm_t comm = nullptr;
     ncclResult_t r = api->init_rank(&comm, tp->size, ids[0], tp->rank);
     trace("rccl: ncclCommInitRank rc=%d", (int)r);
-    if (r != ncclSuccess) {
-        set_error("ncclCommInitRank: %s", api->err(r));
+    // Every rank must take the same plane: a rank whose init failed while its
+    // peers' succeeded would run the IPC schedules against their RCCL calls and
+    // hang both.  Agree on the outcome; any failure sends all to IPC windows.
+    int32_t ok = r == ncclSuccess ? 1 : 0;
+    std::vector<int32_t> oks((size_t)tp->size);
+    if (tp->allgather(&ok, sizeof(ok), oks.data()) != MPI_SUCCESS) ok = 0;
+    for (int32_t o : oks) ok = ok && o;
+    if (!ok) {
+        if (r == ncclSuccess) (void)api->destroy(comm);
+        else set_error("ncclCommInitRank: %s", api->err(r));
+        trace("rccl: a rank's ncclCommInitRank failed; IPC windows in use");
         refused[tp] = true;
         return nullptr;
     }
