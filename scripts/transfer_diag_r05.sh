@@ -6,7 +6,7 @@
 # Each pageable transfer lands on a sentinel and every stress mismatch is
 # located (device result, readback, the rank's own upload) by the worker's
 # where_wrong().  Evidence collection, read once; not a rate estimate.
-# (Run on the tree of commit ddc45df's parent; MSX_WINDOW_LAYOUT was removed
+# (Ran with the round-4 library build and the round-5 worker; MSX_WINDOW_LAYOUT was removed
 # from the library after this run and is ignored since.)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
