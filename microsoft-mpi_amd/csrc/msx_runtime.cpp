@@ -571,7 +571,11 @@ int xfer_sync(void* dst, const void* src, size_t bytes, hipStream_t s)
             if (e == hipSuccess) memcpy(static_cast<char*>(dst) + k * kXferChunk, r.buf[k & 1], len(k));
         }
     }
-    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "page-locked staged copy");
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(s);   // no DMA may still read or fill a ring slot the next call reuses
+        return hip_fail(e, "page-locked staged copy");
+    }
+    return MPI_SUCCESS;
 }
 
 int reduce_local_device(int opidx, Kind k, const void* in, void* inout, size_t count,
