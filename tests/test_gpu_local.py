@@ -225,6 +225,29 @@ def test_mpi_reduce_local_host_buffers_staged(L, pinned, mode):
     assert L.msx_set_host_mode(0) == 0
 
 
+def test_pageable_operands_through_the_page_locked_ring(L):
+    """Host mode 1 stages pageable operands through HBM; since round 5 their
+    copies go through the library's page-locked ring (xfer_sync, 8 MiB slots,
+    DESIGN.md §2), never HIP's pageable-copy path.  Operands of several ring
+    slots with a ragged tail, at odd byte offsets, one staging chunk."""
+    assert L.msx_set_staging_chunk(64 << 20) == 0
+    assert L.msx_set_host_mode(1) == 0
+    try:
+        rng = np.random.default_rng(12)
+        for dt, op, off in (("MPI_FLOAT", "MPI_SUM", 0), ("MPI_INT8_T", "MPI_BXOR", 3), ("MPI_DOUBLE", "MPI_MAX", 8)):
+            kind = KIND[dt]
+            n = (20 << 20) // itemsize(kind) + 7
+            a, b = gen(kind, op, n + off, rng)[off:], gen(kind, op, n + off, rng)[off:]
+            exp = b.copy()
+            oracle.reduce_local(h(op), h(dt), a, exp)
+            bb = b.copy() if off == 0 else b
+            rc = L.MPI_Reduce_local(a.ctypes.data, bb.ctypes.data, n, h(dt), h(op))
+            assert rc == 0, msx.last_error()
+            assert bb.tobytes() == exp.tobytes(), (dt, op, off)
+    finally:
+        assert L.msx_set_host_mode(0) == 0
+
+
 def test_mpi_reduce_local_call_pin_edges(L):
     # host mode 0 pins pageable operands for the call: operands that share
     # pages (one pin of the union), unaligned starts and ragged ends, one
