@@ -50,6 +50,9 @@ def test_record_b_is_rank2_missing_everywhere():
             hyp = classify(it, REC["n"], e, got, tot, REC["p"], rank)
             assert "missing r2" in hyp, (it, rank, hyp)
             assert not any(h.startswith("own input") for h in hyp), hyp
+            # not a window read that raced rank 2's push: that would have summed
+            # rank 2's data of the previous call on the same window half (it - 8)
+            assert not any(h.startswith("stale r2") for h in hyp), hyp
 
 
 def test_record_c_is_own_input_at_allocator_shift():
