@@ -739,6 +739,12 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
     if (rc != MPI_SUCCESS) return rc;
     const int nvis = device_count_noinit();
     int g = ngpus <= 0 || ngpus > nvis ? nvis : ngpus;
+    // MSX_MULTI_SPLIT_TEST=1 (tests only): keep ngpus ranges (up to 16) even
+    // with fewer GPUs, range d on device d % nvis, so a one-GPU box runs the
+    // pinning, aliasing and range logic of the k-GPU split
+    if (nvis >= 1 && ngpus > nvis && getenv("MSX_MULTI_SPLIT_TEST") && atoi(getenv("MSX_MULTI_SPLIT_TEST")) == 1)
+        g = std::min(ngpus, 16);
+    auto dev_of = [nvis](int d) { return d % nvis; };
     BufInfo bi = classify(in), bo = classify(inout);
     const size_t esz = (size_t)kind_size(k), bytes = count * esz;
     if (g <= 1 || bi.place == Place::Device || bo.place == Place::Device || bytes < ((size_t)1 << 20))
@@ -789,7 +795,7 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
     static std::mutex mu;
     static std::vector<hipStream_t> streams;
     std::lock_guard<std::mutex> lk(mu);
-    if ((int)streams.size() < nvis) streams.resize((size_t)nvis, nullptr);
+    if ((int)streams.size() < g) streams.resize((size_t)g, nullptr);
     int cur = 0;
     (void)hipGetDevice(&cur);
     LaunchCfg cfg = g_cfg;
@@ -801,7 +807,7 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
         lo -= lo % align_el;
         if (d + 1 < g) hi -= hi % align_el;
         if (hi <= lo) continue;
-        e = hipSetDevice(d);
+        e = hipSetDevice(dev_of(d));
         if (e == hipSuccess && !streams[(size_t)d]) e = hipStreamCreateWithFlags(&streams[(size_t)d], hipStreamNonBlocking);
         void* din = e == hipSuccess ? alias(in) : nullptr;
         void* dio = e == hipSuccess ? alias(inout) : nullptr;
@@ -812,7 +818,7 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
     }
     for (int d = 0; d < g; ++d) {
         if (!streams[(size_t)d]) continue;
-        (void)hipSetDevice(d);
+        (void)hipSetDevice(dev_of(d));
         hipError_t e2 = hipStreamSynchronize(streams[(size_t)d]);
         if (e == hipSuccess) e = e2;
     }

@@ -40,15 +40,17 @@ def _dev(a, offset=0):
     """Copy numpy array bytes into a fresh device buffer at byte `offset`."""
     raw = np.frombuffer(a.tobytes(), np.uint8)
     t = torch.zeros(raw.size + offset + 64, dtype=torch.uint8, device="cuda")
-    if raw.size:
-        t[offset:offset + raw.size] = torch.from_numpy(raw.copy()).cuda()
+    if raw.size:   # page-locked source (tests/_xfer.py, DESIGN.md §2)
+        t[offset:offset + raw.size] = torch.from_numpy(raw.copy()).pin_memory().cuda()
     torch.cuda.synchronize()      # the library's streams do not order after torch's
     return t, t.data_ptr() + offset
 
 
 def _host(t, offset, like):
-    raw = t[offset:offset + like.nbytes].cpu().numpy()
-    return _raw(raw, like.dtype)
+    h = torch.empty(like.nbytes, dtype=torch.uint8).pin_memory()
+    h.copy_(t[offset:offset + like.nbytes])
+    torch.cuda.synchronize()
+    return _raw(h.numpy(), like.dtype)
 
 
 def _raw(a, dtype=None):
@@ -541,6 +543,41 @@ def test_reduce_local_multi_gpu_host_operands(L, ngpus):
     x = np.ones(8, np.float32)
     assert L.msx_reduce_local_multi(x.ctypes.data, x.ctypes.data, 8, C.MPI_FLOAT, C.MPI_SUM, ngpus) == C.MPI_ERR_BUFFER
     assert L.msx_reduce_local_multi(x.ctypes.data, x.ctypes.data + 4, 1, C.MPI_BYTE, C.MPI_SUM, ngpus) == C.MPI_ERR_OP
+
+
+@pytest.mark.parametrize("ngpus", [2, 3, 8])
+def test_reduce_local_multi_split_on_one_device(L, ngpus):
+    """The k-range split of msx_reduce_local_multi run on this box's one GPU
+    (MSX_MULTI_SPLIT_TEST=1: range d on device d % visible): the call-scoped
+    portable pins (listed like every call pin), the per-device aliases from the
+    registered base plus the offset, 256-B range ends and the ragged tail --
+    the code the 8-GPU node runs, minus the other devices.  Operands in
+    separate buffers, and in one buffer (one pin covering both)."""
+    os.environ["MSX_MULTI_SPLIT_TEST"] = "1"
+    try:
+        rng = np.random.default_rng(91 + ngpus)
+        for n, op, dt in (((3 << 20) // 4 + 5, "MPI_SUM", "MPI_FLOAT"), ((5 << 20) // 8 + 3, "MPI_MAX", "MPI_DOUBLE"),
+                          ((2 << 20) + 7, "MPI_BXOR", "MPI_BYTE")):
+            a, b = _raw(gen(KIND[dt], op, n, rng)), _raw(gen(KIND[dt], op, n, rng))
+            exp = _raw(b)
+            assert oracle.reduce_local(h(op), h(dt), a, exp) == 0
+            ha, hb = _raw(a), _raw(b)
+            assert L.msx_reduce_local_multi(ha.ctypes.data, hb.ctypes.data, n, h(dt), h(op), ngpus) == 0, \
+                msx.last_error()
+            assert hb.tobytes() == exp.tobytes(), (op, dt, n, ngpus, "separate")
+            both = np.concatenate([a, b])             # in and inout on shared pages: one pin
+            assert L.msx_reduce_local_multi(both.ctypes.data, both.ctypes.data + a.nbytes, n, h(dt), h(op),
+                                            ngpus) == 0, msx.last_error()
+            assert both[n:].tobytes() == exp.tobytes(), (op, dt, n, ngpus, "shared pages")
+            assert both[:n].tobytes() == a.tobytes()
+    finally:
+        del os.environ["MSX_MULTI_SPLIT_TEST"]
+    # no pin outlives the call: the same pageable ranges pin again, alone
+    x, y = _raw(gen(KIND["MPI_FLOAT"], "MPI_SUM", 1 << 20, rng)), _raw(gen(KIND["MPI_FLOAT"], "MPI_SUM", 1 << 20, rng))
+    ye = _raw(y)
+    assert oracle.reduce_local(C.MPI_SUM, C.MPI_FLOAT, x, ye) == 0
+    assert L.MPI_Reduce_local(x.ctypes.data, y.ctypes.data, 1 << 20, C.MPI_FLOAT, C.MPI_SUM) == 0
+    assert y.tobytes() == ye.tobytes()
 
 
 def test_copy_geometries_exact(L):
