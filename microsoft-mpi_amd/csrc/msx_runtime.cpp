@@ -551,8 +551,8 @@ int xfer_sync(void* dst, const void* src, size_t bytes, hipStream_t s)
             if (k >= 2) e = hipEventSynchronize(r.ev[sl]);
             if (e != hipSuccess) break;
             memcpy(r.buf[sl], static_cast<const char*>(src) + k * kXferChunk, len(k));
-            e = hipMemcpyAsync(static_cast<char*>(dst) + k * kXferChunk, r.buf[sl], len(k), hipMemcpyHostToDevice,
-                               s);   // xfer: device/pinned
+            e = hipMemcpyAsync(static_cast<char*>(dst) + k * kXferChunk, r.buf[sl], len(k), hipMemcpyDefault,
+                               s);   // xfer: device/pinned (dst may be device or page-locked host memory)
             if (e == hipSuccess) e = hipEventRecord(r.ev[sl], s);
         }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -561,7 +561,7 @@ int xfer_sync(void* dst, const void* src, size_t bytes, hipStream_t s)
         auto issue = [&](size_t k) {
             const int sl = (int)(k & 1);
             hipError_t x = hipMemcpyAsync(r.buf[sl], static_cast<const char*>(src) + k * kXferChunk, len(k),
-                                          hipMemcpyDeviceToHost, s);   // xfer: device/pinned
+                                          hipMemcpyDefault, s);   // xfer: device/pinned (src device or page-locked)
             return x == hipSuccess ? hipEventRecord(r.ev[sl], s) : x;
         };
         e = issue(0);
