@@ -246,6 +246,11 @@ def test_pageable_operands_through_the_page_locked_ring(L):
             rc = L.MPI_Reduce_local(a.ctypes.data, bb.ctypes.data, n, h(dt), h(op))
             assert rc == 0, msx.last_error()
             assert bb.tobytes() == exp.tobytes(), (dt, op, off)
+            # pageable `in`, page-locked `inout`: one operand through the ring, one by DMA
+            tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
+            rc = L.MPI_Reduce_local(a.ctypes.data, tb.data_ptr(), n, h(dt), h(op))
+            assert rc == 0, msx.last_error()
+            assert tb.numpy().tobytes() == exp.tobytes(), (dt, op, off, "mixed")
     finally:
         assert L.msx_set_host_mode(0) == 0
 
