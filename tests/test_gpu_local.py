@@ -214,7 +214,7 @@ def test_mpi_reduce_local_host_buffers_staged(L, pinned, mode):
         oracle.reduce_local(h(op), h(dt), a, exp)
         if pinned:
             ta = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory()
-            tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
+            tb = torch.from_numpy(np.frombuffer(b0, np.uint8).copy()).pin_memory()
             rc = L.MPI_Reduce_local(ta.data_ptr(), tb.data_ptr(), n, h(dt), h(op))
             got = np.frombuffer(tb.numpy().tobytes(), a.dtype)
         else:
@@ -240,14 +240,14 @@ def test_pageable_operands_through_the_page_locked_ring(L):
             kind = KIND[dt]
             n = (20 << 20) // itemsize(kind) + 7
             a, b = gen(kind, op, n + off, rng)[off:], gen(kind, op, n + off, rng)[off:]
-            exp = b.copy()
+            exp, b0 = b.copy(), b.tobytes()
             oracle.reduce_local(h(op), h(dt), a, exp)
             bb = b.copy() if off == 0 else b
             rc = L.MPI_Reduce_local(a.ctypes.data, bb.ctypes.data, n, h(dt), h(op))
             assert rc == 0, msx.last_error()
             assert bb.tobytes() == exp.tobytes(), (dt, op, off)
             # pageable `in`, page-locked `inout`: one operand through the ring, one by DMA
-            tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
+            tb = torch.from_numpy(np.frombuffer(b0, np.uint8).copy()).pin_memory()
             rc = L.MPI_Reduce_local(a.ctypes.data, tb.data_ptr(), n, h(dt), h(op))
             assert rc == 0, msx.last_error()
             assert tb.numpy().tobytes() == exp.tobytes(), (dt, op, off, "mixed")
@@ -535,7 +535,7 @@ def test_reduce_local_multi_gpu_host_operands(L, ngpus):
         for pinned in (False, True):
             if pinned:
                 ta = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory()
-                tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
+                tb = torch.from_numpy(np.frombuffer(b0, np.uint8).copy()).pin_memory()
                 pa, pb = ta.data_ptr(), tb.data_ptr()
             else:
                 ha, hb = _raw(a), _raw(b)
