@@ -214,7 +214,7 @@ def test_mpi_reduce_local_host_buffers_staged(L, pinned, mode):
         oracle.reduce_local(h(op), h(dt), a, exp)
         if pinned:
             ta = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory()
-            tb = torch.from_numpy(np.frombuffer(b0, np.uint8).copy()).pin_memory()
+            tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
             rc = L.MPI_Reduce_local(ta.data_ptr(), tb.data_ptr(), n, h(dt), h(op))
             got = np.frombuffer(tb.numpy().tobytes(), a.dtype)
         else:
@@ -535,7 +535,7 @@ def test_reduce_local_multi_gpu_host_operands(L, ngpus):
         for pinned in (False, True):
             if pinned:
                 ta = torch.from_numpy(np.frombuffer(a.tobytes(), np.uint8).copy()).pin_memory()
-                tb = torch.from_numpy(np.frombuffer(b0, np.uint8).copy()).pin_memory()
+                tb = torch.from_numpy(np.frombuffer(b.tobytes(), np.uint8).copy()).pin_memory()
                 pa, pb = ta.data_ptr(), tb.data_ptr()
             else:
                 ha, hb = _raw(a), _raw(b)
