@@ -538,6 +538,12 @@ int xfer_sync(void* dst, const void* src, size_t bytes, hipStream_t s)
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy");
     }
+    // Earlier work on s (which may wait on other ranks' GPU flags) drains
+    // BEFORE the process-wide ring lock is taken, so a thread holding the lock
+    // only ever waits for its own DMA: two threads running collectives on
+    // different communicators cannot deadlock through the ring.
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "copy: stream before the staging ring");
     XferRing& r = xring();
     std::lock_guard<std::mutex> g(r.mu);
     if (!r.init()) return hip_fail(hipErrorOutOfMemory, "page-locked staging ring");
