@@ -1,6 +1,8 @@
 """msx_dtype_oracle — CPU restatement of MS-MPI's derived-datatype semantics.
 
-ORACLE — TEST INFRASTRUCTURE ONLY.  Imported by tests/ as the checker of the
+ORACLE — TEST INFRASTRUCTURE ONLY; PARITY UNPINNED (no reference test or
+output covers datatypes; pinned by the MPI-2.2 worked examples).
+Imported by tests/ as the checker of the
 datatype engine (microsoft-mpi_amd/csrc/msx_dtype.cpp + msx_pack.hip); the
 product never imports it and there is no CPU packing path in the product.
 

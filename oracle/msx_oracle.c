@@ -16,6 +16,12 @@
  *   *_check_dtype tables      op.cpp:739-1883 (USE_STRICT_MPI undefined)
  * The reference loops run backwards (while(--len >= 0)); every element is
  * independent so the direction does not change any result.
+ *
+ * PARITY UNPINNED (in this task's terms): the reference holds no tests or
+ * fixtures for this path and cannot be built here without stand-ins for the
+ * Windows headers; the known answers it is checked against
+ * (tests/golden/survey_kat.json) came from a shim build.  Independent anchors:
+ * x86 SSE silicon for the float / NaN rules (tests/test_x86_nan_rule.py).
  */
 #include "msx_oracle.h"
 

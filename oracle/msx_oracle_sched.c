@@ -13,6 +13,9 @@
  * (the HA / node-aware variants, reduce.cpp:4180-4292, are not simulated: the
  * flat algorithm is the reference order, as with MSMPI_HA_COLLECTIVE=OFF, and
  * the one the reference takes for every message >= 256 KiB.)
+ * PARITY UNPINNED: no recorded reference output covers these schedules; the
+ * restatement is checked against the association orders derived from the
+ * source text (tests/test_oracle.py), DESIGN.md §2.
  */
 #include <stdint.h>
 #include <stdlib.h>
