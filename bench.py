@@ -20,6 +20,13 @@ fraction of the HBM roofline.
   doubled per the gfx950 calibration + WRITE_SIZE) when present.
 * cpu_baseline: the oracle (C restatement of op.cpp's Op<float>::Sum) timed
   on this host, one thread = one MS-MPI rank, on a bounded sample.
+* N > 1 also runs the collective configs c3-c5 (bench_collectives.py) in
+  child processes, headline configs first, every child under a time limit cut
+  to what is left of one wall budget (MSX_BENCH_WALL_S, default 420 s from
+  process start), so one hung data plane can never cost the JSON line.
+* The HBM probes, the combine variants of --sweep and the cold-cache launches
+  run the bench-only measurement kernels of libmsx_probe.so (msx.probe); the
+  timed steps run the product library's msx_reduce_local_dev.
 """
 import argparse
 import ctypes
@@ -29,6 +36,7 @@ import os
 import sys
 import time
 
+T_START = time.time()          # the wall budget of the N > 1 children counts from here
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "microsoft-mpi_amd"))
 
@@ -43,8 +51,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--variant", type=int, default=-1, help="fp32 SUM kernel variant (-1: default)")
-    ap.add_argument("--sweep", action="store_true", help="time every kernel variant (rank 0 stderr)")
+    ap.add_argument("--sweep", action="store_true",
+                    help="time the probe library's combine variants next to the product kernel (rank 0 stderr)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--elems", type=int, default=N_ELEM)
@@ -58,29 +66,50 @@ def parse():
     return ap.parse_args()
 
 
-# c3 / c4 engine settings timed at N = 8 (one GPU per rank) for the next
-# round's tuning, each in its own child job: the round-3 host-barrier chunks
-# (512 MiB window), host-barrier chunks in the default 960 MiB window, the
-# pipeline in the round-4 512 MiB window, the pipeline with the collect
-# overlapped, the default pipeline (2 ranks sharing one GPU:
-# profiles/r04/c3ab/, profiles/r04/bench_n2_variants.json)
-C3_VARIANTS = (("host_barrier_chunks_r03", {"MSX_TWO_STEP_MAX": str(256 << 20), "MSX_CHUNK_BYTES": str(512 << 20)}),
-               ("host_barrier_window_960MiB", {"MSX_TWO_STEP_MAX": str(256 << 20)}),
-               ("pipeline_window_512MiB", {"MSX_TWO_STEP_MAX": str(1 << 62), "MSX_CHUNK_BYTES": str(512 << 20)}),
-               ("pipeline_collect_overlap", {"MSX_TWO_STEP_MAX": str(1 << 62), "MSX_COLLECT_OVERLAP": "1"}),
-               ("pipeline", {"MSX_TWO_STEP_MAX": str(1 << 62)}))
+# The N > 1 children share one wall budget (from process start, rank 0's
+# clock): each runs under min(its own ceiling, what is left minus a reserve
+# for the cold-cache launch, the JSON line and teardown), and is skipped when
+# less than MIN_CHILD_S would be left.  Worst case with every child hanging:
+# the budget itself.  Order: the IPC plane's c3-c5 (the default data plane),
+# the RCCL planes' c3-c5, RCCL's own allreduce, the engine variant, then the
+# IPC plane's remaining configs and the host-memory multi-GPU split.
+WALL_BUDGET_S = float(os.environ.get("MSX_BENCH_WALL_S", "420"))
+RESERVE_S = 25.0
+MIN_CHILD_S = 20.0
+CHILD_CAP_S = {"ipc_core": 150.0, "rccl_core": 120.0, "rccl_native_core": 120.0, "rccl_allreduce": 90.0,
+               "variant_pipeline": 120.0, "ipc_extras": 150.0, "multi_host": 60.0}
+
+CHILD_ORDER = ("ipc_core", "rccl_core", "rccl_native_core", "rccl_allreduce", "variant_pipeline", "ipc_extras",
+               "multi_host")
 
 
-def run_collectives_child(world, rank, local, scale, transport="ipc", extra_env=None, tag="", port_off=0):
+def child_timeout(name, elapsed_s):
+    """Seconds child `name` may run when `elapsed_s` of the wall budget are
+    gone, or None when it is skipped (less than MIN_CHILD_S left)."""
+    t = min(CHILD_CAP_S[name], WALL_BUDGET_S - elapsed_s - RESERVE_S)
+    return t if t >= MIN_CHILD_S else None
+
+
+# c3 / c4 under the other schedule at N = 8 (one GPU per rank): the GPU-flag
+# pipeline at every size, where the default takes the host-barrier schedule
+# above 256 MiB (DESIGN.md §4's decision rule reads the two against each other)
+C3_VARIANTS = (("pipeline", {"MSX_TWO_STEP_MAX": str(1 << 62)}),)
+
+
+def run_collectives_child(world, rank, local, scale, transport="ipc", extra_env=None, tag="", port_off=0,
+                          parts="all", timeout=150.0):
     """c3-c5 in a child MPI process per rank (isolated from the headline line).
     transport "ipc": IPC windows + xGMI remote writes; "rccl": RCCL send/recv;
-    "rccl_native": RCCL's own collectives where the (op, type) pair maps."""
+    "rccl_native": RCCL's own collectives where the (op, type) pair maps.
+    parts: bench_collectives.py's MSX_COLL_PARTS.  The child is killed after
+    `timeout` seconds."""
     import subprocess
     import tempfile
     out = os.path.join(tempfile.gettempdir(),
-                       f"msx_coll_{transport}{tag}_{os.environ.get('MASTER_PORT', '0')}.json")
+                       f"msx_coll_{transport}{tag}_{parts}_{os.environ.get('MASTER_PORT', '0')}.json")
     env = dict(os.environ)
     env.update(extra_env or {})
+    env["MSX_COLL_PARTS"] = parts
     off = {"ipc": 113, "rccl": 127, "rccl_native": 139}[transport] + port_off   # same on every rank
     env.update({"MSX_SIZE": str(world), "MSX_RANK": str(rank), "MSX_DEVICE": str(local),
                 "MSX_TRANSPORT": transport,
@@ -118,13 +147,12 @@ def run_collectives_child(world, rank, local, scale, transport="ipc", extra_env=
 
     try:
         pr = subprocess.run([sys.executable, os.path.join(REPO, "bench_collectives.py"), out, str(scale)],
-                            env=env, capture_output=True, text=True,
-                            timeout=float(os.environ.get("MSX_COLL_TIMEOUT", "150" if transport == "ipc" else "120")))
+                            env=env, capture_output=True, text=True, timeout=timeout)
         if pr.returncode != 0:
             return {"error": child_error(f"rc={pr.returncode}", pr.stderr)}
     except subprocess.TimeoutExpired as e:
         se = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else e.stderr
-        return {"error": child_error("timed out", se)}
+        return {"error": child_error(f"timed out after {timeout:.0f} s", se)}
     if rank == 0:
         try:
             with open(out) as f:
@@ -180,7 +208,7 @@ def rccl_native_child_main(out, scale):
     dist.destroy_process_group()
 
 
-def rccl_native_allreduce(world, rank, local, scale):
+def rccl_native_allreduce(world, rank, local, scale, timeout=90.0):
     """xGMI reference point: RCCL's own fp32 SUM allreduce (its ring/tree order,
     NOT the reference's association) on c3's 1 GiB/rank, same GPUs.  Runs in a
     child process per rank with its own rendezvous and a time limit, so an
@@ -194,11 +222,11 @@ def rccl_native_allreduce(world, rank, local, scale):
     try:
         pr = subprocess.run([sys.executable, os.path.abspath(__file__), "--rccl-native-child", out,
                              "--coll-scale", str(scale)], env=env, capture_output=True, text=True,
-                            timeout=float(os.environ.get("MSX_RCCL_NATIVE_TIMEOUT", "120")))
+                            timeout=timeout)
         if pr.returncode != 0:
             return {"error": f"rank {rank} child rc={pr.returncode}: {pr.stderr[-600:]}"}
     except subprocess.TimeoutExpired:
-        return {"error": f"rank {rank} child timed out"}
+        return {"error": f"rank {rank} child timed out after {timeout:.0f} s"}
     if rank == 0:
         try:
             with open(out) as f:
@@ -238,7 +266,7 @@ def multi_host_child_main(out, n):
         json.dump(res, f)
 
 
-def run_multi_host_child(n):
+def run_multi_host_child(n, timeout=60.0):
     import subprocess
     import tempfile
     out = os.path.join(tempfile.gettempdir(), f"msx_multi_host_{os.getpid()}.json")
@@ -247,13 +275,13 @@ def run_multi_host_child(n):
         env.pop(k, None)
     try:
         pr = subprocess.run([sys.executable, os.path.abspath(__file__), "--multi-host-child", out,
-                             "--elems", str(n)], env=env, capture_output=True, text=True, timeout=120)
+                             "--elems", str(n)], env=env, capture_output=True, text=True, timeout=timeout)
         if pr.returncode != 0:
             return {"error": f"child rc={pr.returncode}: {pr.stderr[-600:]}"}
         with open(out) as f:
             return json.load(f)
     except subprocess.TimeoutExpired:
-        return {"error": "child timed out"}
+        return {"error": f"child timed out after {timeout:.0f} s"}
     except (OSError, ValueError) as e:
         return {"error": str(e)}
 
@@ -479,7 +507,7 @@ def cpu_baseline_collectives(p=8, reps=20, warmup=3):
     return out
 
 
-def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
+def per_op_roofline(L, C, torch, dev, stream, nbytes):
     """GB/s of HBM traffic (2 reads + 1 write per element) per (op, type), from
     HIP events on the launch stream around 10 launches (median of 3 rounds).
     Operands are random bytes interpreted as the MPI type, except floating
@@ -588,14 +616,6 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes, tree_sweep=False):
             {"pmc_raw_kib": raw, "traffic": int((2 * raw["FETCH_SIZE"] + raw["WRITE_SIZE"]) * 1024),
              "bytes_per_launch": (p + 1) * m * 4})
     out["tree8_pow2_stride/MPI_SUM/MPI_FLOAT"] = entry(time_tree(srcs_pow2))
-    if tree_sweep:
-        for mode, name in ((8, "generic"), (1, "generic_upfront"), (2, "generic_upfront_nt"),
-                           (3, "generic_interleaved_nt"), (4, "fixed_u1"), (5, "fixed_u2"), (6, "fixed_u4"),
-                           (7, "fixed_u2_nt")):
-            for cap in (0, 1024, 4096, 65536):
-                L.msx_tune_tree(mode, cap)
-                out[f"tree8_sweep/{name}/cap{cap}"] = entry(time_tree())
-        L.msx_tune_tree(0, 0)
     del a, b
     return out
 
@@ -654,8 +674,8 @@ def pack_roofline(L, C, torch, dev, stream):
         if rc or not torch.equal(packed, want.view(-1).view(torch.uint8)):
             raise RuntimeError(f"pack parity failed for {name}: rc={rc}")
         # HBM moves whole 32-B sectors: a gapped typed side touches more bytes
-        # than it carries (scripts/gap_probe.py: a bare 16-of-32-B store kernel
-        # reports WRITE_SIZE = 2x its data too), so each entry also reports
+        # than it carries (round 4: a bare 16-of-32-B store kernel, the probe
+        # library's gapped-store mode, reports WRITE_SIZE = 2x its data too), so each entry also reports
         # packed bytes + the typed side's touched 32-B sectors
         typed_sectors = {"vector_16B_blocks_stride32B": 2 * nb, "double_int_records_12of16B": nb * 16 // 12,
                          "subarray3d_fp32_rows1536B": nb}[name]
@@ -687,29 +707,35 @@ def pack_roofline(L, C, torch, dev, stream):
     return out
 
 
-def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12, mixes=True):
+def cold_cache_launch(P, torch, dev, stream, src, acc, n, reps=12, mixes=True):
     """The headline launch with the Infinity Cache cold.  MI355X has a 256 MiB
     memory-side cache (MALL); back to back on the same 256 MiB operands it
-    serves part of every launch (scripts/mall_probe.py: 256 MiB 115 us warm vs
-    140 us cold; from 512 MiB per operand on, warm = cold).  Here each launch
-    follows a read + write pass over 1 GiB of other data and is timed alone
-    with HIP events; the DRAM-only rate next to the 2R+1W ceiling the same
-    cold method gives the copy-like stream mix is what the kernel does without
-    the cache.  Reported beside `value`, never part of it."""
+    serves part of every launch (round 3: 256 MiB 115 us warm vs 140 us cold;
+    from 512 MiB per operand on, warm = cold).  Here each launch follows a
+    read + write pass over 1 GiB of other data and is timed alone with HIP
+    events; the DRAM-only rate next to the 2R+1W ceiling the same cold method
+    gives the copy-like stream mix is what the kernel does without the cache.
+    The launches run the default kernel body (k_combine_dram's) under the probe
+    library's symbol k_probe_combine<1, 64, true, false, -1>, so these single
+    launches stay out of the headline symbol's rocprof average.  Reported
+    beside `value`, never part of it."""
+    from msx import probe
     sp = ctypes.c_void_p(stream.cuda_stream)
-    # the default kernel body under its probe symbol (k_combine_rr<..., 64, ...,
-    # -2>, the body of k_combine_dram), so these single launches stay out of
-    # the headline symbol's rocprof average
-    L.msx_tune_variant_name.restype = ctypes.c_char_p
-    probe_v = [v for v in range(L.msx_tune_variant_count())
-               if L.msx_tune_variant_name(v).decode() == "default_body_probe"]
-    if not probe_v or L.msx_tune_set(probe_v[0], 0) != 0:
+    v = probe.variants().get("default_body_probe")
+    if v is None:
         return {"error": "default_body_probe variant missing"}
+
+    def step():
+        if P.msxp_variant_run(v, src.data_ptr(), acc.data_ptr(), n, sp):
+            raise RuntimeError("probe variant launch failed")
     flush = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+
+    def flush_cache():
+        P.msxp_hbm(probe.READ1, flush.data_ptr(), flush.data_ptr(), flush.numel(), sp)
+        P.msxp_hbm(probe.WRITE1, flush.data_ptr(), flush.data_ptr(), flush.numel(), sp)
     ts, warm = [], []
     for _ in range(reps):
-        L.msx_probe_hbm(3, flush.data_ptr(), flush.data_ptr(), flush.numel(), sp)
-        L.msx_probe_hbm(1, flush.data_ptr(), flush.data_ptr(), flush.numel(), sp)
+        flush_cache()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         step()
@@ -730,34 +756,31 @@ def cold_cache_launch(L, C, torch, dev, stream, step, n, reps=12, mixes=True):
     a2.random_(0, 256)
     b2.random_(0, 256)
     torch.cuda.synchronize()
-    kinds, mixes = (((2, "copy_r1w1", 2), (9, "copy_r1w1_dispatch_order", 2), (0, "read2", 2))
-                    if mixes else ()), {}
+    kinds, mixes = (((probe.COPY, "copy_r1w1", 2), (probe.COPY_DISPATCH_ORDER, "copy_r1w1_dispatch_order", 2),
+                     (probe.READ2, "read2", 2)) if mixes else ()), {}
     for mode, name, streams in kinds:
         pt = []
         for _ in range(reps):
-            L.msx_probe_hbm(3, flush.data_ptr(), flush.data_ptr(), flush.numel(), sp)
-            L.msx_probe_hbm(1, flush.data_ptr(), flush.data_ptr(), flush.numel(), sp)
+            flush_cache()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            L.msx_probe_hbm(mode, a2.data_ptr(), b2.data_ptr(), n * 4, sp)
+            P.msxp_hbm(mode, a2.data_ptr(), b2.data_ptr(), n * 4, sp)
             e1.record(stream)
             torch.cuda.synchronize()
             pt.append(e0.elapsed_time(e1))
         pms = sorted(pt)[reps // 2]
         mixes[name] = round(streams * n * 4 / pms / 1e6, 1)
     del flush, a2, b2
-    L.msx_tune_set(0, 0)
     cms, wms = sorted(ts)[reps // 2], sorted(warm)[reps // 2]
     gbs = n * BYTES_PER_ELEM / cms / 1e6
     return {"cold_us": round(cms * 1e3, 1), "cold_GB_s": round(gbs, 1), "cold_frac": round(gbs / HBM_PEAK_GBS, 4),
             "warm_single_us": round(wms * 1e3, 1), "cold_probe_GB_s": mixes,
             "method": "median of 12 single launches, each after a 1 GiB read + write pass over other data "
                       "(cold) or right after the previous launch (warm); HIP events on the launch stream; "
-                      "the default kernel body under its probe symbol k_combine_rr<3, float, float, 1, 64, "
-                      "true, false, -2>"}
+                      "the default kernel body under the probe symbol k_probe_combine<1, 64, true, false, -1>"}
 
 
-def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
+def hbm_ceiling_probe(P, torch, dev, stream, nbytes):
     """What this GPU's HBM delivers for other stream mixes on the same
     2 x 256 MiB operands, in the tile geometry (k_probe: 16 B per lane,
     256-lane workgroups, one tile each, XCD-contiguous, non-temporal loads):
@@ -765,7 +788,7 @@ def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
     default geometry at this size (k_copy_dram: one-wave workgroups in
     dispatch order).  Median of 3 rounds of 10 launches, HIP events on the
     launch stream.  Context for the roofline's `frac` (which stays against
-    the 8 TB/s spec peak)."""
+    the 8 TB/s spec peak).  Bench-only kernels (libmsx_probe.so)."""
     sp = ctypes.c_void_p(stream.cuda_stream)
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -779,11 +802,11 @@ def hbm_ceiling_probe(L, torch, dev, stream, nbytes):
         ts = []
         for _ in range(3):
             for _ in range(2):
-                L.msx_probe_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, sp)
+                P.msxp_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, sp)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(10):
-                rc = L.msx_probe_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, sp)
+                rc = P.msxp_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, sp)
                 if rc:
                     raise RuntimeError(f"probe {name}: rc={rc}")
             e1.record(stream)
@@ -902,8 +925,8 @@ def main():
     os.environ["MSX_SIZE"], os.environ["MSX_RANK"], os.environ["MSX_DEVICE"] = "1", "0", str(local)
     L = msx.init(errors_return=True)
     C = msx.C
-    if args.variant >= 0:
-        assert L.msx_tune_set(args.variant, 0) == 0
+    from msx import probe
+    P = probe.lib()                          # bench-only measurement kernels
 
     n = args.elems
     g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
@@ -928,27 +951,27 @@ def main():
 
     sweep = {}
     if args.sweep and rank == 0:
-        # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
-        configs = [(v, cap) for v in range(L.msx_tune_variant_count()) for cap in (0, 2048, 4096, 8192)]
-        times = {c: [] for c in configs}
+        # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule
+        # 24): the product kernel and the probe library's variants of its body
+        runs = {"product": step}
+        for name, v in probe.variants().items():
+            runs[name] = (lambda v=v: P.msxp_variant_run(v, src.data_ptr(), acc.data_ptr(), n, sp))
+        times = {k: [] for k in runs}
         for _ in range(3):
-            for (v, cap) in configs:
-                L.msx_tune_set(v, cap)
+            for key, fn in runs.items():
                 for _ in range(3):
-                    step()
+                    fn()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(10):
-                    step()
+                    fn()
                 e1.record(stream)
                 torch.cuda.synchronize()
-                times[(v, cap)].append(e0.elapsed_time(e1) / 10)
-        for (v, cap), ts in times.items():
+                times[key].append(e0.elapsed_time(e1) / 10)
+        for key, ts in times.items():
             ms = sorted(ts)[len(ts) // 2]
-            key = f"{L.msx_tune_variant_name(v).decode()}/cap{cap}"
             sweep[key] = round(n * BYTES_PER_ELEM / ms / 1e6, 1)
             print(f"{key}: {ms * 1e3:.1f} us {sweep[key]:.0f} GB/s", file=sys.stderr)
-        L.msx_tune_set(max(args.variant, 0), 0)
         # operand placement: the default kernel with `in` and `inout` carved
         # from one allocation at exactly 256 MiB apart vs skewed by a few KiB
         # (HBM bank aliasing of two streams a power of two apart)
@@ -1008,71 +1031,101 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms_max = float(t[0]), float(t[1])
 
-    # N > 1: the collective configs c3-c5 in child MPI processes (not part of
-    # `value`); each rank reports whether its child succeeded.
-    coll = coll_rccl = coll_native = rccl_native = c3_variants = None
+    # N > 1: the collective configs in child MPI processes (not part of
+    # `value`), each under a time limit cut to the remaining wall budget
+    # (WALL_BUDGET_S above); rank 0's clock decides, so every rank runs and
+    # skips the same children.  Each rank reports whether its child succeeded.
+    coll = coll_rccl = coll_native = rccl_native = c3_variants = coll_extras = multi_host = None
+    budget = {"wall_budget_s": WALL_BUDGET_S, "reserve_s": RESERVE_S, "child_cap_s": CHILD_CAP_S, "steps": []}
     distinct = torch.cuda.device_count() >= world      # one GPU per rank (RCCL needs it)
-    if world > 1 and not args.no_collectives:
-        ipc_failed = [False]
 
-        def collect(transport):
-            mine = run_collectives_child(world, rank, local, args.coll_scale, transport)
+    def allot(name, collective=True):
+        """Seconds child `name` may run (None: skipped), from rank 0's clock."""
+        el = [time.time() - T_START]
+        if collective:
+            dist.broadcast_object_list(el, src=0)
+        t = child_timeout(name, el[0])
+        step = {"name": name, "start_s": round(el[0], 1), "timeout_s": None if t is None else round(t, 1)}
+        if t is None:
+            step["skipped"] = "wall budget"
+        budget["steps"].append(step)
+        return t
+
+    def took(res):
+        budget["steps"][-1]["elapsed_s"] = round(time.time() - T_START - budget["steps"][-1]["start_s"], 1)
+        if isinstance(res, dict) and "error" in res:
+            budget["steps"][-1]["error"] = True
+        return res
+
+    if world > 1 and not args.no_collectives:
+        def collect(transport, name, parts, extra=None, tag="", port_off=0):
+            t = allot(name)
+            if t is None:
+                return {"skipped": "wall budget"} if rank == 0 else None
+            mine = run_collectives_child(world, rank, local, args.coll_scale, transport, extra, tag, port_off,
+                                         parts=parts, timeout=t)
             errs = [None] * world
             dist.all_gather_object(errs, mine.get("error"))      # every rank's structured error
-            if transport == "ipc":
-                ipc_failed[0] = any(e is not None for e in errs)   # the same on every rank
             res = mine if rank == 0 else None
             if rank == 0 and any(e is not None for e in errs):
                 res["errors"] = [dict(e, rank=r) if isinstance(e, dict) else {"rank": r, "text": e}
                                  for r, e in enumerate(errs) if e is not None]
                 res.setdefault("error", res["errors"][0])
-            return res
-        coll = collect("ipc")
+            return took(res) if rank == 0 else None
+        # 1. the default data plane's headline configs (and the all-peer probe)
+        coll = collect("ipc", "ipc_core", "core")
         if distinct:
-            coll_rccl = collect("rccl")
-            # this library's MPI calls on RCCL's own collectives (MSX_TRANSPORT=
-            # rccl_native: ncclAllReduce / ncclReduce / ncclReduceScatter where
-            # the pair maps, RCCL order; the harness's integer-valued inputs
-            # make every order exact, so `correct` still checks in full)
-            coll_native = collect("rccl_native")
-            mine = rccl_native_allreduce(world, rank, local, args.coll_scale)
-            ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            rccl_native = mine if rank == 0 else None
-            if rank == 0 and not ok.item() and "error" not in rccl_native:
-                rccl_native["error"] = "a non-zero rank's child failed"
-        # the engine-variant sweep (IPC plane only) at N = 8, or at the N that
-        # MSX_BENCH_VARIANTS_AT names (a rehearsal of this code on fewer GPUs)
-        # (skipped when the default IPC run failed: its variants would only
-        # repeat the failure, each up to its child's time limit)
-        if world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")) and ipc_failed[0]:
-            c3_variants = {"skipped": "the default IPC collectives child failed (see collectives.error)"}
-        elif world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")):
-            c3_variants = {}
-            for vi, (name, extra) in enumerate(C3_VARIANTS):
-                mine = run_collectives_child(world, rank, local, args.coll_scale, "ipc",
-                                             dict(extra, MSX_COLL_ONLY="c3c4"), tag="_" + name,
-                                             port_off=200 + 11 * vi)
-                errs = [None] * world
-                dist.all_gather_object(errs, mine.get("error"))
+            # 2. the RCCL send/recv plane, then this library's MPI calls on
+            # RCCL's own collectives (MSX_TRANSPORT=rccl_native: ncclAllReduce /
+            # ncclReduce / ncclReduceScatter where the pair maps, RCCL order;
+            # the harness's integer-valued inputs make every order exact, so
+            # `correct` still checks in full)
+            coll_rccl = collect("rccl", "rccl_core", "core")
+            coll_native = collect("rccl_native", "rccl_native_core", "core")
+            # 3. RCCL's own fp32 allreduce (torch.distributed), the xGMI reference point
+            t = allot("rccl_allreduce")
+            if t is not None:
+                mine = rccl_native_allreduce(world, rank, local, args.coll_scale, timeout=t)
+                ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                rccl_native = mine if rank == 0 else None
                 if rank == 0:
-                    ent = {"env": extra}
-                    for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4")):
-                        v = mine.get(key) or {}
-                        ent[tag] = {k: v.get(k) for k in ("seconds", "busbw_GB_s", "correct") if k in v}
-                    if any(errs):
-                        ent["errors"] = [e for e in errs if e]
-                    c3_variants[name] = ent
-
-    # SURVEY §8(e) strong-scaled local reduce on the MPI path's host buffers:
-    # one 256 MiB fp32 MPI_SUM vector split over every GPU of the node, each
-    # GPU over its own PCIe link (msx_reduce_local_multi), against the same call
-    # on one GPU -- rank 0, after the collectives while the other ranks wait,
-    # in a child process with a time limit (like the collectives) so a failure
-    # there can never take this JSON line down
-    multi_host = None
-    if world > 1 and rank == 0 and not args.no_host_path:
-        multi_host = run_multi_host_child(n)
+                    if not ok.item() and "error" not in rccl_native:
+                        rccl_native["error"] = "a non-zero rank's child failed"
+                    took(rccl_native)
+        # 4. the other schedule of c3 / c4 (IPC plane) at N = 8, or at the N
+        # that MSX_BENCH_VARIANTS_AT names (a rehearsal on fewer GPUs); skipped
+        # when the default IPC run failed (it would only repeat the failure)
+        ipc_failed = [rank == 0 and (coll is None or "error" in coll or "skipped" in coll)]
+        dist.broadcast_object_list(ipc_failed, src=0)
+        if world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")):
+            if ipc_failed[0]:
+                c3_variants = {"skipped": "the default IPC collectives child failed (see collectives.error)"}
+            else:
+                c3_variants = {}
+                for vi, (name, extra) in enumerate(C3_VARIANTS):
+                    mine = collect("ipc", "variant_" + name, "c3c4", extra, tag="_" + name, port_off=200 + 11 * vi)
+                    if rank == 0:
+                        ent = {"env": extra}
+                        if "skipped" in mine:
+                            ent["skipped"] = mine["skipped"]
+                        for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4")):
+                            v = mine.get(key) or {}
+                            ent[tag] = {k: v.get(k) for k in ("seconds", "busbw_GB_s", "correct") if k in v}
+                        if mine.get("errors"):
+                            ent["errors"] = mine["errors"]
+                        c3_variants[name] = ent
+        # 5. the IPC plane's remaining configs (curve, host memory, rooted
+        # reduce, scan, one-sided accumulate)
+        coll_extras = collect("ipc", "ipc_extras", "extras", tag="_extras", port_off=300)
+        # 6. SURVEY §8(e) strong-scaled local reduce on the MPI path's host
+        # buffers: one 256 MiB fp32 MPI_SUM vector split over every GPU of the
+        # node, each GPU over its own PCIe link (msx_reduce_local_multi),
+        # against the same call on one GPU -- rank 0 only, while the other
+        # ranks wait at the closing barrier
+        if rank == 0 and not args.no_host_path:
+            t = allot("multi_host", collective=False)
+            multi_host = took(run_multi_host_child(n, timeout=t)) if t is not None else {"skipped": "wall budget"}
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
     host = None
@@ -1126,18 +1179,18 @@ def main():
 
     per_op = None
     if rank == 0 and world == 1 and not args.no_per_op:
-        per_op = per_op_roofline(L, C, torch, dev, stream, n * 4, tree_sweep=args.sweep)
+        per_op = per_op_roofline(L, C, torch, dev, stream, n * 4)
     pack = None
     if rank == 0 and world == 1 and not args.no_pack:
         pack = pack_roofline(L, C, torch, dev, stream)
-    rma = probe = cold = None
+    rma = hbm = cold = None
     if rank == 0 and world == 1 and not args.no_per_op:
         rma = rma_self_roofline(L, C, torch, dev, n)
-        probe = hbm_ceiling_probe(L, torch, dev, stream, n * 4)
+        hbm = hbm_ceiling_probe(P, torch, dev, stream, n * 4)
     if rank == 0:
         # SURVEY.md §7 "use cold buffers": the headline launch with the Infinity
         # Cache flushed first, reported in `roofline` beside the back-to-back frac
-        cold = cold_cache_launch(L, C, torch, dev, stream, step, n, mixes=(world == 1 and not args.no_per_op))
+        cold = cold_cache_launch(P, torch, dev, stream, src, acc, n, mixes=(world == 1 and not args.no_per_op))
 
     if rank == 0:
         total_bytes = world * args.steps * n * BYTES_PER_ELEM
@@ -1179,15 +1232,22 @@ def main():
                                     "kernel_us_cold": cold["cold_us"],
                                     "cold_method": "median of 12 single launches, each after a 1 GiB read + "
                                                    "write pass over other data (flushes the 256 MiB MALL); "
-                                                   "kernel symbol k_combine_rr<3, float, float, 1, 64, true, "
-                                                   "false, -2> (the default body, k_combine_dram's, under its "
-                                                   "probe name)"})
+                                                   "the default body (k_combine_dram's) under the bench-only "
+                                                   "symbol k_probe_combine<1, 64, true, false, -1>"})
         if host is not None:
             out["host_path"] = host
         if multi_host is not None:
             out["host_path_multi_gpu"] = multi_host
+        # the all-peer write probe of the IPC child (every GPU writing into
+        # all peers' windows at once: the links' measured per-GPU outbound
+        # rate); every plane's busBW is read against it.  Null when the ranks
+        # share a GPU (no byte crosses xGMI there) or the probe did not run.
+        shared = bool(coll and coll.get("gpu_shared"))
+        links = None if shared else ((coll or {}).get("peer_write_probe") or {}).get("outbound_GB_s_per_gpu")
+
         def summarize(c):
-            """c3-c5 of one data plane at a glance: correct, busBW, fractions."""
+            """c3-c5 of one data plane at a glance: correct, busBW, the xGMI
+            fraction against the measured links (null on a shared GPU)."""
             if not c:
                 return None
             sm = {}
@@ -1195,16 +1255,29 @@ def main():
                              ("c5_iallreduce_band_u64", "c5")):
                 v = c.get(key)
                 if v:
-                    sm[tag] = {k: v.get(k) for k in ("correct", "busbw_GB_s", "busbw_frac_measured_links",
-                                                      "busbw_frac_xgmi") if k in v}
-            if c.get("peer_write_probe"):
-                sm["measured_links_GB_s_per_gpu"] = c["peer_write_probe"].get("outbound_GB_s_per_gpu")
-            if "error" in c:
-                sm["error"] = c["error"]
+                    sm[tag] = {k: v.get(k) for k in ("correct", "busbw_GB_s", "seconds", "t_comm_s") if k in v}
+                    bw = v.get("busbw_GB_s")
+                    sm[tag]["busbw_frac_measured_links"] = round(bw / links, 3) if (bw and links) else None
+            for k in ("error", "skipped"):
+                if k in c:
+                    sm[k] = c[k]
             return sm
         if coll is not None or coll_rccl is not None:
-            out["collectives_summary"] = {"ipc": summarize(coll), "rccl": summarize(coll_rccl),
-                                          "rccl_native": summarize(coll_native)}
+            native = None
+            if rccl_native is not None:
+                bw = rccl_native.get("busbw_GB_s")
+                native = {k: rccl_native.get(k) for k in ("correct", "busbw_GB_s", "error") if k in rccl_native}
+                native["busbw_frac_measured_links"] = round(bw / links, 3) if (bw and links) else None
+            out["collectives_summary"] = {"plane": "hbm (ranks share one GPU)" if shared else "xgmi",
+                                          "measured_links_GB_s_per_gpu": links,
+                                          "ipc": summarize(coll), "rccl": summarize(coll_rccl),
+                                          "rccl_native": summarize(coll_native),
+                                          "rccl_own_allreduce_f32": native}
+        if budget["steps"]:
+            budget["wall_s_at_json"] = round(time.time() - T_START, 1)
+            out["wall_budget"] = budget
+        if coll_extras is not None:
+            out["collectives_extras"] = coll_extras
         if coll is not None:
             out["collectives"] = coll
         if coll_rccl is not None:
@@ -1221,8 +1294,8 @@ def main():
             out["datatype_pack_roofline_hbm"] = pack
         if rma is not None:
             out["rma_self_accumulate_f32"] = rma
-        if probe is not None:
-            out["hbm_ceiling_probe"] = probe
+        if hbm is not None:
+            out["hbm_ceiling_probe"] = hbm
         if cold is not None:
             out["infinity_cache"] = cold
         if sweep:

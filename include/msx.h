@@ -134,8 +134,6 @@ int msx_reduce_local_multi(const void* in, void* inout, int64_t count, MPI_Datat
 int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count,
                         MPI_Datatype datatype, MPI_Op op, void* stream);
 
-/* benchmark knobs for the fp32 SUM hot path: variant index (0 = default) and
- * a cap on workgroups (0 = one tile per workgroup). */
 /* Any reference-order tree the engine evaluates: P leaves (power of two <= 16)
  * over srcs[2k] and, when bit k of pairmask is set, its fold pair srcs[2k+1]
  * (leaf k = op(srcs[2k] as inout, srcs[2k+1] as in)); leaves >= nleaves absent
@@ -143,46 +141,21 @@ int msx_reduce_tree_dev(const void* const* srcs, int p, void* out, int64_t count
  * Stream-ordered, device pointers (tests and probes of the tree kernels). */
 int msx_reduce_tree_spec_dev(const void* const* srcs, int P, unsigned pairmask, int nleaves, int chain,
                              void* out, int64_t count, MPI_Datatype datatype, MPI_Op op, void* stream);
-int msx_tune_set(int variant, int grid_cap);
-int msx_tune_variant_count(void);
-/* collective tree combine (msx_reduce_tree_dev and the engine), fp32 SUM only:
- * mode 0 = default (compile-time source count for full trees and chains of
- * 2/4/8 sources, else the generic kernel), 1 = generic with all sources
- * loaded up front, 2 = up front + non-temporal, 3 = generic interleaved +
- * non-temporal, 4/5/6 = compile-time source count with 1/2/4 vectors per lane,
- * 7 = as 5 with non-temporal loads, 8 = generic kernel (loads interleaved with
- * the combines); grid_cap 0 = default. */
-int msx_tune_tree(int mode, int grid_cap);
-const char* msx_tune_variant_name(int variant);
-/* realigning combine for mutually misaligned operands: the cross-lane move of
- * the `in` chunks, 0 = DPP wave shift (default), 1 = ds_bpermute, 2 = DPP on
- * the earlier wave grid skewed by one vector (measurement) */
-int msx_tune_shift(int mode);
-/* Pack / unpack and derived-target accumulate geometry (tuning only): 0 = by
- * size (default; the one-wave tile form when typed span + packed bytes exceed
- * MSX_PACK_TILE_MIN, 512 MiB, for pack / unpack and MSX_ACC_TILE_MIN, 0, for
- * the accumulate), 1 = always the grid-stride form, 2 = always the tile form. */
+/* The engine's local copy kernel (the collectives' collect step): dst <- src,
+ * `bytes` bytes of device memory, stream-ordered (tests of the copy kernels). */
+int msx_copy_dev(void* dst, const void* src, int64_t bytes, void* stream);
+/* Test hook: pack / unpack and derived-target accumulate geometry.  0 = by
+ * size (default: the one-wave tile form when typed span + packed bytes exceed
+ * 512 MiB for pack / unpack, always for the accumulate), 1 = always the
+ * grid-stride form, 2 = always the tile form.  The measurement kernels (HBM
+ * probes, combine variants) live in the bench-only libmsx_probe.so. */
 int msx_tune_pack(int mode);
-/* HBM ceiling probe (measurement only): the default combine's launch geometry
- * with another stream mix over `bytes` per stream (16-B aligned device
- * pointers): mode 0 reads a and b, 1 writes b, 2 copies a -> b, 3 reads a;
- * 4 copies a -> b with the engine's segment-copy kernel (k_copy_segs), 5 with
- * hipMemcpyAsync; 6 writes 16 B of every 32 B of b (gapped store), 7 reads
- * 16 B of every 32 B of a (gapped load); 8 / 9 copy a -> b in a forced
- * geometry (8: k_copy_segs' XCD-contiguous 4-KiB tiles, 9: k_copy_dram's
- * one-wave workgroups in dispatch order).
- * Stream-ordered; b's contents are unspecified afterwards. */
-int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream);
-/* device allocation for measurements: uncached = the engine windows' memory
- * type (hipDeviceMallocUncached), else plain hipMalloc; msx_probe_free releases */
-int msx_probe_alloc(int64_t bytes, int uncached, void** out);
-int msx_probe_free(void* p);
 
 /* host staging chunk size (bytes) for MPI_Reduce_local on host buffers */
 int msx_set_staging_chunk(int64_t bytes);
 /* host operands of MPI_Reduce_local: 0 (default) = pinned host memory is
  * combined in place by the kernel over PCIe (zero-copy), pageable memory of
- * at least MSX_HOST_PIN_MIN bytes (1 MiB) is pinned for the call and combined
+ * at least 1 MiB is pinned for the call and combined
  * the same way (staged through HBM if the driver refuses to pin it);
  * 1 = every host operand is staged through HBM; 2 = pinned memory in place,
  * pageable memory staged */

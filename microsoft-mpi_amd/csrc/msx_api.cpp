@@ -2487,58 +2487,30 @@ MSX_EXPORT int msx_reduce_tree_spec_dev(const void* const* srcs, int P, unsigned
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "tree kernel launch");
 }
 
-MSX_EXPORT int msx_tune_set(int variant, int grid_cap)
+// The engine's local copy (the collect step of the collectives, MPIR_Localcopy
+// of device data, mpid/pt2pt.cpp:929-948): k_copy_segs' XCD-contiguous 4-KiB
+// tiles up to 16 MiB, k_copy_dram's one-wave dispatch-order grid above.
+// Stream-ordered, device pointers (tests of the copy kernels).
+MSX_EXPORT int msx_copy_dev(void* dst, const void* src, int64_t bytes, void* stream)
 {
-    if (variant < 0 || variant >= combine_variant_count() || grid_cap < 0) return MPI_ERR_ARG;
-    launch_cfg().variant = variant;
-    launch_cfg().grid_cap = grid_cap;
-    return MPI_SUCCESS;
+    if (bytes < 0 || (bytes > 0 && (!dst || !src))) return MPI_ERR_ARG;
+    if (bytes == 0) return MPI_SUCCESS;
+    int rc = ensure_device();
+    if (rc != MPI_SUCCESS) return rc;
+    const void* ps = src;
+    void* pd = dst;
+    size_t n = (size_t)bytes;
+    hipError_t e = launch_copy_segs(&ps, &pd, &n, 1, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy kernel launch");
 }
 
-MSX_EXPORT int msx_tune_shift(int mode)
-{
-    return shift_tune_set(mode) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
-}
-
+// Test hook: the pack/unpack/accumulate kernel geometry (0 = by size, the
+// default; 1 = grid-stride form; 2 = tile form at every size), so small test
+// cases run the kernels the default takes at large sizes.
 MSX_EXPORT int msx_tune_pack(int mode)
 {
     return pack_tune_set(mode) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
 }
-
-MSX_EXPORT int msx_tune_tree(int mode, int grid_cap)
-{
-    return tree_tune_set(mode, grid_cap) == 0 ? MPI_SUCCESS : MPI_ERR_ARG;
-}
-
-MSX_EXPORT int msx_probe_hbm(int mode, const void* a, void* b, int64_t bytes, void* stream)
-{
-    if (mode < 0 || mode > 9 || bytes < 0 || !b || (mode != 1 && mode != 6 && !a)) return MPI_ERR_ARG;
-    int rc = ensure_device();
-    if (rc != MPI_SUCCESS) return rc;
-    hipError_t e = launch_probe(mode, a, b, (size_t)bytes, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "probe launch");
-}
-
-// Device memory with the engine windows' cache type (measurement only): the
-// collective trees read uncached window memory, so the bench times them there.
-MSX_EXPORT int msx_probe_alloc(int64_t bytes, int uncached, void** out)
-{
-    if (bytes <= 0 || !out) return MPI_ERR_ARG;
-    *out = nullptr;
-    int rc = ensure_device();
-    if (rc != MPI_SUCCESS) return rc;
-    hipError_t e = uncached ? hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached)
-                            : hipMalloc(out, (size_t)bytes);
-    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "probe allocation");
-}
-
-MSX_EXPORT int msx_probe_free(void* p)
-{
-    return p && hipFree(p) != hipSuccess ? MPI_ERR_ARG : MPI_SUCCESS;
-}
-
-MSX_EXPORT int msx_tune_variant_count(void) { return combine_variant_count(); }
-MSX_EXPORT const char* msx_tune_variant_name(int v) { return combine_variant_name(v); }
 
 MSX_EXPORT int msx_set_staging_chunk(int64_t bytes)
 {

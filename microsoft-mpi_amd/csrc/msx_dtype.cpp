@@ -34,12 +34,12 @@ namespace {
 
 constexpr int64_t kMaxRuns = (int64_t)1 << 25;     // explicit runs kept per type
 
-// Two-level compact forms (Dtype::rn2); MSX_DT_COMPACT2=0 expands them into
+// Two-level compact forms (Dtype::rn2); MSX_TEST_DT_COMPACT2=0 expands them into
 // explicit run lists as before (A/B and fallback).
 bool compact2_enabled()
 {
     static const bool on = [] {
-        const char* e = getenv("MSX_DT_COMPACT2");
+        const char* e = getenv("MSX_TEST_DT_COMPACT2");
         return !e || atoi(e) != 0;
     }();
     return on;

@@ -21,109 +21,17 @@
 #include <string.h>
 #include <type_traits>
 
-#include "msx_dev_ops.h"
+#include "msx_combine_dev.h"
 #include "msx_kernels.h"
 
 namespace msx {
 namespace dev {
-
-// Both registers are inputs of one (empty) asm statement: their loads are
-// issued back to back and waited for together, and no use of either can be
-// scheduled between them.
-__device__ __forceinline__ void issued_together(u32x4& x, u32x4& y)
-{
-    asm volatile("" : "+v"(x), "+v"(y));
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// ---- the streaming combine -------------------------------------------------------
-// Elements [0, head) and [head + nvec*EPV, head + nvec*EPV + tail) are scalar;
-// the vector body starts at element `head`, 16-byte aligned for both operands.
-// T  = element type used for scalar elements;
-// VT = lane type used inside a 16-byte vector (== T except bitwise ops, which
-//      run on 32-bit words regardless of the MPI element type).
-// XG: tile order -- 0 XCD-contiguous eighths, -1 dispatch order (round-robin
-// over XCDs), G > 0 XCD x owns interleaved runs of G consecutive tiles.
-template <int XG>
-__device__ __forceinline__ size_t combine_tile(unsigned b, unsigned nb)
-{
-    if constexpr (XG == 0) {
-        return xcd_tile(b, nb);
-    } else if constexpr (XG < 0) {
-        return b;
-    } else {
-        const unsigned full = (nb / (8u * XG)) * (8u * XG);
-        if (b >= full) return b;
-        const unsigned x = b & 7, j = b >> 3;
-        return ((size_t)(j / XG) * 8 + x) * XG + (j % XG);
-    }
-}
-
-template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, int XG = 0>
-__device__ __forceinline__ void combine_body(const T* __restrict__ in, T* __restrict__ io, size_t head,
-                                             size_t nvec, size_t tail)
-{
-    constexpr size_t EPV = 16 / sizeof(T);
-    constexpr size_t TILE = (size_t)BLOCK * UNROLL;
-    const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in + head);
-    u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
-    const size_t bid = combine_tile<XG>(blockIdx.x, gridDim.x);
-
-    for (size_t t0 = bid * TILE; t0 < nvec; t0 += (size_t)gridDim.x * TILE) {
-        const size_t i0 = t0 + threadIdx.x;
-        if (t0 + TILE <= nvec) {
-            u32x4 a[UNROLL], b[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                a[u] = ld<NTLD>(vin + i0 + (size_t)u * BLOCK);
-                b[u] = ld<NTLD>(vio + i0 + (size_t)u * BLOCK);
-            }
-            // Every load of the tile is issued before the first use: without
-            // this the compiler hoists work on the first operand (logical ops,
-            // complex, byte types) above the second load behind an
-            // s_waitcnt vmcnt(0), halving the bytes in flight (-7..10 %).
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) issued_together(a[u], b[u]);
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-                st<NTST>(vio + i0 + (size_t)u * BLOCK, apply_vec<OP, VT>(b[u], a[u]));
-        } else {
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const size_t i = i0 + (size_t)u * BLOCK;
-                if (i < nvec) {
-                    u32x4 x = vin[i], y = vio[i];
-                    issued_together(x, y);
-                    vio[i] = apply_vec<OP, VT>(y, x);
-                }
-            }
-        }
-    }
-
-    const size_t nscalar = head + tail;
-    if (nscalar) {
-        const size_t body_end = head + nvec * EPV;
-        for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nscalar;
-             s += (size_t)gridDim.x * BLOCK) {
-            const size_t e = s < head ? s : body_end + (s - head);
-            io[e] = Fn<OP>::apply(io[e], in[e]);
-        }
-    }
-}
 
 template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST>
 __global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* __restrict__ io,
                                                    size_t head, size_t nvec, size_t tail)
 {
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
-}
-
-// Tuning variant: the same body in another tile order (XG, see combine_tile).
-template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, int XG>
-__global__ __launch_bounds__(BLOCK) void k_combine_rr(const T* __restrict__ in, T* __restrict__ io,
-                                                      size_t head, size_t nvec, size_t tail)
-{
-    combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST, XG>(in, io, head, nvec, tail);
 }
 
 // Same body for operands far above the 256 MiB Infinity Cache (DRAM-bound):
@@ -186,16 +94,15 @@ __device__ __forceinline__ u32x4 realign(const u32x4& A, const u32x4& B, unsigne
 }
 
 // Lane i takes lane i+1's word: DPP wave_shl:1 (a VALU operand modifier on
-// the GFX9 family, dpp_ctrl 0x130) or a ds_bpermute through the LDS crossbar
-// (__shfl_down).  Lane 63 gets 0 either way; it loads its own next chunk.
-template <bool DPP>
+// the GFX9 family, dpp_ctrl 0x130).  Lane 63 gets 0; it loads its own next
+// chunk.  A ds_bpermute through the LDS crossbar measured the same (within
+// 0.5 %, profiles/r03/misalign/misalign_ab_box2.json).
 __device__ __forceinline__ unsigned from_next_lane(unsigned x)
 {
-    if constexpr (DPP) return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
-    else return __shfl_down(x, 1);
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
 }
 
-template <int OP, class T, class VT, int BLOCK, bool DPP, bool SKEW = false>
+template <int OP, class T, class VT, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_combine_shift(const T* __restrict__ in, T* __restrict__ io, size_t head,
                                                          size_t nvec, size_t tail, unsigned s)
 {
@@ -208,7 +115,7 @@ __global__ __launch_bounds__(BLOCK) void k_combine_shift(const T* __restrict__ i
     // vector grid (vector 0 is left idle, not shifted to lane 0: a grid that
     // started at vector 1 made every wave straddle one more 128-B line per
     // operand, -12 % at 256 MiB)
-    const size_t v = bid * BLOCK + threadIdx.x + (SKEW ? 1 : 0);   // SKEW: the old grid (measurement)
+    const size_t v = bid * BLOCK + threadIdx.x;
     const bool live = v >= 1 && v + 1 < nvec;
     // chunk v+1 is the next lane's chunk v: taken with a lane shuffle, loaded
     // only by the wave's last lane and the last live lane
@@ -225,10 +132,10 @@ __global__ __launch_bounds__(BLOCK) void k_combine_shift(const T* __restrict__ i
     asm volatile("" : "+v"(a), "+v"(y), "+v"(nx));
     __builtin_amdgcn_sched_barrier(0);
     u32x4 b;
-    b.x = from_next_lane<DPP>(a.x);
-    b.y = from_next_lane<DPP>(a.y);
-    b.z = from_next_lane<DPP>(a.z);
-    b.w = from_next_lane<DPP>(a.w);
+    b.x = from_next_lane(a.x);
+    b.y = from_next_lane(a.y);
+    b.z = from_next_lane(a.z);
+    b.w = from_next_lane(a.w);
     if (own_next) b = nx;
     if (live) vio[v] = apply_vec<OP, VT>(y, realign(a, b, s));
     // scalar: [0, head + EPV) and [head + (nvec - 1) * EPV, head + nvec * EPV + tail)
@@ -237,125 +144,6 @@ __global__ __launch_bounds__(BLOCK) void k_combine_shift(const T* __restrict__ i
     for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < nscalar; i += (size_t)gridDim.x * BLOCK) {
         const size_t e = i < first ? i : last0 + (i - first);
         io[e] = Fn<OP>::apply(io[e], in[e]);
-    }
-}
-
-// Tuning variant: KT consecutive tiles per workgroup (one contiguous run of
-// KT*BLOCK vectors per operand) instead of one tile per workgroup; UNR = the
-// KT tiles' loads may all be in flight together (else one tile at a time).
-template <int OP, class T, class VT, int BLOCK, int KT, bool UNR>
-__global__ __launch_bounds__(BLOCK) void k_combine_kt(const T* __restrict__ in, T* __restrict__ io, size_t head,
-                                                      size_t nvec, size_t tail)
-{
-    constexpr size_t EPV = 16 / sizeof(T);
-    const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in + head);
-    u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
-    const size_t t0 = (size_t)xcd_tile(blockIdx.x, gridDim.x) * KT * BLOCK + threadIdx.x;
-    if constexpr (UNR) {
-        u32x4 a[KT], b[KT];
-#pragma unroll
-        for (int j = 0; j < KT; ++j) {
-            const size_t i = t0 + (size_t)j * BLOCK;
-            if (i < nvec) { a[j] = ld<true>(vin + i); b[j] = ld<true>(vio + i); }
-        }
-#pragma unroll
-        for (int j = 0; j < KT; ++j) issued_together(a[j], b[j]);
-#pragma unroll
-        for (int j = 0; j < KT; ++j) {
-            const size_t i = t0 + (size_t)j * BLOCK;
-            if (i < nvec) vio[i] = apply_vec<OP, VT>(b[j], a[j]);
-        }
-    } else {
-#pragma unroll 1
-        for (int j = 0; j < KT; ++j) {
-            const size_t i = t0 + (size_t)j * BLOCK;
-            if (i < nvec) {
-                u32x4 x = ld<true>(vin + i), y = ld<true>(vio + i);
-                issued_together(x, y);
-                vio[i] = apply_vec<OP, VT>(y, x);
-            }
-        }
-    }
-    const size_t nscalar = head + tail;
-    if (nscalar) {
-        const size_t body_end = head + nvec * EPV;
-        for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nscalar; s += (size_t)gridDim.x * BLOCK) {
-            const size_t e = s < head ? s : body_end + (s - head);
-            io[e] = Fn<OP>::apply(io[e], in[e]);
-        }
-    }
-}
-
-// ---- HBM ceiling probe (measurement only) ----------------------------------------
-// The default combine's launch geometry (one 16-B vector per lane, 256-lane
-// workgroups, one tile each, XCD-contiguous tiles, non-temporal loads) with
-// other stream mixes, so the bench can say how close the 2-read + 1-write
-// combine gets to what this GPU's HBM actually delivers for each mix:
-//   MODE 0: read a and b (2R)   MODE 1: write b (1W)
-//   MODE 2: copy a -> b (1R1W)  MODE 3: read a (1R)
-// Reads feed a conditional store on a value random data essentially never
-// produces (`key`), so the compiler cannot drop them.
-template <int MODE>
-__global__ __launch_bounds__(256) void k_probe(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t nvec,
-                                               unsigned key)
-{
-    const size_t i = (size_t)xcd_tile(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
-    if (i >= nvec) return;
-    if constexpr (MODE == 0) {
-        u32x4 x = ld<true>(a + i), y = ld<true>(b + i);
-        issued_together(x, y);
-        const u32x4 r = x ^ y;
-        if ((r.x ^ r.y ^ r.z ^ r.w) == key) b[i] = r;
-    } else if constexpr (MODE == 1) {
-        b[i] = u32x4{key, key ^ (unsigned)i, key, (unsigned)(i >> 32)};
-    } else if constexpr (MODE == 2) {
-        b[i] = ld<true>(a + i);
-    } else if constexpr (MODE == 6) {
-        // gapped store: 16 B of every 32 B (the 16-B-block vector's unpack)
-        b[2 * i] = u32x4{key, key ^ (unsigned)i, key, (unsigned)(i >> 32)};
-    } else if constexpr (MODE == 7) {
-        // gapped load: 16 B of every 32 B (the same vector's pack)
-        const u32x4 x = ld<true>(a + 2 * i);
-        if ((x.x ^ x.y ^ x.z ^ x.w) == key) b[i] = x;
-    } else {
-        const u32x4 x = ld<true>(a + i);
-        if ((x.x ^ x.y ^ x.z ^ x.w) == key) b[i] = x;
-    }
-}
-
-// ---- LDS-staged variant (measurement only) ---------------------------------------
-// The north star's "LDS staging of the incoming chunk": the `in` tile goes
-// global -> LDS -> registers before the combine.  Each element is used once,
-// so the stage adds an LDS write + read per byte and a workgroup barrier for no
-// reuse; it is kept as a tuning variant so the sweep measures that cost
-//  instead of asserting it.
-template <int OP, class T, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_combine_lds(const T* __restrict__ in, T* __restrict__ io,
-                                                       size_t head, size_t nvec, size_t tail)
-{
-    __shared__ u32x4 stage[BLOCK];
-    constexpr size_t EPV = 16 / sizeof(T);
-    const u32x4* __restrict__ vin = reinterpret_cast<const u32x4*>(in + head);
-    u32x4* __restrict__ vio = reinterpret_cast<u32x4*>(io + head);
-    for (size_t t0 = (size_t)blockIdx.x * BLOCK; t0 < nvec; t0 += (size_t)gridDim.x * BLOCK) {
-        const size_t i = t0 + threadIdx.x;
-        const bool live = i < nvec;
-        u32x4 b = {};
-        if (live) {
-            stage[threadIdx.x] = ld<true>(vin + i);
-            b = ld<true>(vio + i);
-        }
-        __syncthreads();
-        if (live) vio[i] = apply_vec<OP, T>(b, stage[threadIdx.x]);
-        __syncthreads();
-    }
-    const size_t nscalar = head + tail;
-    if (nscalar) {
-        const size_t body_end = head + nvec * EPV;
-        for (size_t s = (size_t)blockIdx.x * BLOCK + threadIdx.x; s < nscalar; s += (size_t)gridDim.x * BLOCK) {
-            const size_t e = s < head ? s : body_end + (s - head);
-            io[e] = Fn<OP>::apply(io[e], in[e]);
-        }
     }
 }
 
@@ -389,7 +177,6 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
     const int sg = (int)(blockIdx.x % n);
     const size_t gx = gridDim.x / n;
     const size_t bx = n == 1 ? (size_t)xcd_tile(blockIdx.x, gridDim.x) : (size_t)(blockIdx.x / n);
-    if (c.sys) acquire_system();
     const char* src = static_cast<const char*>(c.src[sg]);
     char* dst = static_cast<char*>(c.dst[sg]);
     const size_t nb = c.nbytes[sg];
@@ -404,7 +191,6 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
         done = nv * 16;
     }
     for (size_t i = done + bx * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
-    if (c.sys) release_system();
 }
 
 // One local copy far above the 256 MiB Infinity Cache (DRAM-bound): the
@@ -417,39 +203,19 @@ __global__ __launch_bounds__(64) void k_copy_dram(const u32x4* __restrict__ s, u
     if (i < nv) d[i] = ld<true>(s + i);
 }
 
-// The small-allreduce push with its arrival flags in one launch: every
-// workgroup copies its part of its segment with system-coherent stores
-// (sc0 sc1: written through to the owner's memory, never left dirty in this
-// GPU's L2, however the importer maps the peer window).  EVERY lane then
-// waits until its own write-through stores have completed at the owner
-// (stores_done: s_waitcnt vmcnt(0), without the L2 writeback an agent-scope
-// fence adds), the workgroup meets at a barrier, and thread 0 counts the
-// workgroup done; the last one posts `seq` into every peer's flag slot with a
-// system-scope release (the threadFenceReduction pattern: every workgroup's
-// data completed before its count, so no flag can overtake any of it).  sys: cached windows, each lane writes
-// its L2 back at system scope instead.
-// `counter` belongs to the calling transport (one per communicator, reset by
-// the last workgroup); the transport's collectives are issued one at a time
-// on its stream, so two launches never share it concurrently.
-__global__ __launch_bounds__(256) void k_push_post(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
-                                                   int sys)
-{
-    push_post_body(c, f, counter, total, sys, blockIdx.x, gridDim.x, blockIdx.y);
-}
-
-// The two-step allreduce's synchronisation points: workgroups [0, total) push
-// (copy_post_body, segment b % n), the last workgroup alone waits for the
-// peers' flags -- one spinning workgroup per rank, so ranks that share a GPU
-// never starve each other's pushes -- and the stream's next launches read
-// what the flags announce.
+// The synchronisation point of every GPU-flag schedule: workgroups [0, total)
+// push (copy_post_body, segment b % n: every peer link starts at once), the
+// last workgroup alone waits for the peers' flags -- one spinning workgroup
+// per rank, so ranks that share a GPU never starve each other's pushes -- and
+// the stream's next launches read what the flags announce.
 __global__ __launch_bounds__(256) void k_push_wait(CopySegs c, PostFlags f, unsigned* counter, unsigned total,
-                                                   int sys, unsigned gx, const unsigned long long* wflags,
+                                                   unsigned gx, const unsigned long long* wflags,
                                                    unsigned long long wseq, int wn, int wskip, int* werr,
                                                    unsigned long long wticks, int wtag)
 {
     const unsigned b = blockIdx.x;
     if (b < total) {
-        copy_post_body(c, f, counter, total, sys, b / (unsigned)c.n, gx, (int)(b % (unsigned)c.n));
+        copy_post_body(c, f, counter, total, b / (unsigned)c.n, gx, (int)(b % (unsigned)c.n));
         return;
     }
     // flags without data (no push workgroups): nothing to order them after,
@@ -471,25 +237,8 @@ using namespace dev;
 constexpr int kBlock = 256;
 constexpr int kUnroll = 1;
 
-template <class T>
-inline void split(const void* in, const void* io, size_t count, size_t& head, size_t& nvec,
-                  size_t& tail)
-{
-    constexpr size_t ES = sizeof(T);
-    const uintptr_t a = (uintptr_t)in, b = (uintptr_t)io;
-    if ((a & 15) != (b & 15) || (a % ES) != 0 || (b % ES) != 0 || (ES == 16 && (a & 15))) {
-        head = count; nvec = 0; tail = 0;   // alignments disagree: all-scalar
-        return;
-    }
-    size_t h = ((16 - (a & 15)) & 15) / ES;
-    if (h > count) h = count;
-    const size_t rest = count - h;
-    const size_t epv = 16 / ES;
-    head = h; nvec = rest / epv; tail = rest - nvec * epv;
-}
-
-// Bytes per operand above which the device combine takes k_combine_dram
-// (MSX_COMBINE_DRAM_MIN overrides): 16 MiB, where the two operands outgrow the
+// Bytes per operand above which the device combine takes k_combine_dram:
+// 16 MiB, where the two operands outgrow the
 // chip's L2 (8 x 4 MiB).  Rounds 1-4 switched only above the 256 MiB Infinity
 // Cache.  fp32 SUM, HIP events, interleaved (scripts/combine_size_sweep.py,
 // profiles/r04/combine_geometry/), XCD-contiguous tiles -> dispatch order,
@@ -506,15 +255,12 @@ size_t combine_dram_min()
 {
     static const size_t v = [] {
         size_t b = (size_t)16 << 20;
-        if (const char* e = getenv("MSX_COMBINE_DRAM_MIN")) b = (size_t)atoll(e);
+        // test hook: 0 runs the DRAM-regime kernel at every size (its parity test)
+        if (const char* e = getenv("MSX_TEST_COMBINE_DRAM_MIN")) b = (size_t)atoll(e);
         return b;
     }();
     return v;
 }
-
-// k_combine_shift's cross-lane move: 0 = DPP wave_shl:1, 1 = ds_bpermute,
-// 2 = DPP with the previous (one-vector-skewed) wave grid
-int g_shift_mode = 0;
 
 // The realigning path (k_combine_shift): both operands element-aligned but
 // at different offsets from 16-byte alignment, and at least 3 vectors.
@@ -542,24 +288,17 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
 {
     size_t head, nvec, tail;
     unsigned sh = 0;
-    if (cfg.grid_cap == 0 && split_shift<T>(in, io, count, head, nvec, tail, sh)) {
+    if (split_shift<T>(in, io, count, head, nvec, tail, sh)) {
         size_t grid = (nvec + BLOCK - 1) / BLOCK;
         const size_t sc = (head + tail + 2 * (16 / sizeof(T)) + BLOCK - 1) / BLOCK;
         if (grid < sc) grid = sc;
         if (grid > 0x7fffffffu) return hipErrorInvalidValue;
-        if (g_shift_mode == 0)
-            hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK, true>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
-                               static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
-        else if (g_shift_mode == 2)
-            hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK, true, true>), dim3((unsigned)grid), dim3(BLOCK), 0,
-                               s, static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
-        else
-            hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK, false>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
-                               static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
+        hipLaunchKernelGGL((k_combine_shift<OP, T, VT, BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
+                           static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail, sh);
         return hipGetLastError();
     }
-    split<T>(in, io, count, head, nvec, tail);
-    if (!cfg.host && cfg.variant == 0 && cfg.grid_cap == 0 && UNROLL == 1 && nvec * 16 > combine_dram_min()) {
+    combine_split<T>(in, io, count, head, nvec, tail);
+    if (!cfg.host && UNROLL == 1 && nvec * 16 > combine_dram_min()) {
         constexpr int DB = 64;
         size_t grid = (nvec + DB - 1) / DB;
         const size_t sc = (head + tail + DB - 1) / DB;
@@ -574,7 +313,6 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
     const size_t sc = (head + tail + BLOCK - 1) / BLOCK;
     if (grid < sc) grid = sc;
     if (grid == 0) return hipSuccess;
-    if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
     if (grid > 0x7fffffffu) grid = 0x7fffffffu;
     if (cfg.host)
         hipLaunchKernelGGL((k_combine_host<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
@@ -584,55 +322,6 @@ hipError_t run_combine(const void* in, void* io, size_t count, hipStream_t s, co
         hipLaunchKernelGGL((k_combine<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>), dim3((unsigned)grid),
                            dim3(BLOCK), 0, s, static_cast<const T*>(in), static_cast<T*>(io), head,
                            nvec, tail);
-    return hipGetLastError();
-}
-
-template <int OP, class T, class VT, int UNROLL, int BLOCK, bool NTLD, bool NTST, int XG = -1>
-hipError_t run_combine_rr(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
-{
-    size_t head, nvec, tail;
-    split<T>(in, io, count, head, nvec, tail);
-    const size_t tile = (size_t)BLOCK * UNROLL;
-    size_t grid = (nvec + tile - 1) / tile;
-    const size_t sc = (head + tail + BLOCK - 1) / BLOCK;
-    if (grid < sc) grid = sc;
-    if (grid == 0) return hipSuccess;
-    if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
-    if (grid > 0x7fffffffu) grid = 0x7fffffffu;
-    hipLaunchKernelGGL((k_combine_rr<OP, T, VT, UNROLL, BLOCK, NTLD, NTST, XG>), dim3((unsigned)grid), dim3(BLOCK), 0,
-                       s, static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail);
-    return hipGetLastError();
-}
-
-template <int OP, class T, class VT, int BLOCK, int KT, bool UNR>
-hipError_t run_combine_kt(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg&)
-{
-    size_t head, nvec, tail;
-    split<T>(in, io, count, head, nvec, tail);
-    const size_t tile = (size_t)BLOCK * KT;
-    size_t grid = (nvec + tile - 1) / tile;
-    const size_t sc = (head + tail + BLOCK - 1) / BLOCK;
-    if (grid < sc) grid = sc;
-    if (grid == 0) return hipSuccess;
-    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_combine_kt<OP, T, VT, BLOCK, KT, UNR>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
-                       static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail);
-    return hipGetLastError();
-}
-
-template <int OP, class T, int BLOCK>
-hipError_t run_combine_lds(const void* in, void* io, size_t count, hipStream_t s, const LaunchCfg& cfg)
-{
-    size_t head, nvec, tail;
-    split<T>(in, io, count, head, nvec, tail);
-    size_t grid = (nvec + BLOCK - 1) / BLOCK;
-    const size_t sc = (head + tail + BLOCK - 1) / BLOCK;
-    if (grid < sc) grid = sc;
-    if (grid == 0) return hipSuccess;
-    if (cfg.grid_cap > 0 && grid > (size_t)cfg.grid_cap) grid = (size_t)cfg.grid_cap;
-    if (grid > 0x7fffffffu) grid = 0x7fffffffu;
-    hipLaunchKernelGGL((k_combine_lds<OP, T, BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
-                       static_cast<const T*>(in), static_cast<T*>(io), head, nvec, tail);
     return hipGetLastError();
 }
 
@@ -653,57 +342,6 @@ hipError_t run_bitwise(const void* in, void* io, size_t nbytes, hipStream_t s, c
 {
     return run_combine<OP, uint8_t, uint32_t, kUnroll, kBlock, true, false>(in, io, nbytes, s, cfg);
 }
-
-// fp32 SUM tuning variants (the benchmark's hot path); index 0 = the default.
-struct Variant {
-    const char* name;
-    hipError_t (*fn)(const void*, void*, size_t, hipStream_t, const LaunchCfg&);
-};
-const Variant kF32SumVariants[] = {
-    {"default", run_combine<O_SUM, float, float, 1, 256, true, false>},
-    {"u1_b128_ntld", run_combine<O_SUM, float, float, 1, 128, true, false>},
-    {"u1_b512_ntld", run_combine<O_SUM, float, float, 1, 512, true, false>},
-    {"u1_b1024_ntld", run_combine<O_SUM, float, float, 1, 1024, true, false>},
-    {"u2_b256_ntld", run_combine<O_SUM, float, float, 2, 256, true, false>},
-    {"u2_b128_ntld", run_combine<O_SUM, float, float, 2, 128, true, false>},
-    {"u4_b256_ntld", run_combine<O_SUM, float, float, 4, 256, true, false>},
-    {"u1_b64_ntld", run_combine<O_SUM, float, float, 1, 64, true, false>},
-    {"u1_b256_ntall", run_combine<O_SUM, float, float, 1, 256, true, true>},
-    {"u1_b256_plain", run_combine<O_SUM, float, float, 1, 256, false, false>},
-    {"u1_b256_lds", run_combine_lds<O_SUM, float, 256>},
-    {"u1_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 256, true, false>},
-    {"u2_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 2, 256, true, false>},
-    {"k2_b256_ntld_seq", run_combine_kt<O_SUM, float, float, 256, 2, false>},
-    {"k4_b256_ntld_seq", run_combine_kt<O_SUM, float, float, 256, 4, false>},
-    {"k2_b256_ntld_unr", run_combine_kt<O_SUM, float, float, 256, 2, true>},
-    {"k4_b256_ntld_unr", run_combine_kt<O_SUM, float, float, 256, 4, true>},
-    {"k2_b128_ntld_unr", run_combine_kt<O_SUM, float, float, 128, 2, true>},
-    // tile-order variants for DRAM-bound sizes (operands far above the 256 MiB
-    // Infinity Cache, scripts/combine_size_sweep.py)
-    {"u1_b256_ntld_xg2", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 2>},
-    {"u1_b256_ntld_xg8", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 8>},
-    {"u1_b256_ntld_xg32", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 32>},
-    {"u1_b256_ntld_xg128", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 128>},
-    {"u1_b256_ntld_xg512", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 512>},
-    {"u1_b64_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 64, true, false, -1>},
-    {"u1_b128_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 128, true, false, -1>},
-    {"u1_b512_ntld_rr", run_combine_rr<O_SUM, float, float, 1, 512, true, false, -1>},
-    {"u1_b256_ntall_rr", run_combine_rr<O_SUM, float, float, 1, 256, true, true, -1>},
-    {"u4_b256_ntld_rr", run_combine_rr<O_SUM, float, float, 4, 256, true, false, -1>},
-    // round 4: around the dispatch-order default (k_combine_dram = u1_b64_ntld_rr)
-    {"u2_b64_ntld_rr", run_combine_rr<O_SUM, float, float, 2, 64, true, false, -1>},
-    {"u1_b64_ntall_rr", run_combine_rr<O_SUM, float, float, 1, 64, true, true, -1>},
-    {"u1_b64_plain_rr", run_combine_rr<O_SUM, float, float, 1, 64, false, false, -1>},
-    // rounds 1-4's default below 256 MiB: XCD-contiguous 256-thread tiles
-    {"u1_b256_ntld_tiles", run_combine_rr<O_SUM, float, float, 1, 256, true, false, 0>},
-    // the default kernel's exact body above 16 MiB per operand (k_combine_dram:
-    // one-wave workgroups in dispatch order) under another symbol
-    // (k_combine_rr<..., 64, ..., -2>): bench.py times its single cold-cache
-    // launches with it, so the rocprof statistics of the headline symbol hold
-    // only the back-to-back launches
-    {"default_body_probe", run_combine_rr<O_SUM, float, float, 1, 64, true, false, -2>},
-};
-constexpr int kNumVariants = (int)(sizeof(kF32SumVariants) / sizeof(kF32SumVariants[0]));
 
 template <int OP>
 hipError_t dispatch_arith(Kind k, const void* in, void* io, size_t n, hipStream_t s,
@@ -749,48 +387,12 @@ hipError_t dispatch_loc(Kind k, const void* in, void* io, size_t n, hipStream_t 
 
 }  // namespace
 
-TreeTune g_tree_tune;
-
-size_t tree_nt_min()
-{
-    static const size_t v = [] {
-        size_t b = (size_t)256 << 20;        // the Infinity Cache (MALL) of one MI355X
-        if (const char* e = getenv("MSX_TREE_NT_MIN")) b = (size_t)atoll(e);
-        return b;
-    }();
-    return v;
-}
-
-int shift_tune_set(int mode)
-{
-    if (mode < 0 || mode > 2) return -1;
-    g_shift_mode = mode;
-    return 0;
-}
-
-int tree_tune_set(int mode, int grid_cap)
-{
-    if (mode < 0 || mode > 17 || grid_cap < 0) return -1;
-    g_tree_tune.mode = mode;
-    g_tree_tune.grid_cap = grid_cap;
-    return 0;
-}
-
-int combine_variant_count() { return kNumVariants; }
-const char* combine_variant_name(int v)
-{
-    return (v >= 0 && v < kNumVariants) ? kF32SumVariants[v].name : nullptr;
-}
-
 hipError_t launch_combine(int opidx, Kind k, const void* in, void* io, size_t n, hipStream_t s,
                           const LaunchCfg& c)
 {
     if (n == 0) return hipSuccess;
     switch (opidx) {
-    case O_SUM:
-        if (k == K_F32 && c.variant > 0 && c.variant < kNumVariants && !c.host)
-            return kF32SumVariants[c.variant].fn(in, io, n, s, c);
-        return dispatch_arith<O_SUM>(k, in, io, n, s, c);
+    case O_SUM:  return dispatch_arith<O_SUM>(k, in, io, n, s, c);
     case O_MAX:  return dispatch_arith<O_MAX>(k, in, io, n, s, c);
     case O_MIN:  return dispatch_arith<O_MIN>(k, in, io, n, s, c);
     case O_PROD: return dispatch_arith<O_PROD>(k, in, io, n, s, c);
@@ -817,40 +419,6 @@ hipError_t launch_tree(int opidx, Kind k, const void* const* srcs, int p, void* 
     t.chain = false;
     for (int i = 0; i < p; ++i) t.src[2 * i] = srcs[i];
     return launch_tree_spec(opidx, k, t, out, n, s);
-}
-
-// Write-through stores (st_wt) for data that GPU flags announce to peers:
-// the two-step pushes (k_push_wait) and tree results behind result-ready
-// flags.  MSX_WT_STORES=0 keeps plain stores (correct only while the peer
-// windows are mapped uncached on the writer).
-// Workgroup-level agent release before each completion count of a
-// flag-announced push / tree (wg_release, msx_tree_dev.h), MSX_WG_RELEASE=1.
-// Off by default: the pushed and result bytes are written through at system
-// scope (sc0 sc1) and every lane waits for their completion before its
-// workgroup counts itself -- the guide's valid write-through producer form --
-// and the per-workgroup buffer_wbl2 costs 5.7x at 64 MiB (2 ranks on one
-// MI355X, 2-step allreduce 123-131 -> 746-747 us; 4 KiB and 1 MiB within
-// noise; scripts/wg_release_ab.sh, profiles/r04/wg_release_ab.log).
-static bool wg_release_on()
-{
-    static const bool on = [] {
-        const char* e = getenv("MSX_WG_RELEASE");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
-// the `sys` word of push_post_body / copy_post_body: 1 = system fences (cached
-// windows), 2 = workgroup release, 0 = store completion only
-static int post_mode(bool sys) { return sys ? 1 : (wg_release_on() ? 2 : 0); }
-
-static bool wt_stores()
-{
-    static const bool on = [] {
-        const char* e = getenv("MSX_WT_STORES");
-        return !e || atoi(e) != 0;
-    }();
-    return on;
 }
 
 hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, size_t n, hipStream_t s)
@@ -884,55 +452,22 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     a.nleaves = (t.nleaves > 0 && t.nleaves <= t.P) ? t.nleaves : t.P;
     a.pairmask = t.pairmask;
     a.chain = t.chain ? 1 : 0;
-    a.sys = t.sys ? 1 : 0;
-    a.wait_flags = t.wait_flags;
-    a.wait_seq = t.wait_seq;
-    a.wait_n = t.wait_n;
-    a.wait_skip = t.wait_skip;
-    a.wait_err = t.wait_err;
-    a.wait_ticks = flag_wait_ticks();
-    a.wait_tag = t.wait_tag;
-    if (t.wait_flags && (!t.wait_err || t.wait_n < 0)) return hipErrorInvalidValue;
-    if (t.push_nseg > 0) {
-        if (t.push_nseg > kMaxSegs || t.push_nflags < 0 || t.push_nflags > 64 || !t.push_counter)
-            return hipErrorInvalidValue;
-        size_t maxb = 0;
-        a.push.n = t.push_nseg;
-        for (int i = 0; i < t.push_nseg; ++i) {
-            a.push.src[i] = t.push_src[i];
-            a.push.dst[i] = t.push_dst[i];
-            a.push.nbytes[i] = t.push_n[i];
-            if (t.push_n[i] > maxb) maxb = t.push_n[i];
-        }
-        a.flags.n = t.push_nflags;
-        a.flags.seq = t.push_seq;
-        for (int i = 0; i < t.push_nflags; ++i) a.flags.dst[i] = t.push_flags[i];
-        if (maxb >= ((size_t)1 << 32)) return hipErrorInvalidValue;   // 32-bit write-through offsets
-        size_t gx = (maxb / 16 + 255) / 256;          // as launch_push_post
-        if (gx < 1) gx = 1;
-        if (gx > 16) gx = 16;
-        a.push_gx = (unsigned)gx;
-        a.npush = (unsigned)(gx * (size_t)t.push_nseg);
-        a.push_counter = t.push_counter;
-        a.push_sys = post_mode(t.push_sys);
-    }
     if (t.done_counter) {
         if (t.done_nflags < 0 || t.done_nflags > 64 || t.done_launches < 1) return hipErrorInvalidValue;
         a.done_counter = t.done_counter;
-        a.rel = wg_release_on() ? 1 : 0;
-        // buffer-store offsets are 32-bit: larger ranges keep plain stores
-        a.wt = (wt_stores() && n * kind_size(k) < ((size_t)1 << 32)) ? 1 : 0;
+        // results that result-ready flags announce to peers: write-through
+        // stores (buffer-store offsets are 32-bit: larger ranges keep plain
+        // stores; the two-step chunks stay far below 4 GiB)
+        a.wt = n * kind_size(k) < ((size_t)1 << 32) ? 1 : 0;
         a.done_launches = t.done_launches;
         a.done_flags.n = t.done_nflags;
         a.done_flags.seq = t.done_seq;
         for (int i = 0; i < t.done_nflags; ++i) a.done_flags.dst[i] = t.done_flags[i];
     }
-    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.wait_flags && !t.push_nseg &&
-        !t.done_counter) {
+    if (!t.chain && t.P == 1 && t.pairmask == 0 && t.nextra == 0 && !t.done_counter) {
         if (t.src[0] == out) return hipSuccess;
         return hipMemcpyAsync(out, t.src[0], n * kind_size(k), hipMemcpyDeviceToDevice, s);   // xfer: device/pinned
     }
-    if (opidx == O_SUM && k == K_F32 && g_tree_tune.mode != 0) return tree_tune_f32_sum(g_tree_tune.mode, a, ns, out, n, s);
     switch (opidx) {
     case O_SUM:    return tree_dispatch<O_SUM>(k, a, ns, out, n, s);
     case O_MAX:    return tree_dispatch<O_MAX>(k, a, ns, out, n, s);
@@ -950,58 +485,6 @@ hipError_t launch_tree_spec(int opidx, Kind k, const TreeSpec& t, void* out, siz
     }
 }
 
-hipError_t launch_probe(int mode, const void* a, void* b, size_t bytes, hipStream_t s)
-{
-    if ((((uintptr_t)a | (uintptr_t)b) & 15) || mode < 0 || mode > 9) return hipErrorInvalidValue;
-    if (mode == 4) return launch_copy_segs(&a, &b, &bytes, 1, false, s);      // the engine's copy kernel
-    if (mode == 8 || mode == 9) return launch_copy_one(a, b, bytes, s, mode == 8 ? 0 : 1);   // forced geometry
-    if (mode == 5) return hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, s);   // HIP's blit; xfer: device/pinned
-    // modes 6 / 7 touch every other 16-B vector of `bytes`: nvec = bytes / 32
-    const size_t nvec = (mode >= 6) ? bytes / 32 : bytes / 16;
-    const size_t grid = (nvec + 255) / 256;
-    if (grid == 0) return hipSuccess;
-    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
-    const u32x4* va = static_cast<const u32x4*>(a);
-    u32x4* vb = static_cast<u32x4*>(b);
-    const unsigned key = 0x9E3779B9u;
-    switch (mode) {
-    case 0: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
-    case 1: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
-    case 2: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
-    case 6: hipLaunchKernelGGL(k_probe<6>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
-    case 7: hipLaunchKernelGGL(k_probe<7>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
-    default: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)grid), dim3(256), 0, s, va, vb, nvec, key); break;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_push_post(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
-                            unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
-                            unsigned* counter, hipStream_t s)
-{
-    if (!counter || nseg <= 0 || nseg > kMaxSegs || nflags > 64 || nflags < 0) return hipErrorInvalidValue;
-    CopySegs c{};
-    c.n = nseg;
-    size_t maxb = 0;
-    for (int i = 0; i < nseg; ++i) {
-        c.src[i] = src[i];
-        c.dst[i] = dst[i];
-        c.nbytes[i] = nbytes[i];
-        if (nbytes[i] > maxb) maxb = nbytes[i];
-    }
-    if (maxb >= ((size_t)1 << 32)) return hipErrorInvalidValue;   // 32-bit write-through offsets
-    PostFlags f{};
-    for (int i = 0; i < nflags; ++i) f.dst[i] = flags[i];
-    f.n = nflags;
-    f.seq = seq;
-    size_t gx = (maxb / 16 + 255) / 256;
-    if (gx < 1) gx = 1;
-    if (gx > 16) gx = 16;
-    hipLaunchKernelGGL(k_push_post, dim3((unsigned)gx, (unsigned)nseg), dim3(256), 0, s, c, f, counter,
-                       (unsigned)(gx * (size_t)nseg), post_mode(sys));
-    return hipGetLastError();
-}
-
 unsigned long long flag_wait_ticks()
 {
     static const unsigned long long t = [] {
@@ -1016,7 +499,7 @@ unsigned long long flag_wait_ticks()
 double flag_wait_seconds() { return (double)flag_wait_ticks() / 1e8; }
 
 hipError_t launch_push_wait(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
-                            unsigned long long* const* flags, int nflags, unsigned long long seq, bool sys,
+                            unsigned long long* const* flags, int nflags, unsigned long long seq,
                             unsigned* counter, const unsigned long long* wait_flags, int wait_n, int wait_skip,
                             int* wait_err, hipStream_t s, int wait_tag)
 {
@@ -1033,32 +516,23 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
         c.nbytes[i] = nbytes[i];
         if (nbytes[i] > maxb) maxb = nbytes[i];
     }
+    if (maxb >= ((size_t)1 << 32)) return hipErrorInvalidValue;   // 32-bit write-through offsets
     f.n = nflags;
     f.seq = seq;
     for (int i = 0; i < nflags; ++i) f.dst[i] = flags[i];
-    // MSX_PUSH_VECS 16-byte granules per workgroup and pass (default 256:
-    // one per lane) and at most MSX_PUSH_GRID_CAP pushing workgroups in all
-    // (default 65536), the copy kernel's geometry.  Rounds 1-3 used 1024 and
-    // 2048, which measured no different up to 64 MiB (profiles/r02/copy/
-    // push_cmp.log) but 4-7% slower at c3/c4 sizes once the chunks were
-    // pipelined (scripts/push_geometry_ab.sh, profiles/r04/pushab/).
-    static const size_t per_wg = [] {
-        const char* e = getenv("MSX_PUSH_VECS");
-        const long long v = e ? atoll(e) : 256;
-        return v >= 256 ? (size_t)v : (size_t)256;
-    }();
-    static const size_t grid_cap = [] {
-        const char* e = getenv("MSX_PUSH_GRID_CAP");
-        const long long v = e ? atoll(e) : 65536;
-        return v >= 1 ? (size_t)v : (size_t)65536;
-    }();
-    size_t gx = (maxb / 16 + per_wg - 1) / per_wg;
-    const size_t cap = nseg > 0 ? std::max<size_t>(1, grid_cap / (size_t)nseg) : 1;
+    // One 16-byte granule per lane and pass, at most kPushGridCap pushing
+    // workgroups in all: the copy kernel's geometry.  Rounds 1-3 used four
+    // granules per lane and 2048 workgroups, which measured the same up to
+    // 64 MiB (profiles/r02/copy/push_cmp.log) but 4-7 % slower at c3/c4 sizes
+    // once the chunks were pipelined (scripts/push_geometry_ab.sh in round 4,
+    // profiles/r04/pushab/).
+    constexpr size_t kPushGridCap = 65536;
+    size_t gx = (maxb / 16 + 255) / 256;
+    const size_t cap = nseg > 0 ? std::max<size_t>(1, kPushGridCap / (size_t)nseg) : 1;
     if (gx < 1) gx = 1;
     if (gx > cap) gx = cap;
     const unsigned total = nseg > 0 ? (unsigned)(gx * (size_t)nseg) : 0u;
-    c.wt = (wt_stores() && maxb < ((size_t)1 << 32)) ? 1 : 0;   // 32-bit buffer offsets
-    hipLaunchKernelGGL(k_push_wait, dim3(total + 1), dim3(256), 0, s, c, f, counter, total, post_mode(sys),
+    hipLaunchKernelGGL(k_push_wait, dim3(total + 1), dim3(256), 0, s, c, f, counter, total,
                        (unsigned)gx, wait_flags, seq, wait_n, wait_skip, wait_err, flag_wait_ticks(), wait_tag);
     return hipGetLastError();
 }
@@ -1075,58 +549,28 @@ hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned lon
     return hipGetLastError();
 }
 
-// Bytes of one local copy above which it takes k_copy_dram (MSX_COPY_DRAM_MIN):
-// 16 MiB, as the combine (combine_dram_min).  Rounds 1-4 switched above
+// Bytes of one local copy above which it takes k_copy_dram: 16 MiB, as the
+// combine (combine_dram_min).  Rounds 1-4 switched above
 // 256 MiB.  HIP events, interleaved (scripts/copy_geometry_probe.py,
 // profiles/r04/combine_geometry/copy.json), tiles -> dispatch order, GB/s back
 // to back / cache flushed: 16 MiB 4637 -> 4284 / 3277 -> 3452 (tiles stay),
 // 32 MiB 4981 -> 5384 / 4153 -> 4427, 64 MiB 5696 -> 6025 / 4706 -> 5335,
 // 128 MiB 6475 -> 6822 / 5247 -> 5780, 256 MiB 7150 -> 7259 / 5836 -> 6237.
-size_t copy_dram_min()
-{
-    static const size_t v = [] {
-        size_t b = (size_t)16 << 20;
-        if (const char* e = getenv("MSX_COPY_DRAM_MIN")) b = (size_t)atoll(e);
-        return b;
-    }();
-    return v;
-}
-
-// One aligned local copy in a forced geometry (probe modes 8 / 9): 0 =
-// k_copy_segs' XCD-contiguous 4-KiB tiles, 1 = k_copy_dram.
-hipError_t launch_copy_one(const void* src, void* dst, size_t nbytes, hipStream_t s, int dram)
-{
-    if ((((uintptr_t)src | (uintptr_t)dst | nbytes) & 15) != 0) return hipErrorInvalidValue;
-    const size_t nv = nbytes / 16;
-    if (nv == 0) return hipSuccess;
-    if (dram) {
-        const size_t grid = (nv + 63) / 64;
-        if (grid > 0x7fffffffu) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_copy_dram, dim3((unsigned)grid), dim3(64), 0, s, static_cast<const u32x4*>(src),
-                           static_cast<u32x4*>(dst), nv);
-        return hipGetLastError();
-    }
-    CopySegs c{};
-    c.n = 1;
-    c.src[0] = src;
-    c.dst[0] = dst;
-    c.nbytes[0] = nbytes;
-    const size_t gx = (nv + 255) / 256;
-    if (gx > 0x7fffffffu) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_copy_segs, dim3((unsigned)gx), dim3(256), 0, s, c);
-    return hipGetLastError();
-}
+constexpr size_t kCopyDramMin = (size_t)16 << 20;
 
 hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size_t* nbytes, int nseg,
-                            bool sys, hipStream_t s)
+                            hipStream_t s)
 {
     // one local copy in the DRAM regime (the collect of a 512 MiB chunk)
-    if (nseg == 1 && !sys && nbytes[0] > copy_dram_min() &&
-        ((((uintptr_t)src[0] | (uintptr_t)dst[0] | nbytes[0]) & 15) == 0))
-        return launch_copy_one(src[0], dst[0], nbytes[0], s, 1);
+    if (nseg == 1 && nbytes[0] > kCopyDramMin && ((((uintptr_t)src[0] | (uintptr_t)dst[0] | nbytes[0]) & 15) == 0)) {
+        const size_t nv = nbytes[0] / 16, grid = (nv + 63) / 64;
+        if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_copy_dram, dim3((unsigned)grid), dim3(64), 0, s, static_cast<const u32x4*>(src[0]),
+                           static_cast<u32x4*>(dst[0]), nv);
+        return hipGetLastError();
+    }
     for (int base = 0; base < nseg; base += kMaxSegs) {
         CopySegs c{};
-        c.sys = sys ? 1 : 0;
         c.n = (nseg - base < kMaxSegs) ? nseg - base : kMaxSegs;
         size_t maxb = 0;
         for (int i = 0; i < c.n; ++i) {
@@ -1136,13 +580,8 @@ hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size
             if (c.nbytes[i] > maxb) maxb = c.nbytes[i];
         }
         if (maxb == 0) continue;
-        // one 4-KiB tile per workgroup, grid-stride beyond MSX_COPY_GRID_CAP
-        // workgroups in all
-        static const size_t cap = [] {
-            const char* e = getenv("MSX_COPY_GRID_CAP");
-            const long long v = e ? atoll(e) : 0;
-            return v > 0 ? (size_t)v : ((size_t)1 << 22);
-        }();
+        // one 4-KiB tile per workgroup, grid-stride beyond 2^22 workgroups in all
+        constexpr size_t cap = (size_t)1 << 22;
         size_t gx = (maxb / 16 + 255) / 256;
         if (gx < 1) gx = 1;
         size_t gmax = cap / (size_t)c.n;

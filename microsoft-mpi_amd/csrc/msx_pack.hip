@@ -336,31 +336,16 @@ constexpr int64_t kRunParallelMin = 8;
 // grid-stride form, 2 = always the tile form.
 int g_pack_mode = 0;
 
-size_t pack_tile_min()
-{
-    static const size_t v = [] {
-        size_t b = (size_t)512 << 20;
-        if (const char* e = getenv("MSX_PACK_TILE_MIN")) b = (size_t)atoll(e);
-        return b;
-    }();
-    return v;
-}
+constexpr size_t kPackTileMin = (size_t)512 << 20;
+size_t pack_tile_min() { return kPackTileMin; }
 
-// Bytes (typed span + packed) of one derived-target accumulate above which it
-// runs k_dt_acc_tile (MSX_ACC_TILE_MIN, default 0: always).  Self-targeted
+// A derived-target accumulate always runs k_dt_acc_tile (the grid-stride
+// k_dt_acc only under msx_tune_pack 1, or beyond 2^31 tiles).  Self-targeted
 // fp32 SUM MPI_Accumulate through a 16-B-block vector target type, grid-stride
 // -> tile form, three interleaved rounds (scripts/acc_probe.py,
 // profiles/r03/acc_geometry/): 256 MiB window 144 -> 140 us per call, 1 GiB
 // 663 -> 521 us.
-size_t acc_tile_min()
-{
-    static const size_t v = [] {
-        size_t b = (size_t)0;
-        if (const char* e = getenv("MSX_ACC_TILE_MIN")) b = (size_t)atoll(e);
-        return b;
-    }();
-    return v;
-}
+size_t acc_tile_min() { return 0; }
 
 int pack_tune_set(int mode)
 {

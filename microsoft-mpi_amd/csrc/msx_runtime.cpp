@@ -181,8 +181,6 @@ int hip_fail(hipError_t e, const char* what)
     return MPI_ERR_OTHER;
 }
 
-LaunchCfg& launch_cfg() { return g_cfg; }
-
 int device_count_noinit()
 {
     int n = 0;
@@ -356,12 +354,12 @@ private:
 };
 
 // Smallest call (bytes per operand) worth pinning; below it the staged copies
-// are cheaper than two register/unregister round trips.  MSX_HOST_PIN_MIN.
+// are cheaper than two register/unregister round trips.  MSX_TEST_HOST_PIN_MIN.
 size_t pin_min_bytes()
 {
     static const size_t v = [] {
         size_t m = (size_t)1 << 20;
-        if (const char* e = getenv("MSX_HOST_PIN_MIN")) m = (size_t)atoll(e);
+        if (const char* e = getenv("MSX_TEST_HOST_PIN_MIN")) m = (size_t)atoll(e);
         return m;
     }();
     return v;
@@ -446,7 +444,7 @@ size_t bounce_max_bytes()
 {
     static const size_t v = [] {
         size_t m = (size_t)256 << 10;
-        if (const char* e = getenv("MSX_HOST_BOUNCE_MAX")) m = (size_t)atoll(e);
+        if (const char* e = getenv("MSX_TEST_HOST_BOUNCE_MAX")) m = (size_t)atoll(e);
         return m;
     }();
     return v;
@@ -745,10 +743,10 @@ int reduce_local_multi(int opidx, Kind k, const void* in, void* inout, size_t co
     if (rc != MPI_SUCCESS) return rc;
     const int nvis = device_count_noinit();
     int g = ngpus <= 0 || ngpus > nvis ? nvis : ngpus;
-    // MSX_MULTI_SPLIT_TEST=1 (tests only): keep ngpus ranges (up to 16) even
+    // MSX_TEST_MULTI_SPLIT=1 (tests only): keep ngpus ranges (up to 16) even
     // with fewer GPUs, range d on device d % nvis, so a one-GPU box runs the
     // pinning, aliasing and range logic of the k-GPU split
-    if (nvis >= 1 && ngpus > nvis && getenv("MSX_MULTI_SPLIT_TEST") && atoi(getenv("MSX_MULTI_SPLIT_TEST")) == 1)
+    if (nvis >= 1 && ngpus > nvis && getenv("MSX_TEST_MULTI_SPLIT") && atoi(getenv("MSX_TEST_MULTI_SPLIT")) == 1)
         g = std::min(ngpus, 16);
     auto dev_of = [nvis](int d) { return d % nvis; };
     BufInfo bi = classify(in), bo = classify(inout);

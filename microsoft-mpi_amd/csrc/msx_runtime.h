@@ -83,19 +83,18 @@ struct Bounce {
     bool get(size_t bytes);  // false: allocation failed (use another path)
 };
 // Host operands up to this many bytes go through a bounce buffer
-// (MSX_HOST_BOUNCE_MAX, default 256 KiB; 0 disables it).
+// (256 KiB; the test hook MSX_TEST_HOST_BOUNCE_MAX=0 disables it).
 size_t bounce_max_bytes();
 
 // Operands a (na bytes) and b (nb bytes; b may be a, or null): pinned host
 // memory is used through its mapped alias; with pin_pageable, pageable memory
-// of at least MSX_HOST_PIN_MIN bytes (default 1 MiB) is pinned for the hold's
+// of at least 1 MiB (test hook: MSX_TEST_HOST_PIN_MIN) is pinned for the hold's
 // lifetime (one pin when the operands share pages).  Each operand aliased this
 // way becomes {Place::Device, alias, pinned_host}.  Returns true when no
 // operand is left in host memory.
 bool alias_host_operands(PinHold& hold, bool pin_pageable, const void* a, size_t na, BufInfo* ia, const void* b,
                          size_t nb, BufInfo* ib);
 
-LaunchCfg& launch_cfg();
 void set_staging_chunk(size_t bytes);
 // host operands: 0 = pinned memory combined in place by the kernel (zero-copy),
 // pageable memory pinned for the call and combined the same way; 1 = every

@@ -360,7 +360,7 @@ public:
         if (rc != MPI_SUCCESS) return rc;
         double t = 600.0;
         if (const char* v = getenv("MSX_BOOTSTRAP_TIMEOUT")) t = atof(v);
-        if (!getenv("MSX_NO_SHM_BARRIER")) (void)shm_.init(hub_, r, s, t);
+        (void)shm_.init(hub_, r, s, t);   // without it: the hub's barriers, no GPU-flag schedules
         // ranks that share a GPU (an unknown bus id shares nothing)
         char bus[32] = {0};
         int dev = -1;
@@ -485,10 +485,15 @@ public:
             size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
             // Uncached device memory: peers write it over xGMI, which does not
             // snoop this GPU's L2, so no reader (kernel, blit or DMA) may hold a
-            // stale line of it.  MSX_WINDOW_CACHED=1 selects plain hipMalloc.
-            const bool cached = getenv("MSX_WINDOW_CACHED") && atoi(getenv("MSX_WINDOW_CACHED"));
-            hipError_t e = cached ? hipMalloc(&win_, want) : hipExtMallocWithFlags(&win_, want, hipDeviceMallocUncached);
-            trace("window: %zu bytes %s rc=%d", want, cached ? "cached" : "uncached", (int)e);
+            // stale line of it.  The kernel driver maps such a buffer MTYPE_UC
+            // on the owner and on every peer that imports it, so neither the
+            // writer's nor the reader's L2 ever holds a line of it, and the
+            // engine's kernels need no per-workgroup system fences (each one
+            // writes back or invalidates a whole XCD L2; rounds 1-2 had them and
+            // they halved the collectives' throughput: p = 2 reduce_scatter
+            // 4.17 -> 2.17 ms, allreduce 64 MiB 511 -> 178 us without).
+            hipError_t e = hipExtMallocWithFlags(&win_, want, hipDeviceMallocUncached);
+            trace("window: %zu bytes uncached rc=%d", want, (int)e);
             if (e != hipSuccess) return hip_fail(e, "window allocation");
             // zeroed before any peer can map it (map_peers below is collective):
             // the arrival flags behind the data areas must start at 0
@@ -532,8 +537,7 @@ public:
             for (uint64_t v : all) lo = std::min(lo, v);
             const size_t bytes = (size_t)lo;
             trace("rma window: %d rank(s) on this GPU, %zu bytes here, %zu agreed", share, (size_t)mine, bytes);
-            const bool cached = getenv("MSX_WINDOW_CACHED") && atoi(getenv("MSX_WINDOW_CACHED"));
-            hipError_t e = cached ? hipMalloc(&rwin_, bytes) : hipExtMallocWithFlags(&rwin_, bytes, hipDeviceMallocUncached);
+            hipError_t e = hipExtMallocWithFlags(&rwin_, bytes, hipDeviceMallocUncached);
             trace("rma window: %zu bytes rc=%d", bytes, (int)e);
             if (e != hipSuccess) {
                 rwin_ = nullptr;
@@ -653,10 +657,6 @@ int transport_create(int rank, int size, Transport** out)
 void transport_destroy(Transport* t)
 {
     if (!t) return;
-    for (int i = 0; i < 2; ++i) {
-        if (t->pipe_tree[i]) (void)hipEventDestroy(t->pipe_tree[i]);
-        if (t->pipe_copy[i]) (void)hipEventDestroy(t->pipe_copy[i]);
-    }
     if (t->aux) (void)hipStreamDestroy(t->aux);
     delete t;
 }
@@ -1001,13 +1001,13 @@ int flag_timeout(const char* op, int me, int word, unsigned long long seq, bool 
     return MPI_ERR_OTHER;
 }
 
-// Fault injection for the timeout diagnostics (tests only):
-// MSX_FAULT_DROP_FLAGS=<rank>:<seq> -- that rank does not post its arrival
+// Fault injection for the timeout diagnostics (test hook):
+// MSX_TEST_DROP_FLAGS=<rank>:<seq> -- that rank does not post its arrival
 // flags of flag-synchronised call <seq>, so its peers' waits run out.
 bool fault_drop_flags(int me, unsigned long long seq)
 {
     static const std::pair<int, unsigned long long> f = [] {
-        const char* e = getenv("MSX_FAULT_DROP_FLAGS");
+        const char* e = getenv("MSX_TEST_DROP_FLAGS");
         int r = -1;
         unsigned long long q = 0;
         if (e && sscanf(e, "%d:%llu", &r, &q) != 2) r = -1;
@@ -1025,42 +1025,9 @@ int sync_stream(hipStream_t s, const char* what)
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
 }
 
-// Per-workgroup system-scope acquire/release in the engine's kernels (k_tree,
-// k_copy_segs).  Every byte that crosses GPUs lands in a window, and windows
-// are UNCACHED allocations: the kernel driver maps such a buffer MTYPE_UC on
-// the owner and on every peer that imports it, so neither the writer's nor
-// the reader's L2 ever holds a line of it, and the end-of-kernel store
-// completion (awaited by hipStreamSynchronize before the host barrier) is all
-// the ordering a reader behind that barrier needs.  The fences only matter for
-// cached windows (MSX_WINDOW_CACHED=1), and there they are kept.  They are not
-// free: each one writes back / invalidates the whole XCD L2 once per
-// workgroup, which halved the collectives' throughput (p = 2 rehearsal:
-// reduce_scatter 4.17 -> 2.17 ms, allreduce 64 MiB 511 -> 178 us).
-// MSX_KERNEL_SYS_FENCE=0/1 overrides the choice.
-bool sys_fences()
-{
-    static const bool on = [] {
-        if (const char* e = getenv("MSX_KERNEL_SYS_FENCE")) return atoi(e) != 0;
-        const char* c = getenv("MSX_WINDOW_CACHED");
-        return c && atoi(c) != 0;
-    }();
-    return on;
-}
-
 // Evaluate RankTree `t` over [start, start+len) elements of the per-rank
 // source pointers `srcs` into `out`.
 struct TreeWait {
-    const unsigned long long* flags = nullptr;   // my window's arrival flags
-    unsigned long long seq = 0;
-    int n = 0, skip = -1;
-    int* err = nullptr;                          // device view of a pinned host word
-    // fused push (TreeSpec::push_*): this rank's contribution to the peers and
-    // its arrival flags, done by the first workgroups of the same launch
-    const std::vector<const void*>* push_src = nullptr;
-    const std::vector<void*>* push_dst = nullptr;
-    const std::vector<size_t>* push_n = nullptr;
-    const std::vector<unsigned long long*>* push_flags = nullptr;
-    unsigned* push_counter = nullptr;
     // result-ready flags after the last of `done_launches` launches
     // (TreeSpec::done_*); done_counter: block 2 of push_counter()
     unsigned* done_counter = nullptr;
@@ -1076,26 +1043,6 @@ int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>
     if (len == 0) return MPI_SUCCESS;
     TreeSpec spec;
     if (wait) {
-        spec.wait_flags = wait->flags;
-        spec.wait_seq = wait->seq;
-        spec.wait_n = wait->n;
-        spec.wait_skip = wait->skip;
-        spec.wait_err = wait->err;
-        if (wait->push_src && !wait->push_src->empty()) {
-            const size_t ns = wait->push_src->size(), nf = wait->push_flags->size();
-            if (ns > 32 || nf > 64) { set_error("fused push: too many peers"); return MPI_ERR_INTERN; }
-            spec.push_nseg = (int)ns;
-            for (size_t i = 0; i < ns; ++i) {
-                spec.push_src[i] = (*wait->push_src)[i];
-                spec.push_dst[i] = (*wait->push_dst)[i];
-                spec.push_n[i] = (*wait->push_n)[i];
-            }
-            spec.push_nflags = (int)nf;
-            for (size_t i = 0; i < nf; ++i) spec.push_flags[i] = (*wait->push_flags)[i];
-            spec.push_seq = wait->seq;
-            spec.push_counter = wait->push_counter;
-            spec.push_sys = sys_fences();
-        }
         if (wait->done_counter) {
             const size_t nf = wait->done_flags ? wait->done_flags->size() : 0;
             if (nf > 64) { set_error("result flags: too many peers"); return MPI_ERR_INTERN; }
@@ -1113,7 +1060,6 @@ int run_rank_tree(int opidx, Kind k, const RankTree& t, const std::vector<char*>
     spec.nleaves = t.nleaves;
     spec.pairmask = t.pairmask;
     spec.chain = t.chain;
-    spec.sys = sys_fences();
     const int nslots = t.chain ? t.P : 2 * (t.nleaves ? t.nleaves : t.P);
     for (int i = 0; i < nslots; ++i)
         spec.src[i] = t.src[i] >= 0 ? srcs[(size_t)t.src[i]] + start * esz : nullptr;
@@ -1421,43 +1367,6 @@ Bounce& engine_bounce(int i)
     return b[i];
 }
 
-// Whether the tree workgroups of a small flag-synchronised call may spin on
-// the peers' flags themselves (MSX_SPIN_TREE=1, the round-2 design: push and
-// tree in one launch).  Default off: ONE workgroup of the push launch waits
-// (k_push_wait) and the tree follows in stream order, so no call ever parks a
-// grid of spinning workgroups on the GPU whose progress depends on another
-// process's kernel being scheduled.
-bool spin_tree_allowed()
-{
-    static const bool on = [] {
-        const char* e = getenv("MSX_SPIN_TREE");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
-// The barrier-free small allreduce pushes and reduces in one launch
-// (MSX_FUSED_PUSH=0: a separate push launch first).
-bool fused_push()
-{
-    static const bool on = [] {
-        const char* e = getenv("MSX_FUSED_PUSH");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
-// The barrier-free small allreduce synchronises on GPU arrival flags
-// (MSX_RD_FLAGS=0: host barrier instead).
-bool rd_flags()
-{
-    static const bool on = [] {
-        const char* e = getenv("MSX_RD_FLAGS");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 // Pinned host word the arrival wait reports a timeout through (engine worker
 // only); returns its device view.
 int* wait_err_word(int** host)
@@ -1501,23 +1410,16 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
     return rc;
 }
 
-// Copies of at least MSX_KERNEL_COPY_MIN bytes (1 MiB) within this GPU's
-// memory (HBM buffers, its own window; 0 disables) run on the engine's copy
-// kernel: 256 MiB local copies take 68 us there and 99 us as hipMemcpyAsync's
-// blit (scripts/copy_probe.py).  Host memory keeps hipMemcpyAsync (DMA).
-size_t kernel_copy_min()
-{
-    static const size_t v = [] {
-        const char* e = getenv("MSX_KERNEL_COPY_MIN");
-        return e ? (size_t)atoll(e) : ((size_t)1 << 20);
-    }();
-    return v;
-}
+// Copies of at least kKernelCopyMin bytes within this GPU's memory (HBM
+// buffers, its own window) run on the engine's copy kernel: 256 MiB local
+// copies take 68 us there and 99 us as hipMemcpyAsync's blit
+// (scripts/copy_probe.py in round 2).  Host memory keeps hipMemcpyAsync (DMA).
+constexpr size_t kKernelCopyMin = (size_t)1 << 20;
 
 int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
 {
     if (!bytes) return MPI_SUCCESS;
-    if (kernel_copy_min() && bytes >= kernel_copy_min()) {
+    if (bytes >= kKernelCopyMin) {
         const BufInfo bs = classify(src), bd = classify(dst);
         int cur = -1;
         (void)hipGetDevice(&cur);
@@ -1528,7 +1430,7 @@ int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)
             (((uintptr_t)bs.dev | (uintptr_t)bd.dev) & 15) == 0) {
             const void* ps = bs.dev;
             void* pd = bd.dev;
-            hipError_t e = launch_copy_segs(&ps, &pd, &bytes, 1, sys_fences(), s);
+            hipError_t e = launch_copy_segs(&ps, &pd, &bytes, 1, s);
             return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "copy kernel");
         }
     }
@@ -1560,37 +1462,6 @@ hipStream_t aux_stream(Transport* tp)
     return tp->aux;
 }
 
-// Cross-stream hand-offs of the pipelined two-step allreduce (two chunks in
-// flight, so two of each), per communicator: one collective at a time per
-// communicator is MPI's ordering rule, not one per process.
-bool pipe_events(Transport* tp)
-{
-    if (tp->pipe_ok < 0) {
-        bool ok = true;
-        for (int i = 0; i < 2; ++i)
-            ok = ok && hipEventCreateWithFlags(&tp->pipe_tree[i], hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&tp->pipe_copy[i], hipEventDisableTiming) == hipSuccess;
-        if (!ok) (void)hipGetLastError();
-        tp->pipe_ok = ok ? 1 : 0;
-    }
-    return tp->pipe_ok == 1;
-}
-
-// MSX_COLLECT_OVERLAP=1: the pipelined allreduce collects chunk i (result
-// wait + OUT -> recvbuf copy) on the aux stream while the engine stream
-// pushes chunk i + 1.  Off by default: 2 ranks sharing one MI355X, c3 1 GiB,
-// two interleaved rounds (scripts/c3_pipeline_ab.sh, profiles/r04/c3ab/):
-// one stream 1.87-1.96 ms, overlapped 2.18 ms -- the two streams compete for
-// the GPU with the other rank's pushes.  Worth re-measuring one rank per GPU.
-bool collect_overlap()
-{
-    static const bool on = [] {
-        const char* e = getenv("MSX_COLLECT_OVERLAP");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
 // A batch of byte ranges moved by one k_copy_segs launch (one grid row each).
 struct Segs {
     std::vector<const void*> src;
@@ -1606,7 +1477,7 @@ struct Segs {
     int run(hipStream_t s, const char* what)
     {
         if (src.empty()) return MPI_SUCCESS;
-        hipError_t e = launch_copy_segs(src.data(), dst.data(), n.data(), (int)src.size(), sys_fences(), s);
+        hipError_t e = launch_copy_segs(src.data(), dst.data(), n.data(), (int)src.size(), s);
         return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, what);
     }
 };
@@ -2103,7 +1974,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     // reached only after finishing its tree on half P.
     const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
     const bool rd_single = (algo == A_RECURSIVE_DOUBLING || algo == A_BINOMIAL) &&
-                           count * esz <= (Qh & ~(size_t)(16 * esz - 1));
+                           count * esz <= (Qh & ~(size_t)(16 * esz - 1)) && p <= 32 && tp->has_done();
     // Rabenseifner in two GPU-synchronised steps per chunk (see below): a
     // chunk is p pieces of at most half an IN sub-slot each and fits half the
     // OUT area above the recursive-doubling results; a longer message runs as
@@ -2111,7 +1982,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
     // decide, so every rank takes the same branch and the same chunks.
     const size_t out_half = ((chunk_bytes() - Qh) / 2) & ~(size_t)255;
     const size_t pc_el = two_step_chunk_el(p, esz);
-    const bool two_step = algo == A_RABENSEIFNER && p >= 2 && p <= 32 && rd_flags() && tp->has_done() &&
+    const bool two_step = algo == A_RABENSEIFNER && p >= 2 && p <= 32 && tp->has_done() &&
                           count * esz <= two_step_max(tp) && pc_el > 0;
     Windows w;
     if ((rc = get_windows(tp, &w, rd_single || two_step)) != MPI_SUCCESS) return rc;
@@ -2142,12 +2013,16 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         // recursive doubling -> all ranks evaluate their own lineage's tree;
         // binomial reduce -> only the root evaluates
         const RankTree t = (algo == A_BINOMIAL) ? tree_reduce_binomial(p, root) : tree_allreduce(p, lineage);
-        if (rd_single && p <= 32 && rd_flags() && tp->has_done()) {
+        if (rd_single) {
             // No host barrier at all.  Each rank pushes its vector into the IN
             // half of every rank that evaluates a tree (all peers for
             // allreduce, the root for reduce) and posts the call's sequence
-            // number into their flag slots, in one kernel; the tree kernel
-            // waits on the GPU until all peers' flags reached the sequence.
+            // number into their flag slots; ONE workgroup of the same launch
+            // (k_push_wait) waits on the GPU until all peers' flags reached the
+            // sequence, and the tree follows in stream order.  (Rounds 1-2 let
+            // every tree workgroup spin on the flags instead, one launch less;
+            // with a multi-MiB tree spinning, five ranks sharing one GPU starved
+            // each other's pushes until the 20 s bound.)
             // A half is reused two calls later: before pushing call s into
             // rank r's half, this rank waits (host, shared memory) until r has
             // posted that it finished call s-2 -- normally long since true.
@@ -2182,62 +2057,22 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             int* err_dev = wait_err_word(&err_host);
             if (!err_dev) { set_error("allreduce: arrival word allocation failed"); return MPI_ERR_NO_MEM; }
             *err_host = 0;
-            // Data and flags in one kernel (the flag ordered after the data);
-            // a rank that also evaluates a tree does both in ONE launch: the
-            // push workgroups come first in the tree kernel's grid
-            // (MSX_FUSED_PUSH=0: separate k_push_post launch).
-            // Not when the result overwrites the vector being pushed (in place):
-            // the tree workgroups wait only for the PEERS' flags, so they could
-            // store the result while this rank's push still reads its input.
             char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev)
                                                   : (bounce_dst ? engine_bounce(1).dev : w.out(me));
-            const bool disjoint = out + count * esz <= mine || mine + count * esz <= out;
-            // Every workgroup of a waiting tree spins until the peers' flags
-            // arrive.  Up to 256 KiB (the default recursive-doubling range) the
-            // grid is small; a larger vector (switch points moved with
-            // MPICH_DEFAULT_*_MSG) gets the two-step pattern instead: ONE
-            // workgroup of the push launch waits, the tree follows on the
-            // stream -- thousands of spinning workgroups per rank starved the
-            // other ranks' pushes on a shared GPU until the 20 s bound.
-            const bool spin_tree = spin_tree_allowed() && nbytes <= ((size_t)256 << 10);
-            const bool fuse = spin_tree && want && fused_push() && !sg.src.empty() && disjoint;
             unsigned* counter = nullptr;
             if (rc == MPI_SUCCESS && !sg.src.empty()) {
                 counter = tp->push_counter();
                 if (!counter) { set_error("allreduce: push counter allocation failed"); return MPI_ERR_NO_MEM; }
             }
-            if (rc == MPI_SUCCESS && !spin_tree) {
+            if (rc == MPI_SUCCESS) {
                 hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
-                                                fl.data(), (int)fl.size(), seq, sys_fences(),
+                                                fl.data(), (int)fl.size(), seq,
                                                 counter ? counter + kCountWords : nullptr, w.flags(me),
                                                 want ? p : 0, me, err_dev, s);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
-            } else if (rc == MPI_SUCCESS && !sg.src.empty() && !fuse) {
-                hipError_t e = launch_push_post(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
-                                                fl.data(), (int)fl.size(), seq, sys_fences(), counter, s);
-                if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
-            } else if (rc == MPI_SUCCESS && sg.src.empty() && !fl.empty()) {
-                hipError_t e = launch_post_flags(fl.data(), (int)fl.size(), seq, s);   // nothing to push
-                if (e != hipSuccess) rc = hip_fail(e, "allreduce arrival flags");
             }
-            if (rc == MPI_SUCCESS && want && !spin_tree) {
+            if (rc == MPI_SUCCESS && want) {
                 rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s);   // after the wait, in stream order
-                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
-            } else if (rc == MPI_SUCCESS && want) {
-                TreeWait tw;
-                tw.flags = w.flags(me);
-                tw.seq = seq;
-                tw.n = p;
-                tw.skip = me;
-                tw.err = err_dev;
-                if (fuse) {
-                    tw.push_src = &sg.src;
-                    tw.push_dst = &sg.dst;
-                    tw.push_n = &sg.n;
-                    tw.push_flags = &fl;
-                    tw.push_counter = counter;
-                }
-                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s, {}, &tw);
                 if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
             }
             const int rs = sync_stream(s, "allreduce tree");
@@ -2250,29 +2085,6 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             tp->rd_parity ^= 1;
             tp->window_open = true;
             trace("allreduce: done (GPU arrival flags, seq %llu) rc=%d", seq, rc);
-            return rc;
-        }
-        if (rd_single) {
-            const size_t half = (size_t)tp->rd_parity * Qh;
-            for (int r = 0; r < p; ++r) subs[r] = w.sub(me, r) + half;
-            const char* mine = nullptr;
-            rc = device_view(bs, src, 0, count * esz, stage, s, &mine);
-            Segs sg;                      // my own contribution is read in place
-            for (int r = 0; r < p; ++r)
-                if (r != me && (root < 0 || r == root)) sg.add(mine, w.sub(r, me) + half, count * esz);
-            subs[(size_t)me] = const_cast<char*>(mine);
-            if (rc == MPI_SUCCESS) rc = sg.run(s, "allreduce push");
-            if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce push");
-            if (rc == MPI_SUCCESS) rc = tp->barrier();                              // A
-            if (rc == MPI_SUCCESS && want) {
-                char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : w.out(me);
-                rc = run_rank_tree(op.opidx, k, t, subs, esz, 0, count, out, s);
-                if (rc == MPI_SUCCESS && out == w.out(me)) rc = copy_async(dst, out, count * esz, s);
-                if (rc == MPI_SUCCESS) rc = sync_stream(s, "allreduce tree");
-            }
-            tp->rd_parity ^= 1;
-            tp->window_open = true;       // no barrier B (see above)
-            trace("allreduce: done (barrier-free) rc=%d", rc);
             return rc;
         }
         for (size_t o = 0; o < count && rc == MPI_SUCCESS; o += qmax) {
@@ -2336,11 +2148,6 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         const size_t nchunks = (count + pc_el - 1) / pc_el;
         unsigned long long seq = 0;
         size_t nranges = 0;
-        // collect stream: chunk ci's result wait and copy overlap chunk ci+1's
-        // push and trees; events order my own tree before my copy and my copy
-        // of chunk ci before my trees of chunk ci+2 (same OUT half)
-        const bool ovl = want && nchunks > 1 && collect_overlap() && pipe_events(tp) && aux_stream(tp);
-        const hipStream_t sc = ovl ? aux_stream(tp) : s;
         std::vector<TwoStepRange> ranges;
         for (size_t ci = 0; ci < nchunks && rc == MPI_SUCCESS; ++ci) {
             const size_t o = ci * pc_el;
@@ -2358,11 +2165,9 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 for (int r = 0; r < p && rc == MPI_SUCCESS; ++r)
                     if (r != me && seq > 2) rc = tp->wait_done(r, seq - 2);
             } else if (rc == MPI_SUCCESS) {
-                hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, false, nullptr,
+                hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, nullptr,
                                                 w.flags(me) + kDoneFlags, p, me, err_dev, s, 3);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce half-free wait");
-                if (rc == MPI_SUCCESS && sc != s && hipStreamWaitEvent(s, tp->pipe_copy[ci % 2], 0) != hipSuccess)
-                    rc = hip_fail(hipGetLastError(), "allreduce collect event wait");
             }
             if (rc != MPI_SUCCESS) break;
             Segs sg;
@@ -2380,7 +2185,7 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
             // step 1: push my pieces and their arrival flags; one workgroup
             // waits for the peers' pieces of mine (none when my piece is empty)
             hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(), fl.data(),
-                                            (int)fl.size(), seq, sys_fences(), counter + kCountWords, w.flags(me),
+                                            (int)fl.size(), seq, counter + kCountWords, w.flags(me),
                                             ranges.empty() ? 0 : p, me, err_dev, s);
             if (e != hipSuccess) rc = hip_fail(e, "allreduce push");
             // step 2: my piece into every receiver's OUT half; the last
@@ -2403,25 +2208,19 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
                 rc = run_rank_tree(op.opidx, k, t, subs, esz, g.e0 - plo, g.e1 - g.e0,
                                    w.out(dests[0]) + obase + g.e0 * esz, s, extra, &tw);
             }
-            if (rc == MPI_SUCCESS && sc != s) {
-                if (hipEventRecord(tp->pipe_tree[ci % 2], s) != hipSuccess || hipStreamWaitEvent(sc, tp->pipe_tree[ci % 2], 0) != hipSuccess)
-                    rc = hip_fail(hipGetLastError(), "allreduce tree event");
-            }
             if (rc == MPI_SUCCESS && want) {
                 // step 3: every peer's result in my OUT half, then into recvbuf
-                e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq, false, nullptr,
-                                     w.flags(me) + kResultFlags, p, me, err_dev, sc, 2);
+                e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq, nullptr,
+                                     w.flags(me) + kResultFlags, p, me, err_dev, s, 2);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce result wait");
                 char* out = bd.place == Place::Device ? static_cast<char*>(bd.dev) : dst;
-                if (rc == MPI_SUCCESS) rc = copy_async(out + o * esz, w.out(me) + obase, len * esz, sc);
-                if (rc == MPI_SUCCESS && sc != s && hipEventRecord(tp->pipe_copy[ci % 2], sc) != hipSuccess)
-                    rc = hip_fail(hipGetLastError(), "allreduce collect event");
+                if (rc == MPI_SUCCESS) rc = copy_async(out + o * esz, w.out(me) + obase, len * esz, s);
             }
             // step 4: this chunk's halves are free again (read by my trees and
-            // my copy, both earlier on the collect stream) -- only a later
-            // chunk of this call waits on it
+            // my copy, both earlier on the stream) -- only a later chunk of
+            // this call waits on it
             if (rc == MPI_SUCCESS && ci + 2 < nchunks) {
-                e = launch_post_flags(done_to.data(), (int)done_to.size(), seq, sc);
+                e = launch_post_flags(done_to.data(), (int)done_to.size(), seq, s);
                 if (e != hipSuccess) rc = hip_fail(e, "allreduce done flags");
             }
             tp->rd_parity ^= 1;
@@ -2429,10 +2228,6 @@ int do_allreduce(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_
         ++g_stats.flag_calls;
         const int rsy = sync_stream(s, "allreduce two-step");
         if (rc == MPI_SUCCESS) rc = rsy;
-        if (sc != s) {
-            const int rsc = sync_stream(sc, "allreduce two-step collect");
-            if (rc == MPI_SUCCESS) rc = rsc;
-        }
         if (rc == MPI_SUCCESS && __atomic_load_n(err_host, __ATOMIC_ACQUIRE))
             rc = flag_timeout(root < 0 ? "allreduce" : "reduce", me, __atomic_load_n(err_host, __ATOMIC_ACQUIRE), seq);
         tp->post_done(seq);
@@ -2581,8 +2376,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
     // allreduce does, one host sync per call instead of four per round.
     const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
     const size_t qh_el = esz ? (Qh / esz) & ~(size_t)15 : 0;
-    const bool one_step = p >= 2 && p <= 32 && rd_flags() && tp->has_done() && total * esz <= two_step_max(tp) &&
-                          qh_el > 0;
+    const bool one_step = p >= 2 && p <= 32 && tp->has_done() && total * esz <= two_step_max(tp) && qh_el > 0;
     Windows w;
     if ((rc = get_windows(tp, &w, one_step)) != MPI_SUCCESS) return rc;
     // sub-slot k of IN(r) receives rank k's contribution to r's block, qe
@@ -2632,7 +2426,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
                 for (int r = 0; r < p && rc == MPI_SUCCESS; ++r)
                     if (r != me && seq > 2) rc = tp->wait_done(r, seq - 2);
             } else if (rc == MPI_SUCCESS) {
-                hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, false, nullptr,
+                hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, seq - 2, nullptr,
                                                 w.flags(me) + kDoneFlags, p, me, err_dev, s, 3);
                 if (e != hipSuccess) rc = hip_fail(e, "reduce_scatter half-free wait");
             }
@@ -2655,7 +2449,7 @@ int do_reduce_scatter(Comm* c, const void* sendbuf, void* recvbuf, const int* re
             const size_t mylen = o < mycnt ? std::min(qh_el, mycnt - o) : 0;
             if (rc == MPI_SUCCESS) {
                 hipError_t e = launch_push_wait(sg.src.data(), sg.dst.data(), sg.n.data(), (int)sg.src.size(),
-                                                fl.data(), (int)fl.size(), seq, sys_fences(), counter + kCountWords,
+                                                fl.data(), (int)fl.size(), seq, counter + kCountWords,
                                                 w.flags(me), mylen ? p : 0, me, err_dev, s);
                 if (e != hipSuccess) rc = hip_fail(e, "reduce_scatter push");
             }
@@ -2853,7 +2647,6 @@ int combine2(int opidx, Kind k, const char* inout_src, const char* in, char* out
     t.P = 2;
     t.src[0] = inout_src;
     t.src[2] = in;
-    t.sys = sys_fences();
     if (out2) {                          // the same result stored twice
         t.extra[0] = out2;
         t.nextra = 1;
@@ -2861,48 +2654,6 @@ int combine2(int opidx, Kind k, const char* inout_src, const char* in, char* out
     hipError_t e = launch_tree_spec(opidx, k, t, out, n, s);
     return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "scan combine");
 }
-
-// One fused scan step (small vectors): the first workgroups push `psrc` into
-// the consumer's window and post its flag (k_tree's fused push; psrc == null:
-// nothing to push), the tree workgroups wait for the partial this rank
-// consumes (wflag >= v) and store a op tmp into out (and out2).  out must not
-// alias psrc: the tree does not wait for this launch's own push.
-int scan_fused_step(int opidx, Kind k, const char* a, const char* tmp, char* out, char* out2, size_t count,
-                    hipStream_t s, const unsigned long long* wflag, unsigned long long v, int* err,
-                    const void* psrc, void* pdst, size_t pbytes, unsigned long long* pflag, unsigned* pcounter)
-{
-    TreeSpec t;
-    t.P = 2;
-    t.src[0] = a;
-    t.src[2] = tmp;
-    t.sys = sys_fences();
-    if (out2) {
-        t.extra[0] = out2;
-        t.nextra = 1;
-    }
-    t.wait_flags = wflag;
-    t.wait_seq = v;
-    t.wait_n = 1;
-    t.wait_skip = -1;
-    t.wait_err = err;
-    if (psrc) {
-        t.push_nseg = 1;
-        t.push_src[0] = psrc;
-        t.push_dst[0] = pdst;
-        t.push_n[0] = pbytes;
-        t.push_nflags = 1;
-        t.push_flags[0] = pflag;
-        t.push_seq = v;
-        t.push_counter = pcounter;
-        t.push_sys = sys_fences();
-    }
-    hipError_t e = launch_tree_spec(opidx, k, t, out, count, s);
-    return e == hipSuccess ? MPI_SUCCESS : hip_fail(e, "scan step");
-}
-
-// vectors up to this size take the fused scan steps (as the barrier-free
-// small allreduce: the fused push's system-coherent 8-byte stores)
-constexpr size_t kScanFuseMax = (size_t)256 << 10;
 
 int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datatype dt,
             const OpRef& op, bool exclusive)
@@ -2919,8 +2670,7 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     // GPU-synchronised when the vector fits half an IN sub-slot (count, type,
     // p and the environment decide: the same on every rank)
     const size_t Qh = (sub_len(chunk_bytes(), p) / 2) & ~(size_t)255;
-    const bool flags = p >= 2 && p <= 32 && rd_flags() && tp->has_done() && bytes <= Qh &&
-                       bytes <= two_step_max(tp);
+    const bool flags = p >= 2 && p <= 32 && tp->has_done() && bytes <= Qh && bytes <= two_step_max(tp);
     Windows w;
     if ((rc = get_windows(tp, &w, flags)) != MPI_SUCCESS) return rc;
     // Each step's partial is PUSHED into the consumer's IN window (an xGMI
@@ -2931,11 +2681,10 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
     ce -= ce % 16;
     if (ce == 0) { set_error("scan: window too small"); return MPI_ERR_INTERN; }
     const size_t bstride = (bytes + 255) & ~(size_t)255;
-    char* partial = dev_scratch(5 * bstride + 256);
+    char* partial = dev_scratch(4 * bstride + 256);
     if (!partial) { set_error("scan: scratch allocation failed"); return MPI_ERR_NO_MEM; }
     char* res = partial + bstride;
-    char* partial2 = res + bstride;      // fused steps: the partial alternates with this one
-    char* src_stage = partial2 + bstride;   // host operands the kernels cannot address
+    char* src_stage = res + bstride;     // host operands the kernels cannot address
     char* dst_stage = src_stage + bstride;
     BufInfo bs = classify(src), bd = classify(recvbuf);
     PinHold pins;                        // host buffers: device aliases for the call
@@ -2973,7 +2722,6 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
         const char* cur_r = exclusive ? nullptr : srcv; // current result (have)
         bool same = !exclusive;                         // partial and result hold one value
         char* outv = dst_dev ? static_cast<char*>(dstv) : dst_stage;
-        const bool fuse = spin_tree_allowed() && fused_push() && bytes <= kScanFuseMax;
         int step = 0;
         for (int mask = 1; mask < p && rc == MPI_SUCCESS; mask <<= 1, ++step) {
             const int dst = me ^ mask;
@@ -2987,53 +2735,7 @@ int do_scan(Comm* c, const void* sendbuf, void* recvbuf, size_t count, MPI_Datat
             void* pd = feeds ? static_cast<void*>(w.sub(dst, me) + half) : nullptr;
             size_t pn = bytes;
             unsigned long long* pf = feeds ? w.flags(dst) + kScanFlags + me : nullptr;
-            if (fuse && use) {
-                // push (if any), wait and the first combine in one launch; the
-                // new partial goes to the buffer the push is NOT reading
-                const char* tmp = w.sub(me, dst) + half;
-                const unsigned long long* wf = w.flags(me) + kScanFlags + dst;
-                char* np = last ? nullptr : (cur_p == partial ? partial2 : partial);
-                const void* fps = feeds ? ps : nullptr;
-                if (me > dst) {
-                    char* nr = last ? outv : res;
-                    if (have && same) {
-                        rc = np ? scan_fused_step(op.opidx, k, cur_p, tmp, np, nr, count, s, wf, v, err_dev, fps, pd,
-                                                  pn, pf, counter)
-                                : scan_fused_step(op.opidx, k, cur_r, tmp, nr, nullptr, count, s, wf, v, err_dev, fps,
-                                                  pd, pn, pf, counter);
-                    } else {
-                        if (np) {
-                            rc = scan_fused_step(op.opidx, k, cur_p, tmp, np, nullptr, count, s, wf, v, err_dev, fps,
-                                                 pd, pn, pf, counter);
-                            if (rc == MPI_SUCCESS)
-                                rc = have ? combine2(op.opidx, k, cur_r, tmp, nr, count, s)
-                                          : copy_async(nr, tmp, bytes, s);
-                        } else if (have) {   // last step: only the result (no push: dst < me)
-                            rc = scan_fused_step(op.opidx, k, cur_r, tmp, nr, nullptr, count, s, wf, v, err_dev,
-                                                 nullptr, nullptr, 0, nullptr, nullptr);
-                        } else {             // Exscan's first fold is a copy: wait, then copy
-                            hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, v, false,
-                                                            nullptr, wf, 1, -1, err_dev, s);
-                            rc = e == hipSuccess ? copy_async(nr, tmp, bytes, s) : hip_fail(e, "scan wait");
-                        }
-                        same = false;
-                    }
-                    cur_r = nr;
-                    have = true;
-                } else {
-                    rc = scan_fused_step(op.opidx, k, cur_p, tmp, np, nullptr, count, s, wf, v, err_dev, fps, pd, pn,
-                                         pf, counter);
-                    same = false;
-                }
-                cur_p = np;
-                continue;
-            }
-            if (fuse && feeds) {             // push only: data and flag in one launch
-                hipError_t e = launch_push_post(&ps, &pd, &pn, 1, &pf, 1, v, sys_fences(), counter, s);
-                if (e != hipSuccess) rc = hip_fail(e, "scan push");
-                continue;
-            }
-            hipError_t e = launch_push_wait(&ps, &pd, &pn, feeds ? 1 : 0, &pf, feeds ? 1 : 0, v, sys_fences(),
+            hipError_t e = launch_push_wait(&ps, &pd, &pn, feeds ? 1 : 0, &pf, feeds ? 1 : 0, v,
                                             counter + kCountWords,
                                             use ? w.flags(me) + kScanFlags + dst : w.flags(me), use ? 1 : 0, -1,
                                             err_dev, s);
@@ -4118,14 +3820,14 @@ int p2p_send(Comm* u, int to, const char* src, size_t bytes, int* err_dev)
         const uint64_t c = ++sent;
         const size_t off = (size_t)i * Qh, len = std::min(Qh, bytes - off);
         if (c > 2) {                                  // the half's previous chunk was copied out
-            hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, c - 2, false, nullptr,
+            hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, c - 2, nullptr,
                                             w.flags(u->rank) + kP2PAck + to, 1, -1, err_dev, s);
             if (e != hipSuccess) { rc = hip_fail(e, "p2p ack wait"); break; }
         }
         const void* ps = src + off;
         void* pd = w.sub(to, u->rank) + (size_t)(c & 1) * Qh;
         unsigned long long* pf = w.flags(to) + kP2PData + u->rank;
-        hipError_t e = launch_push_wait(&ps, &pd, &len, 1, &pf, 1, c, sys_fences(), counter + kCountWords,
+        hipError_t e = launch_push_wait(&ps, &pd, &len, 1, &pf, 1, c, counter + kCountWords,
                                         w.flags(u->rank), 0, -1, err_dev, s);
         if (e != hipSuccess) rc = hip_fail(e, "p2p push");
     }
@@ -4144,7 +3846,7 @@ int p2p_recv(Comm* u, int from, char* dst, size_t bytes, int* err_dev)
     for (int i = 0; i < n && rc == MPI_SUCCESS; ++i) {
         const uint64_t c = ++got;
         const size_t off = (size_t)i * Qh, len = std::min(Qh, bytes - off);
-        hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, c, false, nullptr,
+        hipError_t e = launch_push_wait(nullptr, nullptr, nullptr, 0, nullptr, 0, c, nullptr,
                                         w.flags(u->rank) + kP2PData + from, 1, -1, err_dev, s);
         if (e != hipSuccess) { rc = hip_fail(e, "p2p data wait"); break; }
         rc = copy_async(dst + off, w.sub(u->rank, from) + (size_t)(c & 1) * Qh, len, s);

@@ -44,13 +44,10 @@ public:
     // PCI bus ids, allgathered at init, so every rank holds the same value).
     // The GPU-flag Rabenseifner schedules default off there (two_step_max).
     bool gpu_shared = false;
-    // The engine's second stream and the pipelined allreduce's cross-stream
-    // events belong to the communicator, so collectives of two communicators
-    // running at once from different threads never wait on each other's
-    // events (msx_transport.cpp, aux_stream / pipe_events).
+    // The engine's second stream belongs to the communicator, so collectives
+    // of two communicators running at once from different threads never
+    // wait on each other (msx_transport.cpp, aux_stream).
     hipStream_t aux = nullptr;
-    hipEvent_t pipe_tree[2] = {nullptr, nullptr}, pipe_copy[2] = {nullptr, nullptr};
-    int pipe_ok = -1;   // -1 = not created yet
     // lock-step host collectives over the bootstrap hub (all ranks, same n)
     virtual int allgather(const void* mine, size_t n, void* all) = 0;
     virtual int barrier() = 0;

@@ -12,15 +12,13 @@
 namespace msx {
 namespace dev {
 
-// ---- copy-segment and flag descriptors (k_copy_segs, k_push_post, k_tree) -------
+// ---- copy-segment and flag descriptors (k_copy_segs, k_push_wait, k_tree) -------
 constexpr int kMaxSegs = 32;
 struct CopySegs {
     const void* src[kMaxSegs];
     void* dst[kMaxSegs];
     size_t nbytes[kMaxSegs];
     int n;
-    int sys;
-    int wt;    // copy_post_body: write-through stores (st_wt), see there
 };
 
 struct PostFlags {
@@ -40,22 +38,6 @@ __device__ __forceinline__ void stores_done()
     __atomic_signal_fence(__ATOMIC_SEQ_CST);      // no compiler motion of stores past the wait
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// Producer half of a GPU-flag hand-off, done by ONE lane of a workgroup after
-// every lane waited for its own stores (stores_done) and the workgroup met at a
-// barrier: an agent-scope release (buffer_wbl2 sc1 + wait) before the lane
-// counts the workgroup done, so the count -- and the flag the last workgroup
-// posts with a system-scope release -- is ordered after ALL of the
-// workgroup's stores in the HSA model, not only by the stores' completion
-// (MI355X_MICROARCH.md, inter-workgroup visibility, producer form).  The asm
-// wait keeps the compiler from dropping the wait after the writeback (the
-// guide's ROCm 7.2 hazard).  Mode 2 of the kernels' `sys` word; mode 0 (vmcnt
-// only, rounds 1-3) stays selectable with MSX_WG_RELEASE=0.
-__device__ __forceinline__ void wg_release()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Write-through stores for data a GPU flag announces to another GPU: relaxed
@@ -109,44 +91,6 @@ __device__ __forceinline__ void st_wt_elem(T* p, const T& v)
     }
 }
 
-// The small-allreduce push (k_push_post, and the first workgroups of a fused
-// k_tree launch): see the comment at k_push_post.
-__device__ __forceinline__ void push_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
-                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
-{
-    const char* src = static_cast<const char*>(c.src[sg]);
-    char* dst = static_cast<char*>(c.dst[sg]);
-    const size_t nb = c.nbytes[sg];
-    const size_t stride = (size_t)gx * 256;
-    size_t done = 0;
-    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
-        // 16-byte write-through buffer stores (segments stay far below 4 GiB:
-        // at most half an IN sub-slot)
-        const size_t nv = nb / 16;
-        const __amdgpu_buffer_rsrc_t r = wt_rsrc(dst);
-        for (size_t i = (size_t)bx * 256 + threadIdx.x; i < nv; i += stride)
-            st_wt_at(r, 16 * i, reinterpret_cast<const u32x4*>(src)[i]);
-        done = nv * 16;
-    }
-    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride)
-        st_wt_elem(dst + i, src[i]);
-    // sys: 1 = cached windows (system fence per lane), 2 = workgroup release
-    // (wg_release), 0 = stores' completion only
-    if (sys == 1) __threadfence_system();
-    else stores_done();                                 // vmcnt(0): this lane's stores completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (sys == 2) wg_release();
-        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == total - 1) {
-            if (sys == 1) __threadfence_system();
-            for (int k = 0; k < f.n; ++k)
-                __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next call
-        }
-    }
-}
-
 // Count finished workgroup b of nb; true in exactly one workgroup, after all
 // nb have counted.  Thousands of workgroups adding to ONE word serialise
 // (a 4096-workgroup tree took 70 us instead of 38), so workgroup b counts on
@@ -167,14 +111,19 @@ __device__ __forceinline__ bool count_done(unsigned* base, unsigned b, unsigned 
     return true;
 }
 
-// Bulk variant for multi-MiB segments (the two-step allreduce's pieces):
-// write-through stores (st_wt) from a full grid, four loads in flight per lane
-// (as k_copy_segs), then push_post_body's fenced count and flag post.  `sys`
-// (cached windows) writes the L2 back at system scope before counting.
-// MSX_WT_STORES=0 (wt == 0) keeps plain 16-byte stores, which rely on the
-// windows' uncached mapping at the writer.
+// The push of every GPU-flag schedule (k_push_wait): segment sg's bytes into
+// a peer's window with 16-byte write-through stores (st_wt_at: sc0 sc1, so a
+// completed store is at the owner whatever cache type the writer's mapping of
+// the peer window has) from a full grid, four loads in flight per lane (as
+// k_copy_segs).  EVERY lane then waits until its own stores have completed
+// (stores_done: s_waitcnt vmcnt(0), without the L2 writeback an agent-scope
+// fence adds), the workgroup meets at a barrier, and thread 0 counts the
+// workgroup done (count_done); the last one posts `seq` into every flag with a
+// system-scope release -- the threadFenceReduction pattern: every
+// workgroup's data completed before its count, so no flag can overtake any of
+// it.  The launcher keeps every segment below 4 GiB (32-bit buffer offsets).
 __device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlags& f, unsigned* counter,
-                                               unsigned total, int sys, unsigned bx, unsigned gx, int sg)
+                                               unsigned total, unsigned bx, unsigned gx, int sg)
 {
     const char* src = static_cast<const char*>(c.src[sg]);
     char* dst = static_cast<char*>(c.dst[sg]);
@@ -184,36 +133,21 @@ __device__ __forceinline__ void copy_post_body(const CopySegs& c, const PostFlag
     if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
         const size_t nv = nb / 16;
         const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-        u32x4* d4 = reinterpret_cast<u32x4*>(dst);
         size_t i = (size_t)bx * 256 + threadIdx.x;
-        if (c.wt) {
-            const __amdgpu_buffer_rsrc_t r = wt_rsrc(dst);
-            for (; i + 3 * stride < nv; i += 4 * stride) {
-                const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
-                st_wt_at(r, 16 * i, a0); st_wt_at(r, 16 * (i + stride), a1);
-                st_wt_at(r, 16 * (i + 2 * stride), a2); st_wt_at(r, 16 * (i + 3 * stride), a3);
-            }
-            for (; i < nv; i += stride) st_wt_at(r, 16 * i, s4[i]);
-        } else {
-            for (; i + 3 * stride < nv; i += 4 * stride) {
-                const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
-                d4[i] = a0; d4[i + stride] = a1; d4[i + 2 * stride] = a2; d4[i + 3 * stride] = a3;
-            }
-            for (; i < nv; i += stride) d4[i] = s4[i];
+        const __amdgpu_buffer_rsrc_t r = wt_rsrc(dst);
+        for (; i + 3 * stride < nv; i += 4 * stride) {
+            const u32x4 a0 = s4[i], a1 = s4[i + stride], a2 = s4[i + 2 * stride], a3 = s4[i + 3 * stride];
+            st_wt_at(r, 16 * i, a0); st_wt_at(r, 16 * (i + stride), a1);
+            st_wt_at(r, 16 * (i + 2 * stride), a2); st_wt_at(r, 16 * (i + 3 * stride), a3);
         }
+        for (; i < nv; i += stride) st_wt_at(r, 16 * i, s4[i]);
         done = nv * 16;
     }
-    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) {
-        if (c.wt) st_wt_elem(dst + i, src[i]);
-        else dst[i] = src[i];
-    }
-    if (sys == 1) __threadfence_system();
-    else stores_done();
+    for (size_t i = done + (size_t)bx * 256 + threadIdx.x; i < nb; i += stride) st_wt_elem(dst + i, src[i]);
+    stores_done();
     __syncthreads();
-    if (threadIdx.x == 0 && sys == 2) wg_release();
     // counter: a kCountWords block (count_done); b = this workgroup's index
     if (threadIdx.x == 0 && count_done(counter, (unsigned)sg + bx * (unsigned)c.n, total)) {
-        if (sys == 1) __threadfence_system();
         for (int k = 0; k < f.n; ++k)
             __hip_atomic_store(f.dst[k], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -239,76 +173,51 @@ struct TreeArgs {
     int nleaves;   // leaves present (<= P); the rest of the P-leaf tree is empty
     unsigned pairmask;
     int chain;
-    int sys;   // sources/outputs shared with other GPUs: system-coherent access
     int wt;    // results announced by done_flags: write-through stores (st_wt)
-    int rel;   // tree_done: one lane's agent-scope release per workgroup (wg_release)
-    const unsigned long long* wait_flags;   // see TreeSpec
-    unsigned long long wait_seq;
-    int wait_n;
-    int wait_skip;
-    int* wait_err;
-    unsigned long long wait_ticks;   // bound of the wait in s_memrealtime ticks (100 MHz)
-    int wait_tag;                    // phase code reported with a timeout
-    // fused push (barrier-free small allreduce): the first npush workgroups
-    // copy this rank's contribution into the peers' IN halves and post the
-    // arrival flags (push_post_body) instead of evaluating the tree
-    unsigned npush;
-    unsigned push_gx;     // workgroups per push segment
-    int push_sys;
-    unsigned* push_counter;
-    CopySegs push;
-    PostFlags flags;
     // result-ready flags (barrier-free two-step allreduce): once every tree
     // workgroup of all `done_launches` launches has stored its results, post
     // done_flags (see tree_done)
     unsigned* done_counter;       // kCountWords block: [0] count_done, [1] launches done
     unsigned done_launches;
     PostFlags done_flags;
-    // tile order (tuning only, msx_tune_tree modes 9-11): 0 = XCD-contiguous
-    // eighths, > 0 = XCD x owns interleaved runs of xg consecutive tiles,
-    // -1 = dispatch order
+    // tile order: 0 = XCD-contiguous eighths (the default), -1 = dispatch
+    // order (the one-wave DRAM-regime geometry, msx_tree_impl.h)
     int xg;
 };
 
 // Workgroup b of nb -> tile under TreeArgs::xg (a bijection on [0, nb)).
 __device__ __forceinline__ size_t tree_tile(int xg, unsigned b, unsigned nb)
 {
-    if (xg == 0) return xcd_tile(b, nb);
-    if (xg < 0) return b;
-    const unsigned g = (unsigned)xg, full = (nb / (8u * g)) * (8u * g);
-    if (b >= full) return b;
-    const unsigned x = b & 7, j = b >> 3;
-    return ((size_t)(j / g) * 8 + x) * g + (j % g);
+    return xg == 0 ? xcd_tile(b, nb) : b;
 }
 
 // End of a tree workgroup when the launch posts result-ready flags: the
-// threadFenceReduction pattern of push_post_body, extended over the launches
+// threadFenceReduction pattern of copy_post_body, extended over the launches
 // that together evaluate one call (stream-ordered, so at most one is in
-// flight).  Every lane waits for its own stores (stores_done; cached windows:
-// system fence), thread 0 counts the workgroup, the launch's last workgroup
-// counts the launch, and the last workgroup of the last launch posts the
-// flags with system-scope release stores.  Both words are left zero for the
-// next call.
+// flight).  Every lane waits for its own write-through stores (stores_done),
+// thread 0 counts the workgroup, the launch's last workgroup counts the
+// launch, and the last workgroup of the last launch posts the flags with
+// system-scope release stores.  Both words are left zero for the next call.
 __device__ __forceinline__ void tree_done(const TreeArgs& a, unsigned b, unsigned nb)
 {
-    if (a.sys) __threadfence_system();
-    else stores_done();
+    stores_done();
     __syncthreads();
     if (threadIdx.x != 0) return;
-    if (a.rel && !a.sys) wg_release();
     if (!count_done(a.done_counter, b, nb)) return;
     // launches of the call: word 1 of the block
     const unsigned l = __hip_atomic_fetch_add(a.done_counter + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (l != a.done_launches - 1) return;
     __hip_atomic_store(a.done_counter + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.sys) __threadfence_system();
     for (int k = 0; k < a.done_flags.n; ++k)
         __hip_atomic_store(a.done_flags.dst[k], a.done_flags.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Arrival wait of the barrier-free small allreduce: thread 0 of every
-// workgroup polls the peers' flags (uncached window memory, system-scope
-// loads) until each reaches the call's sequence number.  Bounded: after
+// The GPU-side wait of every flag schedule, run by ONE workgroup of a
+// k_push_wait launch: thread 0 polls the peers' flags (uncached window
+// memory, system-scope loads) until each reaches the call's sequence number;
+// the launches after it on the stream read what the flags announce.  Only a
+// single workgroup per rank ever spins, so ranks that share a GPU cannot
+// starve each other's pushes.  Bounded: after
 // `ticks` of s_memrealtime (100 MHz; MSX_FLAG_TIMEOUT_MS, default 20 s) it
 // reports through *wait_err -- tag * 65536 + 1 + the first peer whose flag is
 // missing, so the host can name the phase and the peer -- and the workgroup
@@ -343,27 +252,6 @@ __device__ __forceinline__ bool wait_flags_body(const unsigned long long* flags,
     return ok != 0;
 }
 
-__device__ __forceinline__ bool arrival_wait(const TreeArgs& a)
-{
-    return wait_flags_body(a.wait_flags, a.wait_seq, a.wait_n, a.wait_skip, a.wait_err, a.wait_ticks, a.wait_tag);
-}
-
-// Start-of-kernel system acquire: invalidate this CU's L1 and the XCD's L2
-// lines for memory other GPUs may have written since (peer HBM over xGMI).
-__device__ __forceinline__ void acquire_system()
-{
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    __syncthreads();
-}
-
-// End-of-kernel system release: write this XCD's dirty L2 lines back so peers
-// reading over xGMI see them (one fence per workgroup).
-__device__ __forceinline__ void release_system()
-{
-    __syncthreads();
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-}
-
 template <class F, class V, class LD>
 __device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
 {
@@ -396,45 +284,6 @@ __device__ __forceinline__ V tree_eval(const TreeArgs& a, LD load)
 #pragma unroll
         for (int k = 0; k + w < kMaxLeaves; k += 2 * w)
             if (k + w < a.nleaves) v[k] = F::apply(v[k], v[k + w]);
-    }
-    return v[0];
-}
-
-// The same tree over 16-byte vectors, with every source vector loaded
-// (non-temporal: each is read once) before the first combine, so all of them
-// are in flight together.
-template <class F, bool NT>
-__device__ __forceinline__ u32x4 tree_vec(const TreeArgs& a, size_t i)
-{
-    auto ld_src = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
-    u32x4 v[kMaxLeaves], w[kMaxLeaves];
-    if (a.chain) {
-#pragma unroll
-        for (int k = 0; k < kMaxLeaves; ++k)
-            if (k < a.P) v[k] = ld_src(k);
-        __builtin_amdgcn_sched_barrier(0);
-        u32x4 r = v[0];
-#pragma unroll
-        for (int k = 1; k < kMaxLeaves; ++k)
-            if (k < a.P) r = F::apply(r, v[k]);
-        return r;
-    }
-#pragma unroll
-    for (int k = 0; k < kMaxLeaves; ++k) {
-        if (k < a.nleaves) {
-            v[k] = ld_src(2 * k);
-            if ((a.pairmask >> k) & 1u) w[k] = ld_src(2 * k + 1);
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < kMaxLeaves; ++k)
-        if (k < a.nleaves && ((a.pairmask >> k) & 1u)) v[k] = F::apply(v[k], w[k]);
-#pragma unroll
-    for (int d = 1; d < kMaxLeaves; d *= 2) {
-#pragma unroll
-        for (int k = 0; k + d < kMaxLeaves; k += 2 * d)
-            if (k + d < a.nleaves) v[k] = F::apply(v[k], v[k + d]);
     }
     return v[0];
 }
@@ -558,47 +407,28 @@ __device__ __forceinline__ void tree_fixed(const TreeArgs& a, u32x4* __restrict_
     }
 }
 
-// UPFRONT: all source vectors loaded before the first combine (tree_vec), else
-// loads interleaved with the combines as the tree consumes them (tree_eval);
-// NT: non-temporal source loads.  The fp32 SUM tuning sweep times all four
-// (p = 8, 32 MiB each): interleaved plain loads 51.7 us (5.8 TB/s), up front
-// 57.1 us -- holding every source vector costs 146 VGPRs instead of 77, half
-// the waves per SIMD -- and non-temporal loads 3-8 % slower either way.
-template <int OP, class T, class VT, int BLOCK, bool UPFRONT = false, bool NT = false, int NL = 0, int U = 1,
+// The generic kernel (NL == 0: any P <= 16 tree with pairs and absent
+// leaves, any chain) loads the sources as the tree consumes them (tree_eval):
+// p = 8 fp32 SUM, 32 MiB per source, that measured 51.7 us against 57.1 us
+// with every source vector loaded up front (146 VGPRs instead of 77, half the
+// waves per SIMD; round-2 tuning sweep).  NL > 0: tree_fixed.
+// NT: non-temporal source loads.
+template <int OP, class T, class VT, int BLOCK, bool NT = false, int NL = 0, int U = 1,
           bool CHAIN = false, bool MASKED = false>
 __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out, size_t nvec,
                                                 size_t tail, int vec_ok)
 {
     constexpr size_t EPV = 16 / sizeof(T);
-    unsigned b = blockIdx.x, nb = gridDim.x;
-    if (a.npush) {
-        // fused push: the first npush workgroups push this rank's vector and
-        // post its flags; they never wait, so the peers' trees always progress
-        if (b < a.npush) {
-            // segment b % n: every peer's push starts at once (see k_copy_segs)
-            const unsigned ns = (unsigned)a.push.n;
-            push_post_body(a.push, a.flags, a.push_counter, a.npush, a.push_sys, b / ns, a.push_gx, (int)(b % ns));
-            return;
-        }
-        b -= a.npush;
-        nb -= a.npush;
-    }
+    const unsigned b = blockIdx.x, nb = gridDim.x;
     const size_t stride = (size_t)nb * BLOCK;
     const size_t bid = tree_tile(a.xg, b, nb);   // XCD-contiguous by default (see combine_body)
-    if (a.wait_flags && !arrival_wait(a)) return;
-    if (a.sys) acquire_system();
     if constexpr (NL > 0) {
         if (vec_ok)
             tree_fixed<VecFn<OP, VT>, NL, U, BLOCK, NT, CHAIN, MASKED>(a, reinterpret_cast<u32x4*>(out), nvec, bid, nb);
     } else if (vec_ok) {
         for (size_t i = bid * BLOCK + threadIdx.x; i < nvec; i += stride) {
-            u32x4 r;
-            if constexpr (UPFRONT) {
-                r = tree_vec<VecFn<OP, VT>, NT>(a, i);
-            } else {
-                auto load = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
-                r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
-            }
+            auto load = [&](int k) { return ld<NT>(reinterpret_cast<const u32x4*>(a.s[k]) + i); };
+            const u32x4 r = tree_eval<VecFn<OP, VT>, u32x4>(a, load);
             put_vec(a, reinterpret_cast<u32x4*>(out), i, r);
         }
     }
@@ -615,19 +445,19 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
             for (int e = 0; e < a.nextra; ++e) static_cast<T*>(a.extra[e])[first + s] = r;
         }
     }
-    if (a.sys) release_system();
     if (a.done_counter) tree_done(a, b, nb);
 }
 
 }  // namespace dev
 
-// host side: the per-op tree launchers (msx_tree_*.hip) and the tuning knob
-extern TreeTune g_tree_tune;
-// source bytes of one tree launch above which its loads are non-temporal
-size_t tree_nt_min();
+// host side: the per-op tree launchers (msx_tree_*.hip)
+// Source bytes of one tree launch above which its loads are non-temporal:
+// the 256 MiB Infinity Cache (MALL) of one MI355X.  p = 8 fp32 SUM, per-source
+// MiB -> us plain / non-temporal (scripts/tree_probe.py in round 3,
+// profiles/r03/tree/size_sweep/): 32: 46.7 / 47.8, 48: 85.6 / 72.5,
+// 64: 117.4 / 96.6, 128: 224.3 / 189.3.
+constexpr size_t kTreeNtMin = (size_t)256 << 20;
 template <int OP>
 hipError_t tree_dispatch(Kind k, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s);
-// fp32 SUM tuning modes of msx_tune_tree (msx_tree_sum.hip)
-hipError_t tree_tune_f32_sum(int mode, const dev::TreeArgs& a, int ns, void* out, size_t n, hipStream_t s);
 
 }  // namespace msx

@@ -1,7 +1,7 @@
 // msx_tree_impl.h — host-side launch of k_tree (msx_tree_dev.h) for one MPI_Op
-// family per translation unit (msx_tree_sum.hip with the fp32 SUM tuning
-// modes, msx_tree_prod/max/min/loc/land/lor/lxor/bit.hip), so the template
-// instantiations compile in parallel.  Included by those files only.
+// family per translation unit (msx_tree_sum/prod/max/min/loc/land/lor/lxor/
+// bit.hip), so the template instantiations compile in parallel.  Included by
+// those files only.
 #pragma once
 #include "msx_tree_dev.h"
 
@@ -14,8 +14,8 @@ constexpr int kTreeBlock = 256;
 constexpr int kTreeGridCap = 4096;          // generic kernel: grid-stride beyond this
 constexpr int kFixedGridCap = 1 << 20;      // compile-time-source kernel: one tile per workgroup
 
-template <int OP, class T, class VT, bool UPFRONT = false, bool NT = false, int NL = 0, int U = 1,
-          bool CHAIN = false, int BLOCK = kTreeBlock, bool MASKED = false>
+template <int OP, class T, class VT, bool NT = false, int NL = 0, int U = 1, bool CHAIN = false,
+          int BLOCK = kTreeBlock, bool MASKED = false>
 hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     bool ok = ((uintptr_t)out & 15) == 0;
@@ -28,12 +28,10 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
     size_t grid = (work + BLOCK - 1) / BLOCK;
     // one tile per workgroup for the compile-time-source kernel and for the
     // one-wave DRAM-regime form of the generic one; grid-stride beyond
-    const size_t cap = g_tree_tune.grid_cap > 0 ? (size_t)g_tree_tune.grid_cap
-                                                : (size_t)(NL > 0 || BLOCK == 64 ? kFixedGridCap : kTreeGridCap);
+    const size_t cap = (size_t)(NL > 0 || BLOCK == 64 ? kFixedGridCap : kTreeGridCap);
     if (grid > cap) grid = cap;
     if (grid == 0) return hipSuccess;
-    grid += a.npush;                         // fused push workgroups come first
-    hipLaunchKernelGGL((k_tree<OP, T, VT, BLOCK, UPFRONT, NT, NL, U, CHAIN, MASKED>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((k_tree<OP, T, VT, BLOCK, NT, NL, U, CHAIN, MASKED>), dim3((unsigned)grid),
                        dim3(BLOCK), 0, s, a, static_cast<T*>(out), nvec, tail, ok ? 1 : 0);
     return hipGetLastError();
 }
@@ -49,19 +47,16 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
 // (scripts/tree_dram_ab.sh, profiles/r03/tree/dram_geometry/): 64 MiB per
 // source 96.3 -> 90.9 us (0.78 -> 0.83 of peak), 128 MiB 201.7 -> 186.8 us
 // (0.75 -> 0.81); 64-lane workgroups in XCD-contiguous order and 256-lane ones
-// in dispatch order gain 1-2 % only.  Not with fused push workgroups (their
-// copy loop assumes 256 lanes; only small calls fuse).
+// in dispatch order gain 1-2 % only.
 template <int OP, class T, class VT, bool NT, int NL, int U, bool CHAIN, bool MASKED = false>
 hipError_t run_tree_fixed(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
 {
     if constexpr (NT) {
-        if (a.npush == 0) {
-            TreeArgs b = a;
-            b.xg = -1;
-            return run_tree<OP, T, VT, false, NT, NL, U, CHAIN, 64, MASKED>(b, nsrc, out, count, s);
-        }
+        TreeArgs b = a;
+        b.xg = -1;
+        return run_tree<OP, T, VT, NT, NL, U, CHAIN, 64, MASKED>(b, nsrc, out, count, s);
     }
-    return run_tree<OP, T, VT, false, NT, NL, U, CHAIN, kTreeBlock, MASKED>(a, nsrc, out, count, s);
+    return run_tree<OP, T, VT, NT, NL, U, CHAIN, kTreeBlock, MASKED>(a, nsrc, out, count, s);
 }
 
 template <int OP, class T, class VT, int U = 1, bool NT = false>
@@ -103,22 +98,16 @@ hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hi
     }
     if constexpr (NT) {
         // the generic kernel in the same DRAM-regime geometry (run_tree_fixed)
-        if (a.npush == 0) {
-            TreeArgs b = a;
-            b.xg = -1;
-            return run_tree<OP, T, VT, false, NT, 0, 1, false, 64>(b, nsrc, out, count, s);
-        }
+        TreeArgs b = a;
+        b.xg = -1;
+        return run_tree<OP, T, VT, NT, 0, 1, false, 64>(b, nsrc, out, count, s);
     }
-    return run_tree<OP, T, VT, false, NT>(a, nsrc, out, count, s);
+    return run_tree<OP, T, VT, NT>(a, nsrc, out, count, s);
 }
 
 // Source loads: plain while the call's sources fit the 256 MiB Infinity Cache
 // (just written by the scatter, so partly resident: plain loads hit it),
-// non-temporal beyond (streaming: the cache only churns).  p = 8 fp32 SUM,
-// per-source MiB -> us plain / non-temporal (scripts/tree_probe.py,
-// profiles/r03/tree/size_sweep/): 32: 46.7 / 47.8, 48: 85.6 / 72.5,
-// 64: 117.4 / 96.6, 128: 224.3 / 189.3.  MSX_TREE_NT_MIN overrides the bound
-// (tree_nt_min, msx_kernels.hip).
+// non-temporal beyond (streaming: the cache only churns); kTreeNtMin.
 
 template <int OP, class T, class VT, int U = 1>
 hipError_t run_tree_auto(const TreeArgs& a, int nsrc, void* out, size_t count, hipStream_t s)
@@ -126,7 +115,7 @@ hipError_t run_tree_auto(const TreeArgs& a, int nsrc, void* out, size_t count, h
     // sources actually read: a tree's leaves plus the second operand of each
     // folded pair (nsrc counts the 2P slots), a chain's P vectors
     const size_t nread = a.chain ? (size_t)a.P : (size_t)a.nleaves + (size_t)__builtin_popcount(a.pairmask);
-    if (count * sizeof(T) * nread > tree_nt_min())
+    if (count * sizeof(T) * nread > kTreeNtMin)
         return run_tree_sel<OP, T, VT, U, true>(a, nsrc, out, count, s);
     return run_tree_sel<OP, T, VT, U, false>(a, nsrc, out, count, s);
 }

@@ -174,14 +174,8 @@ def lib():
         "msx_pack_dev": (i, [p, i64, i, p, p]),
         "msx_unpack_dev": (i, [p, i64, i, p, p]),
         "msx_reduce_tree_dev": (i, [ctypes.POINTER(p), i, p, i64, i, i, p]),
-        "msx_tune_set": (i, [i, i]),
-        "msx_tune_tree": (i, [i, i]),
         "msx_tune_pack": (i, [i]),
-        "msx_tune_variant_count": (i, []),
-        "msx_tune_variant_name": (ctypes.c_char_p, [i]),
-        "msx_probe_hbm": (i, [i, p, p, i64, p]),
-        "msx_probe_alloc": (i, [i64, i, ctypes.POINTER(p)]),
-        "msx_probe_free": (i, [p]),
+        "msx_copy_dev": (i, [p, p, i64, p]),
         "msx_set_staging_chunk": (i, [i64]),
         "msx_set_host_mode": (i, [i]),
     }

@@ -3,7 +3,7 @@
 Every cross-rank wait in the engine is bounded (GPU flag waits by
 MSX_FLAG_TIMEOUT_MS, measured on the 100 MHz s_memrealtime clock inside the
 kernel; host barriers by MSX_BOOTSTRAP_TIMEOUT) and names what it waited for.
-MSX_FAULT_DROP_FLAGS=<rank>:<seq> (test-only fault injection,
+MSX_TEST_DROP_FLAGS=<rank>:<seq> (test-only fault injection,
 msx_transport.cpp fault_drop_flags) makes <rank> skip its arrival-flag posts
 of flag-synchronised call <seq>, so its peer's wait must run out.
 
@@ -68,7 +68,7 @@ def _run(mode, bar_timeout):
         env.update({"MSX_SIZE": "2", "MSX_RANK": str(r), "MSX_DEVICE": "0",
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
                     "MSX_BOOTSTRAP_TIMEOUT": str(bar_timeout), "MSX_FLAG_TIMEOUT_MS": "3000",
-                    "MSX_FAULT_DROP_FLAGS": "1:1", "FAULT_MODE": mode})
+                    "MSX_TEST_DROP_FLAGS": "1:1", "FAULT_MODE": mode})
         env.pop("MSMPI_FORCE_ASYNC_WORKFLOW", None)
         procs.append(subprocess.Popen([sys.executable, "-c",
                                        f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],

@@ -258,7 +258,7 @@ def test_pageable_operands_through_the_page_locked_ring(L):
 def test_mpi_reduce_local_call_pin_edges(L):
     # host mode 0 pins pageable operands for the call: operands that share
     # pages (one pin of the union), unaligned starts and ragged ends, one
-    # operand on the device, sizes either side of MSX_HOST_PIN_MIN, repeated
+    # operand on the device, sizes either side of the 1 MiB pinning threshold, repeated
     # calls on the same buffers (the pin is released every time), and a
     # read-only `in` mapping the driver refuses to pin (staged instead)
     import mmap
@@ -404,29 +404,6 @@ def test_tree_every_legal_pair(L, p):
         assert got == lv[0].tobytes(), f"{op} {dt} p={p}"
 
 
-def test_tree_tuning_modes_agree(L):
-    # every msx_tune_tree mode evaluates the same fp32 SUM tree (p = 8, ragged
-    # 3 Mi + 5 elements, one source misaligned -> scalar path for mode 4..7)
-    rng = np.random.default_rng(77)
-    n = (3 << 20) + 5
-    xs = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(8)]
-    lv = list(xs)
-    while len(lv) > 1:
-        lv = [lv[i] + lv[i + 1] for i in range(0, len(lv), 2)]
-    want = lv[0].view(np.uint32)
-    for offset in (0, 4):
-        dv = [_dev(x, offset if r == 3 else 0) for r, x in enumerate(xs)]
-        arr = (ctypes.c_void_p * 8)(*[d[1] for d in dv])
-        for mode in range(18):
-            for cap in (0, 1024):
-                assert L.msx_tune_tree(mode, cap) == 0
-                out = torch.zeros(n, dtype=torch.float32, device="cuda")
-                assert L.msx_reduce_tree_dev(arr, 8, out.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
-                torch.cuda.synchronize()
-                assert np.array_equal(out.cpu().numpy().view(np.uint32), want), (mode, cap, offset)
-    assert L.msx_tune_tree(0, 0) == 0
-
-
 def _oracle_tree(op, dt, srcs, P, pairmask, nleaves, chain):
     """The engine's tree evaluated with the oracle's combine (msx_tree_dev.h
     tree_eval): leaf k = srcs[2k] (op)= srcs[2k+1] when paired, then the
@@ -553,12 +530,12 @@ def test_reduce_local_multi_gpu_host_operands(L, ngpus):
 @pytest.mark.parametrize("ngpus", [2, 3, 8])
 def test_reduce_local_multi_split_on_one_device(L, ngpus):
     """The k-range split of msx_reduce_local_multi run on this box's one GPU
-    (MSX_MULTI_SPLIT_TEST=1: range d on device d % visible): the call-scoped
+    (MSX_TEST_MULTI_SPLIT=1: range d on device d % visible): the call-scoped
     portable pins (listed like every call pin), the per-device aliases from the
     registered base plus the offset, 256-B range ends and the ragged tail --
     the code the 8-GPU node runs, minus the other devices.  Operands in
     separate buffers, and in one buffer (one pin covering both)."""
-    os.environ["MSX_MULTI_SPLIT_TEST"] = "1"
+    os.environ["MSX_TEST_MULTI_SPLIT"] = "1"
     try:
         rng = np.random.default_rng(91 + ngpus)
         for n, op, dt in (((3 << 20) // 4 + 5, "MPI_SUM", "MPI_FLOAT"), ((5 << 20) // 8 + 3, "MPI_MAX", "MPI_DOUBLE"),
@@ -576,7 +553,7 @@ def test_reduce_local_multi_split_on_one_device(L, ngpus):
             assert both[n:].tobytes() == exp.tobytes(), (op, dt, n, ngpus, "shared pages")
             assert both[:n].tobytes() == a.tobytes()
     finally:
-        del os.environ["MSX_MULTI_SPLIT_TEST"]
+        del os.environ["MSX_TEST_MULTI_SPLIT"]
     # no pin outlives the call: the same pageable ranges pin again, alone
     x, y = _raw(gen(KIND["MPI_FLOAT"], "MPI_SUM", 1 << 20, rng)), _raw(gen(KIND["MPI_FLOAT"], "MPI_SUM", 1 << 20, rng))
     ye = _raw(y)
@@ -586,19 +563,33 @@ def test_reduce_local_multi_split_on_one_device(L, ngpus):
 
 
 def test_copy_geometries_exact(L):
-    # the engine's local copy in both geometries (probe modes 8 / 9: k_copy_segs'
-    # XCD-contiguous tiles, k_copy_dram's one-wave dispatch order) and the
-    # default launcher (mode 4: k_copy_dram above 256 MiB) copy every byte
+    # the engine's local copy (msx_copy_dev): k_copy_segs' XCD-contiguous tiles
+    # up to 16 MiB, k_copy_dram's one-wave dispatch order above; every byte
+    # copied, nothing written past the end
     for nbytes in (4096, (1 << 20) + 48, (300 << 20) + 16):
         a = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
-        for mode in (4, 8, 9):
-            b = torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda")
-            torch.cuda.synchronize()      # the library's streams do not order after torch's
-            assert L.msx_probe_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, _stream()) == 0, msx.last_error()
-            torch.cuda.synchronize()
-            assert torch.equal(b[:nbytes], a), (mode, nbytes)
-            assert int(b[nbytes:].count_nonzero()) == 0, (mode, nbytes)     # nothing written past the end
+        b = torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()      # the library's streams do not order after torch's
+        assert L.msx_copy_dev(b.data_ptr(), a.data_ptr(), nbytes, _stream()) == 0, msx.last_error()
+        torch.cuda.synchronize()
+        assert torch.equal(b[:nbytes], a), nbytes
+        assert int(b[nbytes:].count_nonzero()) == 0, nbytes
         del a, b
+
+
+def test_probe_hbm_copy_modes_exact():
+    # the bench-only probe library's copies (bench.py hbm_ceiling_probe): the
+    # 16-B tile copy and the dispatch-order one-wave copy move every byte
+    from msx import probe
+    P = probe.lib()
+    nbytes = (64 << 20) + 16
+    a = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
+    for mode in (probe.COPY, probe.COPY_DISPATCH_ORDER):
+        b = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        assert P.msxp_hbm(mode, a.data_ptr(), b.data_ptr(), nbytes, _stream()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(b, a), mode
 
 
 def test_benchmark_size_fp32_sum_bit_exact(L):
@@ -611,15 +602,16 @@ def test_benchmark_size_fp32_sum_bit_exact(L):
     assert L.msx_reduce_local_dev(a.data_ptr(), b.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
     torch.cuda.synchronize()
     assert torch.equal(b.view(torch.int32), exp.view(torch.int32))
-    # and for every tuning variant
+    # and every measurement variant of the bench-only probe library (the same
+    # combine body in other launch geometries, bench.py --sweep / cold launches)
+    from msx import probe
     ref = b.clone()
-    for v in range(L.msx_tune_variant_count()):
-        assert L.msx_tune_set(v, 0) == 0
+    for name, v in probe.variants().items():
         c = b.clone()
-        assert L.msx_reduce_local_dev(a.data_ptr(), c.data_ptr(), n, C.MPI_FLOAT, C.MPI_SUM, _stream()) == 0
         torch.cuda.synchronize()
-        assert torch.equal(c.view(torch.int32), (ref + a).view(torch.int32)), L.msx_tune_variant_name(v)
-    assert L.msx_tune_set(0, 0) == 0
+        assert probe.lib().msxp_variant_run(v, a.data_ptr(), c.data_ptr(), n, _stream()) == 0, name
+        torch.cuda.synchronize()
+        assert torch.equal(c.view(torch.int32), (ref + a).view(torch.int32)), name
 
 
 NAN_CASES_F32 = [0x7FC00001, 0xFFC00002, 0x7FA00003, 0xFF800000, 0x7F800000, 0x3F800000, 0x80000000, 0x00000001]
@@ -728,14 +720,14 @@ print("DRAM_BAD", len(bad), bad[:5], flush=True)
 
 def test_dram_regime_kernel_every_pair(L, tmp_path):
     """k_combine_dram (operands above the Infinity Cache: one-wave workgroups
-    in dispatch order) for every legal pair: MSX_COMBINE_DRAM_MIN=0 makes a
+    in dispatch order) for every legal pair: MSX_TEST_COMBINE_DRAM_MIN=0 makes a
     child process route every vector-path call through it; bit-exact against
     the oracle, aligned and with an 8-byte common offset (head/tail paths).
     The in-process tests above cover it at its natural sizes (8 GiB fp32,
     4 GiB + 13 B BXOR)."""
     import subprocess
     import sys
-    env = dict(os.environ, MSX_COMBINE_DRAM_MIN="0")
+    env = dict(os.environ, MSX_TEST_COMBINE_DRAM_MIN="0")
     r = subprocess.run([sys.executable, "-c", f"REPO={msx.REPO_ROOT!r}\n" + _DRAM_CHILD], capture_output=True,
                        text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]

@@ -194,7 +194,7 @@ for i, (opn, dtn, count) in enumerate([("MPI_SUM", "MPI_FLOAT", 20001), ("MPI_MA
         elif not (excl and rank == 0):
             check(f"scan host {opn} {dtn} excl={excl}", hr, exp[rank])
 
-# Host (pageable) buffers above MSX_HOST_PIN_MIN: pinned for the call and used
+# Host (pageable) buffers of 1 MiB and more: pinned for the call and used
 # in place by the kernels (allreduce send/recv and in place, reduce_scatter,
 # reduce at the last rank, scan), checked against the reference schedules
 cnt = (3 << 20) // 4 + 5
@@ -335,7 +335,7 @@ if rc: fails.append(f"testall rc={rc} {msx.last_error()}")
 else: check("testall allreduce int", fromdev(ra, xa[rank]), ea[rank])
 
 # Back-to-back stress of the barrier-free allreduce paths (GPU arrival flags,
-# alternating IN / OUT halves; with MSX_RD_FLAGS=0 the host-barrier variants)
+# alternating IN / OUT halves; above MSX_TWO_STEP_MAX the host-barrier schedules)
 # interleaved with the other window users: small rooted reduces (the same
 # arrival-flag path, non-roots push to the root only), a chunked large
 # allreduce (full barrier first), non-blocking calls through the engine
@@ -445,17 +445,16 @@ def _free_port():
 @pytest.mark.parametrize("p,chunk,transport,rd_flags", [(2, None, None, None), (3, 65536, None, None),
                                                         (4, 1 << 20, None, None), (5, None, None, None),
                                                         (3, 65536, "rccl", None), (8, None, None, None),
-                                                        (7, 1 << 20, None, None), (3, None, None, "0"),
-                                                        (4, 65536, None, "0"), (3, None, None, "unfused"),
+                                                        (7, 1 << 20, None, None), (8, None, None, "pageable"),
                                                         (4, None, None, "ts512k"), (6, None, None, None),
-                                                        (3, None, None, "plain_stores+ts"), (4, None, None, "switch0"),
+                                                        (4, None, None, "switch0"),
                                                         (3, None, None, "switch0"), (5, None, None, "switchmax"),
                                                         (5, 65536, None, "switch0"), (7, None, None, "switchmax"),
                                                         (8, None, None, "switch0"), (3, None, None, "staged"),
-                                                        (4, 1 << 20, None, "cached"), (3, None, "rccl_native", None),
+                                                        (3, None, "rccl_native", None),
                                                         (2, None, None, "+ts"), (5, None, None, "+ts"),
                                                         (8, None, None, "+ts"), (3, 65536, None, "+ts"),
-                                                        (8, None, None, "switch0+ts")])
+                                                        (4, 65536, None, "+ts"), (8, None, None, "switch0+ts")])
 def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
     """`+ts`: the GPU-flag Rabenseifner schedules (two-step allreduce / reduce,
     one-step reduce_scatter, flag scan) forced on.  Ranks that share a GPU
@@ -480,8 +479,11 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             env["MSX_CHUNK_BYTES"] = str(chunk)     # many chunks, pieces across block edges
         if transport:
             env["MSX_TRANSPORT"] = transport
-        if mode == "unfused":
-            env["MSX_FUSED_PUSH"] = "0"             # flag path with a separate push launch
+        if mode == "pageable":
+            # the harness's own transfers pageable (tests/_xfer.py) with
+            # sentinels: a hole in a pageable copy is then located by
+            # where_wrong instead of hidden by page-locked transfers
+            env["MSX_TEST_PINNED"] = "0"
         elif mode in ("switch0", "switchmax"):
             # the reference's flat switch points moved (mpid/env.cpp:514-608): at 0
             # every allreduce of >= pof2 elements is Rabenseifner (blocks of a few
@@ -490,20 +492,14 @@ def test_collectives_p_ranks_on_one_gpu(p, chunk, transport, rd_flags):
             v = "0" if mode == "switch0" else "2147483647"
             for k in ("ALLREDUCE_SHORT_MSG", "REDUCE_SHORT_MSG", "REDSCAT_COMMUTATIVE_LONG_MSG"):
                 env["MPICH_DEFAULT_" + k] = v
-        elif mode == "cached":
-            # the documented fallback: cached windows, every engine kernel with
-            # system-scope acquire / release fences
-            env["MSX_WINDOW_CACHED"] = "1"
         elif mode == "staged":
             # host buffers staged through HBM: no call-scoped pinning, no bounce buffers
-            env["MSX_HOST_PIN_MIN"] = str(1 << 40)
-            env["MSX_HOST_BOUNCE_MAX"] = "0"
-        elif mode == "plain_stores":
-            env["MSX_WT_STORES"] = "0"              # two-step pushes / results with plain stores
+            env["MSX_TEST_HOST_PIN_MIN"] = str(1 << 40)
+            env["MSX_TEST_HOST_BOUNCE_MAX"] = "0"
         elif mode == "ts512k":
             env["MSX_TWO_STEP_MAX"] = str(512 << 10)   # two-step and host-barrier Rabenseifner alternate
         elif mode is not None:
-            env["MSX_RD_FLAGS"] = mode          # host-barrier small allreduce / reduce
+            raise AssertionError(f"unknown mode {mode}")
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []

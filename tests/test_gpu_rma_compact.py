@@ -111,7 +111,7 @@ def test_rma_two_level_compact_target_types(p, compact2):
         env.update({"MSX_SIZE": str(p), "MSX_RANK": str(r), "MSX_DEVICE": "0",
                     "MSX_BOOTSTRAP_PORT": str(port), "MSX_BOOTSTRAP_ADDR": "127.0.0.1",
                     "MSX_BOOTSTRAP_TIMEOUT": "180",
-                    "MSX_DT_COMPACT2": compact2})      # 0: the explicit run-list form, for contrast
+                    "MSX_TEST_DT_COMPACT2": compact2})      # 0: the explicit run-list form, for contrast
         procs.append(subprocess.Popen([sys.executable, "-c", f"REPO={REPO!r}\n" + textwrap.dedent(WORKER)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
     results = []
