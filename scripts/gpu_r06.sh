@@ -9,6 +9,8 @@
 #                  (MSX_BENCH_VARIANTS_AT=8) and rank 3's IPC core child hung
 #                  on the host (MSX_BENCH_TEST_HANG), under a 300 s wall budget
 #   MODE prof      rocprofv3 kernel trace + stats of a short N = 1 bench
+#   MODE geom      the combine's launch geometries, warm and cold (scripts/combine_geometry_probe.py)
+#   MODE measure   bench, geom, prof, then rehearse, in one session
 cd "$(dirname "$0")/.." || exit 2
 OUT=${1:-gpurun_out/r06}
 MODE=${2:-test}
@@ -23,7 +25,8 @@ step() {  # step <name> <timeout_s> cmd...
     tail -n 3 "$OUT/$name.log"
     [ $rc -eq 0 ] || { echo "abort after $name (rc=$rc)"; exit $rc; }
 }
-case "$MODE" in
+run_mode() {
+case "$1" in
 test)
     step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
     step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread \
@@ -37,8 +40,21 @@ rehearse)
         step bench_n8_hang 420 python bench.py --gpus 8 --steps 20 --warmup 5
     ;;
 prof)
-    step prof_n1 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o n1 --output-format csv -- \
-        python bench.py --steps 50 --warmup 10 --no-host-path --no-per-op --no-pack --no-collectives --cpu-seconds 1
+    # kernel trace + stats of the default N = 1 bench command, then FETCH_SIZE
+    # and WRITE_SIZE in separate --pmc passes (the guide's HBM section:
+    # FETCH_SIZE x 2 on gfx950) over the device-side tables
+    B="bench.py --no-host-path --no-collectives --cpu-seconds 1"
+    step prof_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv -- python bench.py
+    step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o pmc_fetch --output-format csv -- python $B
+    step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o pmc_write --output-format csv -- python $B
     ;;
-*) echo "unknown mode $MODE"; exit 2 ;;
+geom)
+    step geom 300 python scripts/combine_geometry_probe.py 64,256,1024 3
+    ;;
+measure)
+    run_mode bench && run_mode geom && run_mode prof && run_mode rehearse
+    ;;
+*) echo "unknown mode $1"; exit 2 ;;
 esac
+}
+run_mode "$MODE"
