@@ -144,10 +144,10 @@ int msx_reduce_tree_spec_dev(const void* const* srcs, int P, unsigned pairmask, 
 /* The engine's local copy kernel (the collectives' collect step): dst <- src,
  * `bytes` bytes of device memory, stream-ordered (tests of the copy kernels). */
 int msx_copy_dev(void* dst, const void* src, int64_t bytes, void* stream);
-/* Test hook: pack / unpack and derived-target accumulate geometry.  0 = by
- * size (default: the one-wave tile form when typed span + packed bytes exceed
- * 512 MiB for pack / unpack, always for the accumulate), 1 = always the
- * grid-stride form, 2 = always the tile form.  The measurement kernels (HBM
+/* Test hook: pack / unpack geometry.  0 = by size (default: the one-wave tile
+ * form when typed span + packed bytes exceed 512 MiB), 1 = always the
+ * grid-stride form, 2 = always the tile form.  (The derived-target accumulate
+ * always runs its tile form.)  The measurement kernels (HBM
  * probes, combine variants) live in the bench-only libmsx_probe.so. */
 int msx_tune_pack(int mode);
 

@@ -94,7 +94,7 @@ hipError_t launch_copy_segs(const void* const* src, void* const* dst, const size
                             int nseg, hipStream_t s);
 
 // pack/unpack geometry (test hook, msx_tune_pack): 0 by size, 1 grid-stride
-// form, 2 tile form (msx_pack.hip)
+// form, 2 tile form (msx_pack.hip); the accumulate always runs its tile form
 int pack_tune_set(int mode);
 
 }  // namespace msx

@@ -248,19 +248,11 @@ __device__ __forceinline__ void acc_elem(char* t, const char* p)
     }
 }
 
-template <int OP, class T, bool REG, bool ALIGNED>
-__global__ __launch_bounds__(kPackBlock) void k_dt_acc(CopyArgs a)
-{
-    constexpr int E = (int)sizeof(T);
-    const int64_t stride = (int64_t)gridDim.x * kPackBlock;
-    for (int64_t g = (int64_t)blockIdx.x * kPackBlock + threadIdx.x; g < a.ngran; g += stride)
-        acc_elem<OP, T, ALIGNED>(a.typed + typed_off<E, REG, false>(a, g), a.packed + g * E);
-}
-
-// Tile form of k_dt_acc (the pack kernels' k_dt_pack_tile): one-wave
-// workgroups in dispatch order, kUnroll x 64 consecutive elements each, every
-// operand of the tile loaded before the first combine when the elements are
-// aligned.
+// The derived-target accumulate, in the pack kernels' tile form
+// (k_dt_pack_tile): one-wave workgroups in dispatch order, kUnroll x 64
+// consecutive elements each, every operand of the tile loaded before the first
+// combine when the elements are aligned.  (Rounds 2-5 also carried a
+// grid-stride form; the tile form beat it at every size measured, below.)
 template <int OP, class T, bool REG, bool ALIGNED>
 __global__ __launch_bounds__(64) void k_dt_acc_tile(CopyArgs a)
 {
@@ -339,13 +331,11 @@ int g_pack_mode = 0;
 constexpr size_t kPackTileMin = (size_t)512 << 20;
 size_t pack_tile_min() { return kPackTileMin; }
 
-// A derived-target accumulate always runs k_dt_acc_tile (the grid-stride
-// k_dt_acc only under msx_tune_pack 1, or beyond 2^31 tiles).  Self-targeted
-// fp32 SUM MPI_Accumulate through a 16-B-block vector target type, grid-stride
-// -> tile form, three interleaved rounds (scripts/acc_probe.py,
+// A derived-target accumulate always runs k_dt_acc_tile.  Self-targeted fp32
+// SUM MPI_Accumulate through a 16-B-block vector target type, grid-stride ->
+// tile form, three interleaved rounds (scripts/acc_probe.py,
 // profiles/r03/acc_geometry/): 256 MiB window 144 -> 140 us per call, 1 GiB
 // 663 -> 521 us.
-size_t acc_tile_min() { return 0; }
 
 int pack_tune_set(int mode)
 {
@@ -433,21 +423,14 @@ hipError_t run_acc(const DevLayout& L, int64_t count, const void* packed, void* 
         if (L.regular && (L.blen % E)) return hipErrorInvalidValue;
         const bool aligned = L.align >= (int)alignof(T);
         const bool reg = L.regular != 0;
-        const size_t span = (size_t)(a.ngran / a.gsize) * (size_t)a.extent + (size_t)a.ngran * E;
         const int64_t tiles = (a.ngran + 64 * kUnroll - 1) / (64 * kUnroll);
-        if (tiles <= 0x7fffffffll && (g_pack_mode == 2 || (g_pack_mode == 0 && span > acc_tile_min()))) {
-            const dim3 tg((unsigned)tiles), tb(64);
-            if (reg && aligned) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, true, true>), tg, tb, 0, s, a);
-            else if (reg) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, true, false>), tg, tb, 0, s, a);
-            else if (aligned) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, false, true>), tg, tb, 0, s, a);
-            else hipLaunchKernelGGL((k_dt_acc_tile<OP, T, false, false>), tg, tb, 0, s, a);
-            return hipGetLastError();
-        }
-        const dim3 grid(grid_for(a.ngran)), block(kPackBlock);
-        if (reg && aligned) hipLaunchKernelGGL((k_dt_acc<OP, T, true, true>), grid, block, 0, s, a);
-        else if (reg) hipLaunchKernelGGL((k_dt_acc<OP, T, true, false>), grid, block, 0, s, a);
-        else if (aligned) hipLaunchKernelGGL((k_dt_acc<OP, T, false, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_dt_acc<OP, T, false, false>), grid, block, 0, s, a);
+        if (tiles == 0) return hipSuccess;
+        if (tiles > 0x7fffffffll) return hipErrorInvalidValue;     // > 2^39 elements: beyond any HBM
+        const dim3 tg((unsigned)tiles), tb(64);
+        if (reg && aligned) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, true, true>), tg, tb, 0, s, a);
+        else if (reg) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, true, false>), tg, tb, 0, s, a);
+        else if (aligned) hipLaunchKernelGGL((k_dt_acc_tile<OP, T, false, true>), tg, tb, 0, s, a);
+        else hipLaunchKernelGGL((k_dt_acc_tile<OP, T, false, false>), tg, tb, 0, s, a);
         return hipGetLastError();
     }
 }

@@ -143,7 +143,14 @@ const Variant kVariants[] = {
     {"u4_b256_ntld_tiles", run_variant<4, 256, true, false, 0>},
     {"u1_b64_ntall_rr", run_variant<1, 64, true, true, -1>},
     {"u1_b64_plain_rr", run_variant<1, 64, false, false, -1>},
+    {"u1_b256_ntld_xg8", run_variant<1, 256, true, false, 8>},
     {"u1_b256_ntld_xg32", run_variant<1, 256, true, false, 32>},
+    {"u1_b256_ntld_xg128", run_variant<1, 256, true, false, 128>},
+    {"u1_b64_ntld_tiles", run_variant<1, 64, true, false, 0>},      // one-wave workgroups, XCD-contiguous eighths
+    {"u1_b64_ntld_xg8", run_variant<1, 64, true, false, 8>},
+    {"u1_b64_ntld_xg32", run_variant<1, 64, true, false, 32>},
+    {"u1_b64_ntld_xg128", run_variant<1, 64, true, false, 128>},
+    {"u1_b64_ntld_xg512", run_variant<1, 64, true, false, 512>},
     {"u1_b256_lds", run_variant_lds<256>},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
