@@ -37,7 +37,7 @@ __global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* 
 // Same body for operands far above the 256 MiB Infinity Cache (DRAM-bound):
 // one-wave workgroups in dispatch order (round-robin over XCDs), so the eight
 // XCDs stream neighbouring tiles and DRAM sees three streams instead of 24.
-// Interleaved A/B (scripts/combine_cold_ab.sh, profiles/r03/mall/ab/): 1 GiB
+// Interleaved A/B (profiles/r03/mall/ab/): 1 GiB
 // back to back 5.63 -> 6.06 TB/s, 256 MiB with the cache cold 5.83 -> 6.05,
 // 256 MiB back to back (cache-assisted) 7.12 -> 7.01 -- so it is taken only
 // above kDramMin bytes per operand.
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void k_copy_segs(CopySegs c)
     // workgroup and lane (16-B non-temporal loads), as the HBM probe's copy:
     // the earlier grid-stride form (<= 512 workgroups per segment, 4 loads in
     // flight per lane) copied 256 MiB locally at 5.5 TB/s of traffic, this
-    // form at the probe's ~8 TB/s (scripts/copy_probe.py).  A single segment
+    // form at the probe's ~8 TB/s (profiles/r02/copy/copy_cmp.log).  A single segment
     // (a local copy) takes the XCD-contiguous tile order of the combine.
     const unsigned n = (unsigned)c.n;
     const int sg = (int)(blockIdx.x % n);
@@ -240,7 +240,7 @@ constexpr int kUnroll = 1;
 // Bytes per operand above which the device combine takes k_combine_dram:
 // 16 MiB, where the two operands outgrow the
 // chip's L2 (8 x 4 MiB).  Rounds 1-4 switched only above the 256 MiB Infinity
-// Cache.  fp32 SUM, HIP events, interleaved (scripts/combine_size_sweep.py,
+// Cache.  fp32 SUM, HIP events, interleaved (round-4 size sweep,
 // profiles/r04/combine_geometry/), XCD-contiguous tiles -> dispatch order,
 // GB/s back to back / with the Infinity Cache flushed first:
 //    16 MiB 7077 -> 6560 / 4309 -> 4280 (L2-resident: tiles stay)
@@ -524,7 +524,7 @@ hipError_t launch_push_wait(const void* const* src, void* const* dst, const size
     // workgroups in all: the copy kernel's geometry.  Rounds 1-3 used four
     // granules per lane and 2048 workgroups, which measured the same up to
     // 64 MiB (profiles/r02/copy/push_cmp.log) but 4-7 % slower at c3/c4 sizes
-    // once the chunks were pipelined (scripts/push_geometry_ab.sh in round 4,
+    // once the chunks were pipelined (round-4 A/B,
     // profiles/r04/pushab/).
     constexpr size_t kPushGridCap = 65536;
     size_t gx = (maxb / 16 + 255) / 256;
@@ -551,7 +551,7 @@ hipError_t launch_post_flags(unsigned long long* const* dst, int n, unsigned lon
 
 // Bytes of one local copy above which it takes k_copy_dram: 16 MiB, as the
 // combine (combine_dram_min).  Rounds 1-4 switched above
-// 256 MiB.  HIP events, interleaved (scripts/copy_geometry_probe.py,
+// 256 MiB.  HIP events, interleaved (round-4 probe,
 // profiles/r04/combine_geometry/copy.json), tiles -> dispatch order, GB/s back
 // to back / cache flushed: 16 MiB 4637 -> 4284 / 3277 -> 3452 (tiles stay),
 // 32 MiB 4981 -> 5384 / 4153 -> 4427, 64 MiB 5696 -> 6025 / 4706 -> 5335,

@@ -333,7 +333,7 @@ size_t pack_tile_min() { return kPackTileMin; }
 
 // A derived-target accumulate always runs k_dt_acc_tile.  Self-targeted fp32
 // SUM MPI_Accumulate through a 16-B-block vector target type, grid-stride ->
-// tile form, three interleaved rounds (scripts/acc_probe.py,
+// tile form, three interleaved rounds (round 3,
 // profiles/r03/acc_geometry/): 256 MiB window 144 -> 140 us per call, 1 GiB
 // 663 -> 521 us.
 

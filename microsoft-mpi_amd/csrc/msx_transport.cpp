@@ -1413,7 +1413,7 @@ int get_windows(Transport* tp, Windows* w, bool rd_single = false)
 // Copies of at least kKernelCopyMin bytes within this GPU's memory (HBM
 // buffers, its own window) run on the engine's copy kernel: 256 MiB local
 // copies take 68 us there and 99 us as hipMemcpyAsync's blit
-// (scripts/copy_probe.py in round 2).  Host memory keeps hipMemcpyAsync (DMA).
+// (profiles/r02/copy/copy_cmp.log).  Host memory keeps hipMemcpyAsync (DMA).
 constexpr size_t kKernelCopyMin = (size_t)1 << 20;
 
 int copy_async(void* dst, const void* src, size_t bytes, hipStream_t s)

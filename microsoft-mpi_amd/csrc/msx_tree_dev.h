@@ -312,7 +312,7 @@ template <int OP, class VT> struct VecFn {
 // vectors per lane issued before the first combine, tiles of BLOCK*U vectors.
 // Same association and operand roles as tree_vec / tree_eval.  The generic
 // kernel's runtime leaf tests cost 25 % (p = 8, fp32 SUM, 32 MiB per source:
-// 55 us generic vs 44.6 us here, scripts/tree_probe.py).
+// 55 us generic vs 44.6 us here, profiles/r02/tree_probe.json).
 //
 // MASKED (trees only): the same NL-leaf tree with the non-power-of-two fold's
 // leaf pairs (pairmask: leaf k = f(s[2k], s[2k+1])) taken at run time -- NL,
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(BLOCK) void k_tree(TreeArgs a, T* __restrict__ out,
 // host side: the per-op tree launchers (msx_tree_*.hip)
 // Source bytes of one tree launch above which its loads are non-temporal:
 // the 256 MiB Infinity Cache (MALL) of one MI355X.  p = 8 fp32 SUM, per-source
-// MiB -> us plain / non-temporal (scripts/tree_probe.py in round 3,
+// MiB -> us plain / non-temporal (round 3,
 // profiles/r03/tree/size_sweep/): 32: 46.7 / 47.8, 48: 85.6 / 72.5,
 // 64: 117.4 / 96.6, 128: 224.3 / 189.3.
 constexpr size_t kTreeNtMin = (size_t)256 << 20;

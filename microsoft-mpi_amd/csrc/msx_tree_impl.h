@@ -44,7 +44,7 @@ hipError_t run_tree(const TreeArgs& a, int nsrc, void* out, size_t count, hipStr
 // exceed the Infinity Cache): one-wave workgroups in dispatch order, as
 // k_combine_dram, so the eight XCDs read neighbouring tiles of every source.
 // p = 8 fp32 SUM, uncached sources, two interleaved rounds
-// (scripts/tree_dram_ab.sh, profiles/r03/tree/dram_geometry/): 64 MiB per
+// (profiles/r03/tree/dram_geometry/): 64 MiB per
 // source 96.3 -> 90.9 us (0.78 -> 0.83 of peak), 128 MiB 201.7 -> 186.8 us
 // (0.75 -> 0.81); 64-lane workgroups in XCD-contiguous order and 256-lane ones
 // in dispatch order gain 1-2 % only.
@@ -88,7 +88,7 @@ hipError_t run_tree_sel(const TreeArgs& a, int nsrc, void* out, size_t count, hi
         // loads leaf 0's vectors again for them, which at DRAM sizes costs
         // more than the generic kernel's leaf tests (p = 5/6/7 over 8 leaves,
         // 128 MiB per source: 185/199/215 us masked vs 141/163/179 us generic,
-        // scripts/tree_fold_probe.py, profiles/r04/tree_fold_probe.log)
+        // profiles/r04/tree_fold_probe.log)
         switch (a.P) {
         case 2: return run_tree_fixed<OP, T, VT, NT, 2, U, false, true>(a, nsrc, out, count, s);
         case 4: return run_tree_fixed<OP, T, VT, NT, 4, U, false, true>(a, nsrc, out, count, s);
