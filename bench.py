@@ -716,7 +716,7 @@ def cold_cache_launch(P, torch, dev, stream, src, acc, n, reps=12, mixes=True):
     events; the DRAM-only rate next to the 2R+1W ceiling the same cold method
     gives the copy-like stream mix is what the kernel does without the cache.
     The launches run the default kernel body (k_combine_dram's) under the probe
-    library's symbol k_probe_combine<1, 64, true, false, -1>, so these single
+    library's symbol k_probe_combine<1, 64, true, false, 128>, so these single
     launches stay out of the headline symbol's rocprof average.  Reported
     beside `value`, never part of it."""
     from msx import probe
@@ -757,7 +757,8 @@ def cold_cache_launch(P, torch, dev, stream, src, acc, n, reps=12, mixes=True):
     b2.random_(0, 256)
     torch.cuda.synchronize()
     kinds, mixes = (((probe.COPY, "copy_r1w1", 2), (probe.COPY_DISPATCH_ORDER, "copy_r1w1_dispatch_order", 2),
-                     (probe.READ2, "read2", 2)) if mixes else ()), {}
+                     (probe.COPY_XCD_RUNS, "copy_r1w1_xcd_runs128", 2), (probe.READ2, "read2", 2))
+                    if mixes else ()), {}
     for mode, name, streams in kinds:
         pt = []
         for _ in range(reps):
@@ -777,7 +778,7 @@ def cold_cache_launch(P, torch, dev, stream, src, acc, n, reps=12, mixes=True):
             "warm_single_us": round(wms * 1e3, 1), "cold_probe_GB_s": mixes,
             "method": "median of 12 single launches, each after a 1 GiB read + write pass over other data "
                       "(cold) or right after the previous launch (warm); HIP events on the launch stream; "
-                      "the default kernel body under the probe symbol k_probe_combine<1, 64, true, false, -1>"}
+                      "the default kernel body under the probe symbol k_probe_combine<1, 64, true, false, 128>"}
 
 
 def hbm_ceiling_probe(P, torch, dev, stream, nbytes):
@@ -797,7 +798,7 @@ def hbm_ceiling_probe(P, torch, dev, stream, nbytes):
         b.random_(0, 256)
     out = {}
     for mode, name, streams in ((0, "read2", 2), (3, "read1", 1), (1, "write1", 1), (2, "copy_r1w1", 2),
-                                (9, "copy_r1w1_dispatch_order", 2),
+                                (9, "copy_r1w1_dispatch_order", 2), (10, "copy_r1w1_xcd_runs128", 2),
                                 (6, "write_16of32B", 0.5), (7, "read_16of32B", 0.5)):
         ts = []
         for _ in range(3):
@@ -1233,7 +1234,7 @@ def main():
                                     "cold_method": "median of 12 single launches, each after a 1 GiB read + "
                                                    "write pass over other data (flushes the 256 MiB MALL); "
                                                    "the default body (k_combine_dram's) under the bench-only "
-                                                   "symbol k_probe_combine<1, 64, true, false, -1>"})
+                                                   "symbol k_probe_combine<1, 64, true, false, 128>"})
         if host is not None:
             out["host_path"] = host
         if multi_host is not None:
@@ -1242,7 +1243,7 @@ def main():
         # all peers' windows at once: the links' measured per-GPU outbound
         # rate); every plane's busBW is read against it.  Null when the ranks
         # share a GPU (no byte crosses xGMI there) or the probe did not run.
-        shared = bool(coll and coll.get("gpu_shared"))
+        shared = not distinct or bool(coll and coll.get("gpu_shared"))
         links = None if shared else ((coll or {}).get("peer_write_probe") or {}).get("outbound_GB_s_per_gpu")
 
         def summarize(c):

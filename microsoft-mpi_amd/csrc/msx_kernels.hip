@@ -34,18 +34,23 @@ __global__ __launch_bounds__(BLOCK) void k_combine(const T* __restrict__ in, T* 
     combine_body<OP, T, VT, UNROLL, BLOCK, NTLD, NTST>(in, io, head, nvec, tail);
 }
 
-// Same body for operands far above the 256 MiB Infinity Cache (DRAM-bound):
-// one-wave workgroups in dispatch order (round-robin over XCDs), so the eight
-// XCDs stream neighbouring tiles and DRAM sees three streams instead of 24.
-// Interleaved A/B (profiles/r03/mall/ab/): 1 GiB
-// back to back 5.63 -> 6.06 TB/s, 256 MiB with the cache cold 5.83 -> 6.05,
-// 256 MiB back to back (cache-assisted) 7.12 -> 7.01 -- so it is taken only
-// above kDramMin bytes per operand.
+// Same body for operands beyond the L2 (DRAM-bound): one-wave workgroups,
+// and XCD x owns interleaved runs of kDramRun consecutive 1-KiB tiles (128 KiB
+// of each operand), so the eight XCDs stream eight neighbouring 128-KiB
+// windows: per-XCD L2 locality and few concurrent DRAM streams at once.
+// Rounds 4-5 ran the same workgroups in plain dispatch order (round-robin over
+// XCDs).  fp32 SUM, interleaved, 5 rounds, us back to back / cache flushed
+// (scripts/combine_geometry_probe.py, profiles/r06/geometry/), dispatch
+// order -> runs of 128: 128 MiB 61.1 -> 58.3 / 70.4 -> 66.4, 256 MiB 118.3 ->
+// 113.4 / 137.2 -> 130.3, 512 MiB 280.9 -> 264.5 / 274.2 -> 262.2, 2 GiB
+// 1096 -> 1061 / 1093 -> 1059; 1 GiB within 0.5 %.  Runs of 64, 256 and 512
+// tiles, 128-lane workgroups and XCD-contiguous eighths do not beat it.
+constexpr int kDramRun = 128;
 template <int OP, class T, class VT, int BLOCK, bool NTLD, bool NTST>
 __global__ __launch_bounds__(BLOCK) void k_combine_dram(const T* __restrict__ in, T* __restrict__ io,
                                                         size_t head, size_t nvec, size_t tail)
 {
-    combine_body<OP, T, VT, 1, BLOCK, NTLD, NTST, -1>(in, io, head, nvec, tail);
+    combine_body<OP, T, VT, 1, BLOCK, NTLD, NTST, kDramRun>(in, io, head, nvec, tail);
 }
 
 // Same body, launched by the host-memory path of MPI_Reduce_local (pinned

@@ -181,14 +181,20 @@ struct TreeArgs {
     unsigned done_launches;
     PostFlags done_flags;
     // tile order: 0 = XCD-contiguous eighths (the default), -1 = dispatch
-    // order (the one-wave DRAM-regime geometry, msx_tree_impl.h)
+    // order (the one-wave DRAM-regime geometry, msx_tree_impl.h), G > 0 = XCD
+    // x owns interleaved runs of G consecutive tiles (combine_tile's orders)
     int xg;
 };
 
 // Workgroup b of nb -> tile under TreeArgs::xg (a bijection on [0, nb)).
 __device__ __forceinline__ size_t tree_tile(int xg, unsigned b, unsigned nb)
 {
-    return xg == 0 ? xcd_tile(b, nb) : b;
+    if (xg == 0) return xcd_tile(b, nb);
+    if (xg < 0) return b;
+    const unsigned g = (unsigned)xg, full = (nb / (8u * g)) * (8u * g);
+    if (b >= full) return b;
+    const unsigned x = b & 7, j = b >> 3;
+    return ((size_t)(j / g) * 8 + x) * g + (j % g);
 }
 
 // End of a tree workgroup when the launch posts result-ready flags: the

@@ -14,7 +14,7 @@ from . import PKG_ROOT
 PROBE_PATH = os.path.join(PKG_ROOT, "lib", "libmsx_probe.so")
 
 # msxp_hbm modes
-READ2, WRITE1, COPY, READ1, GAP_STORE, GAP_LOAD, COPY_DISPATCH_ORDER = 0, 1, 2, 3, 6, 7, 9
+READ2, WRITE1, COPY, READ1, GAP_STORE, GAP_LOAD, COPY_DISPATCH_ORDER, COPY_XCD_RUNS = 0, 1, 2, 3, 6, 7, 9, 10
 
 _lib = None
 
@@ -32,7 +32,8 @@ def lib():
                             ("msxp_free", i, [p]),
                             ("msxp_variant_count", i, []),
                             ("msxp_variant_name", ctypes.c_char_p, [i]),
-                            ("msxp_variant_run", i, [i, p, p, i64, p])):
+                            ("msxp_variant_run", i, [i, p, p, i64, p]),
+                            ("msxp_tree8", i, [ctypes.POINTER(p), p, i64, i, p])):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

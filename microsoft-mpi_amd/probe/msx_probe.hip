@@ -4,17 +4,21 @@
 // to what this GPU's HBM delivers:
 //   * msxp_hbm: other stream mixes in the default combine's launch geometry
 //     (16 B per lane, 256-lane workgroups, one tile each, XCD-contiguous,
-//     non-temporal loads), plus a copy in k_combine_dram's one-wave
-//     dispatch-order geometry and 16-of-32-byte gapped loads / stores;
+//     non-temporal loads), plus copies with one-wave workgroups in dispatch
+//     order (k_copy_dram's) and in XCD runs of 128 tiles (k_combine_dram's),
+//     and 16-of-32-byte gapped loads / stores;
 //   * msxp_variant_*: the fp32 SUM combine body (msx_combine_dev.h, the exact
 //     device code of k_combine / k_combine_dram) in other launch geometries,
 //     for the tuning sweep, and the default DRAM-regime body under its own
 //     symbol (k_probe_combine<..., 64, ..., -1>) so single cold-cache launches
-//     stay out of the headline kernel's rocprof statistics.
+//     stay out of the headline kernel's rocprof statistics;
+//   * msxp_tree8: the product's 8-source DRAM-regime tree (k_tree, fp32 SUM,
+//     non-temporal loads, one-wave workgroups) in another tile order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "msx_combine_dev.h"
+#include "msx_tree_dev.h"
 
 #define MSXP_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -53,10 +57,12 @@ __global__ __launch_bounds__(256) void k_probe(const u32x4* __restrict__ a, u32x
     }
 }
 
-// copy a -> b in k_combine_dram's geometry: one-wave workgroups, dispatch order
+// copy a -> b with one-wave workgroups in tile order XG (-1 dispatch order,
+// k_copy_dram's; 128 = XCD runs of 128 tiles, k_combine_dram's)
+template <int XG>
 __global__ __launch_bounds__(64) void k_probe_copy_rr(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t nvec)
 {
-    const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    const size_t i = combine_tile<XG>(blockIdx.x, gridDim.x) * 64 + threadIdx.x;
     if (i < nvec) b[i] = ld<true>(a + i);
 }
 
@@ -133,9 +139,10 @@ struct Variant {
 };
 
 // index 0: the product's default body above 16 MiB per operand (k_combine_dram:
-// one-wave workgroups in dispatch order) under the probe symbol
+// one-wave workgroups, XCD runs of 128 tiles) under the probe symbol
 const Variant kVariants[] = {
-    {"default_body_probe", run_variant<1, 64, true, false, -1>},
+    {"default_body_probe", run_variant<1, 64, true, false, 128>},
+    {"u1_b64_ntld_rr", run_variant<1, 64, true, false, -1>},          // rounds 4-5 default above 16 MiB
     {"u1_b256_ntld_tiles", run_variant<1, 256, true, false, 0>},      // rounds 1-4 default: XCD-contiguous tiles
     {"u1_b256_ntld_rr", run_variant<1, 256, true, false, -1>},
     {"u1_b128_ntld_rr", run_variant<1, 128, true, false, -1>},
@@ -149,8 +156,12 @@ const Variant kVariants[] = {
     {"u1_b64_ntld_tiles", run_variant<1, 64, true, false, 0>},      // one-wave workgroups, XCD-contiguous eighths
     {"u1_b64_ntld_xg8", run_variant<1, 64, true, false, 8>},
     {"u1_b64_ntld_xg32", run_variant<1, 64, true, false, 32>},
-    {"u1_b64_ntld_xg128", run_variant<1, 64, true, false, 128>},
+    {"u1_b64_ntld_xg64", run_variant<1, 64, true, false, 64>},
+    {"u1_b64_ntld_xg256", run_variant<1, 64, true, false, 256>},
     {"u1_b64_ntld_xg512", run_variant<1, 64, true, false, 512>},
+    {"u1_b128_ntld_xg64", run_variant<1, 128, true, false, 64>},
+    {"u1_b128_ntld_xg128", run_variant<1, 128, true, false, 128>},
+    {"u1_b64_ntall_xg128", run_variant<1, 64, true, true, 128>},
     {"u1_b256_lds", run_variant_lds<256>},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -166,11 +177,12 @@ MSXP_EXPORT int msxp_hbm(int mode, const void* a, void* b, int64_t bytes, void* 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const u32x4* va = static_cast<const u32x4*>(a);
     u32x4* vb = static_cast<u32x4*>(b);
-    if (mode == 9) {
+    if (mode == 9 || mode == 10) {
         const size_t nv = (size_t)bytes / 16, grid = (nv + 63) / 64;
         if (grid == 0) return 0;
         if (grid > 0x7fffffffu) return 1;
-        hipLaunchKernelGGL(k_probe_copy_rr, dim3((unsigned)grid), dim3(64), 0, s, va, vb, nv);
+        if (mode == 9) hipLaunchKernelGGL(k_probe_copy_rr<-1>, dim3((unsigned)grid), dim3(64), 0, s, va, vb, nv);
+        else hipLaunchKernelGGL(k_probe_copy_rr<128>, dim3((unsigned)grid), dim3(64), 0, s, va, vb, nv);
         return hipGetLastError() == hipSuccess ? 0 : 2;
     }
     const size_t nvec = (mode >= 6) ? (size_t)bytes / 32 : (size_t)bytes / 16;
@@ -211,4 +223,29 @@ MSXP_EXPORT int msxp_variant_run(int v, const void* in, void* inout, int64_t cou
 {
     if (v < 0 || v >= kNumVariants || count < 0 || !in || !inout) return 1;
     return kVariants[v].fn(in, inout, (size_t)count, static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : 2;
+}
+
+// out[i] = ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7)) over n fp32 (16-byte aligned
+// pointers, n a multiple of 4): the product's k_tree<SUM, float, float, 64,
+// NT, 8 leaves> -- the tree above 256 MiB of sources -- with tile order xg
+// (-1 dispatch order, the product's; 0 XCD-contiguous; G > 0 XCD runs of G)
+MSXP_EXPORT int msxp_tree8(const void* const* srcs, void* out, int64_t n, int xg, void* stream)
+{
+    using namespace msx::dev;
+    if (!srcs || !out || n <= 0 || (n & 3)) return 1;
+    TreeArgs a{};
+    for (int k = 0; k < 8; ++k) {
+        if (!srcs[k] || ((uintptr_t)srcs[k] & 15)) return 1;
+        a.s[2 * k] = a.s[2 * k + 1] = srcs[k];
+    }
+    if ((uintptr_t)out & 15) return 1;
+    a.P = 8;
+    a.nleaves = 8;
+    a.xg = xg;
+    a.done_launches = 1;
+    const size_t nvec = (size_t)n / 4, grid = (nvec + 63) / 64;
+    if (grid > 0x7fffffffu) return 1;
+    hipLaunchKernelGGL((k_tree<msx::O_SUM, float, float, 64, true, 8, 1, false, false>), dim3((unsigned)grid), dim3(64), 0,
+                       static_cast<hipStream_t>(stream), a, static_cast<float*>(out), nvec, (size_t)0, 1);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
 }

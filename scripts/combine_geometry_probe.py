@@ -81,6 +81,37 @@ for mib in sizes:
         res[name] = {"warm_us": round(w * 1e3, 1), "cold_us": round(c * 1e3, 1),
                      "warm_frac": round(12 * n / w / 1e6 / 8000, 4), "cold_frac": round(12 * n / c / 1e6 / 8000, 4)}
         print(f"{mib} MiB {name}: warm {w * 1e3:.1f} us cold {c * 1e3:.1f} us", file=sys.stderr)
+    # the local copy (1R1W) in the same orders: k_copy_segs' 256-lane tiles,
+    # k_copy_dram's dispatch order, XCD runs of 128 tiles
+    copies = {"copy_tiles256": probe.COPY, "copy_dispatch": probe.COPY_DISPATCH_ORDER,
+              "copy_xcd_runs128": probe.COPY_XCD_RUNS}
+    cw, cc = {k: [] for k in copies}, {k: [] for k in copies}
+    for _ in range(rounds):
+        for name, mode in copies.items():
+            fn = lambda: P.msxp_hbm(mode, a.data_ptr(), b.data_ptr(), n * 4, sp)
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(10):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            cw[name].append(e0.elapsed_time(e1) / 10)
+            ts = []
+            for _ in range(5):
+                flush_cache()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                fn()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            cc[name].append(sorted(ts)[2])
+    for name in copies:
+        w, c = sorted(cw[name])[len(cw[name]) // 2], sorted(cc[name])[len(cc[name]) // 2]
+        res[name] = {"warm_us": round(w * 1e3, 1), "cold_us": round(c * 1e3, 1),
+                     "warm_frac": round(8 * n / w / 1e6 / 8000, 4), "cold_frac": round(8 * n / c / 1e6 / 8000, 4)}
     out[str(mib)] = res
     del a, b
     torch.cuda.empty_cache()

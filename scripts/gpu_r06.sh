@@ -11,6 +11,10 @@
 #   MODE prof      rocprofv3 kernel trace + stats of a short N = 1 bench
 #   MODE geom      the combine's launch geometries, warm and cold (scripts/combine_geometry_probe.py)
 #   MODE measure   bench, geom, prof, then rehearse, in one session
+#   MODE geom2     the geometry sweep at 8 MiB - 2 GiB, 5 rounds
+#   MODE full      test, bench, geom2, treegeom, prof
+#   MODE rehearse_clean  N = 8 on the one GPU, default sequence, nothing hung
+#   MODE treegeom  the 8-source DRAM-regime tree in other tile orders (scripts/tree_geometry_probe.py)
 cd "$(dirname "$0")/.." || exit 2
 OUT=${1:-gpurun_out/r06}
 MODE=${2:-test}
@@ -51,8 +55,22 @@ prof)
 geom)
     step geom 300 python scripts/combine_geometry_probe.py 64,256,1024 3
     ;;
+geom2)
+    step geom2 400 python scripts/combine_geometry_probe.py 8,16,32,64,128,256,512,1024,2048 5
+    ;;
+treegeom)
+    step treegeom 300 python scripts/tree_geometry_probe.py 32,64,128 3
+    ;;
+rehearse_clean)
+    # the default N = 8 sequence with every rank on this box's one GPU (no hang)
+    MSX_BENCH_VARIANTS_AT=8 MSX_BENCH_LOG=$OUT/coll_n8_clean.log \
+        step bench_n8_clean 500 python bench.py --gpus 8 --steps 20 --warmup 5
+    ;;
 measure)
     run_mode bench && run_mode geom && run_mode prof && run_mode rehearse
+    ;;
+full)
+    run_mode test && run_mode bench && run_mode geom2 && run_mode treegeom && run_mode prof
     ;;
 *) echo "unknown mode $1"; exit 2 ;;
 esac
