@@ -610,7 +610,7 @@ def per_op_roofline(L, C, torch, dev, stream, nbytes):
     out["tree8/MPI_SUM/MPI_FLOAT"] = entry(time_tree())
     # HBM bytes per launch from the committed PMC passes (16-B streaming loads:
     # FETCH_SIZE doubled per the gfx950 calibration), against (p + 1) * 32 MiB
-    raw = pmc_raw("k_tree<3, float, float, 256, false, false, 8, 1, false>")
+    raw = pmc_raw("k_tree<3, float, float, 256, false, 8, 1, false, false>")
     if raw:
         out["tree8/MPI_SUM/MPI_FLOAT"].update(
             {"pmc_raw_kib": raw, "traffic": int((2 * raw["FETCH_SIZE"] + raw["WRITE_SIZE"]) * 1024),
