@@ -286,6 +286,165 @@ def run_multi_host_child(n, timeout=60.0):
         return {"error": str(e)}
 
 
+class ChildRunners:
+    """The N > 1 child processes run_children starts (tests substitute fakes)."""
+    collectives = staticmethod(run_collectives_child)
+    rccl_allreduce = staticmethod(rccl_native_allreduce)
+    multi_host = staticmethod(run_multi_host_child)
+
+
+def run_children(dist, world, rank, local, scale, n, distinct, no_host_path, runners=ChildRunners):
+    """The collective configs and the node-level host split at N > 1, in child
+    processes, each under a time limit cut to the remaining wall budget
+    (WALL_BUDGET_S, CHILD_ORDER); rank 0's clock decides, so every rank runs
+    and skips the same children.  Collective over `dist` (every rank calls
+    it); returns rank 0's results (other ranks: their own, unused).
+    distinct: one GPU per rank (the RCCL planes need it)."""
+    import torch
+    coll = coll_rccl = coll_native = rccl_native = c3_variants = coll_extras = multi_host = None
+    budget = {"wall_budget_s": WALL_BUDGET_S, "reserve_s": RESERVE_S, "child_cap_s": CHILD_CAP_S, "steps": []}
+
+    def allot(name, collective=True):
+        """Seconds child `name` may run (None: skipped), from rank 0's clock."""
+        el = [time.time() - T_START]
+        if collective:
+            dist.broadcast_object_list(el, src=0)
+        t = child_timeout(name, el[0])
+        step = {"name": name, "start_s": round(el[0], 1), "timeout_s": None if t is None else round(t, 1)}
+        if t is None:
+            step["skipped"] = "wall budget"
+        budget["steps"].append(step)
+        return t
+
+    def took(res):
+        budget["steps"][-1]["elapsed_s"] = round(time.time() - T_START - budget["steps"][-1]["start_s"], 1)
+        if isinstance(res, dict) and "error" in res:
+            budget["steps"][-1]["error"] = True
+        return res
+
+    def collect(transport, name, parts, extra=None, tag="", port_off=0):
+        t = allot(name)
+        if t is None:
+            return {"skipped": "wall budget"} if rank == 0 else None
+        mine = runners.collectives(world, rank, local, scale, transport, extra, tag, port_off,
+                                     parts=parts, timeout=t)
+        errs = [None] * world
+        dist.all_gather_object(errs, mine.get("error"))      # every rank's structured error
+        res = mine if rank == 0 else None
+        if rank == 0 and any(e is not None for e in errs):
+            res["errors"] = [dict(e, rank=r) if isinstance(e, dict) else {"rank": r, "text": e}
+                             for r, e in enumerate(errs) if e is not None]
+            res.setdefault("error", res["errors"][0])
+        return took(res) if rank == 0 else None
+    # 1. the default data plane's headline configs (and the all-peer probe)
+    coll = collect("ipc", "ipc_core", "core")
+    if distinct:
+        # 2. the RCCL send/recv plane, then this library's MPI calls on
+        # RCCL's own collectives (MSX_TRANSPORT=rccl_native: ncclAllReduce /
+        # ncclReduce / ncclReduceScatter where the pair maps, RCCL order;
+        # the harness's integer-valued inputs make every order exact, so
+        # `correct` still checks in full)
+        coll_rccl = collect("rccl", "rccl_core", "core")
+        coll_native = collect("rccl_native", "rccl_native_core", "core")
+        # 3. RCCL's own fp32 allreduce (torch.distributed), the xGMI reference point
+        t = allot("rccl_allreduce")
+        if t is not None:
+            mine = runners.rccl_allreduce(world, rank, local, scale, timeout=t)
+            ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            rccl_native = mine if rank == 0 else None
+            if rank == 0:
+                if not ok.item() and "error" not in rccl_native:
+                    rccl_native["error"] = "a non-zero rank's child failed"
+                took(rccl_native)
+    # 4. the other schedule of c3 / c4 (IPC plane) at N = 8, or at the N
+    # that MSX_BENCH_VARIANTS_AT names (a rehearsal on fewer GPUs); skipped
+    # when the default IPC run failed (it would only repeat the failure)
+    ipc_failed = [rank == 0 and (coll is None or "error" in coll or "skipped" in coll)]
+    dist.broadcast_object_list(ipc_failed, src=0)
+    if world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")):
+        if ipc_failed[0]:
+            c3_variants = {"skipped": "the default IPC collectives child failed (see collectives.error)"}
+        else:
+            c3_variants = {}
+            for vi, (name, extra) in enumerate(C3_VARIANTS):
+                mine = collect("ipc", "variant_" + name, "c3c4", extra, tag="_" + name, port_off=200 + 11 * vi)
+                if rank == 0:
+                    ent = {"env": extra}
+                    if "skipped" in mine:
+                        ent["skipped"] = mine["skipped"]
+                    for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4")):
+                        v = mine.get(key) or {}
+                        ent[tag] = {k: v.get(k) for k in ("seconds", "busbw_GB_s", "correct") if k in v}
+                    if mine.get("errors"):
+                        ent["errors"] = mine["errors"]
+                    c3_variants[name] = ent
+    # 5. the IPC plane's remaining configs (curve, host memory, rooted
+    # reduce, scan, one-sided accumulate)
+    coll_extras = collect("ipc", "ipc_extras", "extras", tag="_extras", port_off=300)
+    # 6. SURVEY §8(e) strong-scaled local reduce on the MPI path's host
+    # buffers: one 256 MiB fp32 MPI_SUM vector split over every GPU of the
+    # node, each GPU over its own PCIe link (msx_reduce_local_multi),
+    # against the same call on one GPU -- rank 0 only, while the other
+    # ranks wait at the closing barrier
+    if rank == 0 and not no_host_path:
+        t = allot("multi_host", collective=False)
+        multi_host = took(runners.multi_host(n, timeout=t)) if t is not None else {"skipped": "wall budget"}
+    return {"coll": coll, "coll_rccl": coll_rccl, "coll_native": coll_native, "rccl_native": rccl_native,
+            "c3_variants": c3_variants, "coll_extras": coll_extras, "multi_host": multi_host, "budget": budget,
+            "distinct": distinct}
+
+
+def collectives_report(kids):
+    """Rank 0's JSON fields for run_children's results: per data plane, c3-c5
+    correct / busBW and the fraction of the links' measured rate (the IPC
+    child's all-peer write probe: every GPU writing into all peers' windows at
+    once); null fractions when the ranks share a GPU (no byte crosses xGMI)
+    or the probe did not run."""
+    coll, coll_rccl, coll_native = kids["coll"], kids["coll_rccl"], kids["coll_native"]
+    rccl_native, budget = kids["rccl_native"], kids["budget"]
+    out = {}
+    shared = not kids["distinct"] or bool(coll and coll.get("gpu_shared"))
+    links = None if shared else ((coll or {}).get("peer_write_probe") or {}).get("outbound_GB_s_per_gpu")
+
+    def summarize(c):
+        if not c:
+            return None
+        sm = {}
+        for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4"),
+                         ("c5_iallreduce_band_u64", "c5")):
+            v = c.get(key)
+            if v:
+                sm[tag] = {k: v.get(k) for k in ("correct", "busbw_GB_s", "seconds", "t_comm_s") if k in v}
+                bw = v.get("busbw_GB_s")
+                sm[tag]["busbw_frac_measured_links"] = round(bw / links, 3) if (bw and links) else None
+        for k in ("error", "skipped"):
+            if k in c:
+                sm[k] = c[k]
+        return sm
+    if coll is not None or coll_rccl is not None:
+        native = None
+        if rccl_native is not None:
+            bw = rccl_native.get("busbw_GB_s")
+            native = {k: rccl_native.get(k) for k in ("correct", "busbw_GB_s", "error", "skipped") if k in rccl_native}
+            native["busbw_frac_measured_links"] = round(bw / links, 3) if (bw and links) else None
+        out["collectives_summary"] = {"plane": "hbm (ranks share one GPU)" if shared else "xgmi",
+                                      "measured_links_GB_s_per_gpu": links,
+                                      "ipc": summarize(coll), "rccl": summarize(coll_rccl),
+                                      "rccl_native": summarize(coll_native),
+                                      "rccl_own_allreduce_f32": native}
+    if budget["steps"]:
+        budget["wall_s_at_json"] = round(time.time() - T_START, 1)
+        out["wall_budget"] = budget
+    for key, name in (("coll_extras", "collectives_extras"), ("coll", "collectives"),
+                      ("coll_rccl", "collectives_rccl_transport"), ("coll_native", "collectives_rccl_native_transport"),
+                      ("rccl_native", "rccl_native_allreduce_f32"), ("c3_variants", "c3_c4_engine_variants"),
+                      ("multi_host", "host_path_multi_gpu")):
+        if kids[key]:
+            out[name] = kids[key]
+    return out
+
+
 def traffic_from_profiles(kernel_substr="k_combine_dram<3, float, float, 64, true, false>"):
     """Per-launch HBM bytes of the default fp32 SUM kernel from the newest
     committed rocprofv3 PMC collection (profiles/<round>/pmc_*counter_collection.csv,
@@ -1033,100 +1192,11 @@ def main():
     elapsed, kern_ms_max = float(t[0]), float(t[1])
 
     # N > 1: the collective configs in child MPI processes (not part of
-    # `value`), each under a time limit cut to the remaining wall budget
-    # (WALL_BUDGET_S above); rank 0's clock decides, so every rank runs and
-    # skips the same children.  Each rank reports whether its child succeeded.
-    coll = coll_rccl = coll_native = rccl_native = c3_variants = coll_extras = multi_host = None
-    budget = {"wall_budget_s": WALL_BUDGET_S, "reserve_s": RESERVE_S, "child_cap_s": CHILD_CAP_S, "steps": []}
-    distinct = torch.cuda.device_count() >= world      # one GPU per rank (RCCL needs it)
-
-    def allot(name, collective=True):
-        """Seconds child `name` may run (None: skipped), from rank 0's clock."""
-        el = [time.time() - T_START]
-        if collective:
-            dist.broadcast_object_list(el, src=0)
-        t = child_timeout(name, el[0])
-        step = {"name": name, "start_s": round(el[0], 1), "timeout_s": None if t is None else round(t, 1)}
-        if t is None:
-            step["skipped"] = "wall budget"
-        budget["steps"].append(step)
-        return t
-
-    def took(res):
-        budget["steps"][-1]["elapsed_s"] = round(time.time() - T_START - budget["steps"][-1]["start_s"], 1)
-        if isinstance(res, dict) and "error" in res:
-            budget["steps"][-1]["error"] = True
-        return res
-
+    # `value`), under one wall budget (run_children)
+    kids = None
     if world > 1 and not args.no_collectives:
-        def collect(transport, name, parts, extra=None, tag="", port_off=0):
-            t = allot(name)
-            if t is None:
-                return {"skipped": "wall budget"} if rank == 0 else None
-            mine = run_collectives_child(world, rank, local, args.coll_scale, transport, extra, tag, port_off,
-                                         parts=parts, timeout=t)
-            errs = [None] * world
-            dist.all_gather_object(errs, mine.get("error"))      # every rank's structured error
-            res = mine if rank == 0 else None
-            if rank == 0 and any(e is not None for e in errs):
-                res["errors"] = [dict(e, rank=r) if isinstance(e, dict) else {"rank": r, "text": e}
-                                 for r, e in enumerate(errs) if e is not None]
-                res.setdefault("error", res["errors"][0])
-            return took(res) if rank == 0 else None
-        # 1. the default data plane's headline configs (and the all-peer probe)
-        coll = collect("ipc", "ipc_core", "core")
-        if distinct:
-            # 2. the RCCL send/recv plane, then this library's MPI calls on
-            # RCCL's own collectives (MSX_TRANSPORT=rccl_native: ncclAllReduce /
-            # ncclReduce / ncclReduceScatter where the pair maps, RCCL order;
-            # the harness's integer-valued inputs make every order exact, so
-            # `correct` still checks in full)
-            coll_rccl = collect("rccl", "rccl_core", "core")
-            coll_native = collect("rccl_native", "rccl_native_core", "core")
-            # 3. RCCL's own fp32 allreduce (torch.distributed), the xGMI reference point
-            t = allot("rccl_allreduce")
-            if t is not None:
-                mine = rccl_native_allreduce(world, rank, local, args.coll_scale, timeout=t)
-                ok = torch.tensor([0 if "error" in mine else 1], dtype=torch.int32)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-                rccl_native = mine if rank == 0 else None
-                if rank == 0:
-                    if not ok.item() and "error" not in rccl_native:
-                        rccl_native["error"] = "a non-zero rank's child failed"
-                    took(rccl_native)
-        # 4. the other schedule of c3 / c4 (IPC plane) at N = 8, or at the N
-        # that MSX_BENCH_VARIANTS_AT names (a rehearsal on fewer GPUs); skipped
-        # when the default IPC run failed (it would only repeat the failure)
-        ipc_failed = [rank == 0 and (coll is None or "error" in coll or "skipped" in coll)]
-        dist.broadcast_object_list(ipc_failed, src=0)
-        if world == int(os.environ.get("MSX_BENCH_VARIANTS_AT", "8")):
-            if ipc_failed[0]:
-                c3_variants = {"skipped": "the default IPC collectives child failed (see collectives.error)"}
-            else:
-                c3_variants = {}
-                for vi, (name, extra) in enumerate(C3_VARIANTS):
-                    mine = collect("ipc", "variant_" + name, "c3c4", extra, tag="_" + name, port_off=200 + 11 * vi)
-                    if rank == 0:
-                        ent = {"env": extra}
-                        if "skipped" in mine:
-                            ent["skipped"] = mine["skipped"]
-                        for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4")):
-                            v = mine.get(key) or {}
-                            ent[tag] = {k: v.get(k) for k in ("seconds", "busbw_GB_s", "correct") if k in v}
-                        if mine.get("errors"):
-                            ent["errors"] = mine["errors"]
-                        c3_variants[name] = ent
-        # 5. the IPC plane's remaining configs (curve, host memory, rooted
-        # reduce, scan, one-sided accumulate)
-        coll_extras = collect("ipc", "ipc_extras", "extras", tag="_extras", port_off=300)
-        # 6. SURVEY §8(e) strong-scaled local reduce on the MPI path's host
-        # buffers: one 256 MiB fp32 MPI_SUM vector split over every GPU of the
-        # node, each GPU over its own PCIe link (msx_reduce_local_multi),
-        # against the same call on one GPU -- rank 0 only, while the other
-        # ranks wait at the closing barrier
-        if rank == 0 and not args.no_host_path:
-            t = allot("multi_host", collective=False)
-            multi_host = took(run_multi_host_child(n, timeout=t)) if t is not None else {"skipped": "wall budget"}
+        kids = run_children(dist, world, rank, local, args.coll_scale, n, torch.cuda.device_count() >= world,
+                            args.no_host_path)
     # host-memory path (the MPI buffers start and end in host memory): measured
     # on rank 0 only, reported beside the device-resident value.
     host = None
@@ -1237,58 +1307,8 @@ def main():
                                                    "symbol k_probe_combine<1, 64, true, false, 128>"})
         if host is not None:
             out["host_path"] = host
-        if multi_host is not None:
-            out["host_path_multi_gpu"] = multi_host
-        # the all-peer write probe of the IPC child (every GPU writing into
-        # all peers' windows at once: the links' measured per-GPU outbound
-        # rate); every plane's busBW is read against it.  Null when the ranks
-        # share a GPU (no byte crosses xGMI there) or the probe did not run.
-        shared = not distinct or bool(coll and coll.get("gpu_shared"))
-        links = None if shared else ((coll or {}).get("peer_write_probe") or {}).get("outbound_GB_s_per_gpu")
-
-        def summarize(c):
-            """c3-c5 of one data plane at a glance: correct, busBW, the xGMI
-            fraction against the measured links (null on a shared GPU)."""
-            if not c:
-                return None
-            sm = {}
-            for key, tag in (("c3_allreduce_sum_f32", "c3"), ("c4_reduce_scatter_max_f64", "c4"),
-                             ("c5_iallreduce_band_u64", "c5")):
-                v = c.get(key)
-                if v:
-                    sm[tag] = {k: v.get(k) for k in ("correct", "busbw_GB_s", "seconds", "t_comm_s") if k in v}
-                    bw = v.get("busbw_GB_s")
-                    sm[tag]["busbw_frac_measured_links"] = round(bw / links, 3) if (bw and links) else None
-            for k in ("error", "skipped"):
-                if k in c:
-                    sm[k] = c[k]
-            return sm
-        if coll is not None or coll_rccl is not None:
-            native = None
-            if rccl_native is not None:
-                bw = rccl_native.get("busbw_GB_s")
-                native = {k: rccl_native.get(k) for k in ("correct", "busbw_GB_s", "error") if k in rccl_native}
-                native["busbw_frac_measured_links"] = round(bw / links, 3) if (bw and links) else None
-            out["collectives_summary"] = {"plane": "hbm (ranks share one GPU)" if shared else "xgmi",
-                                          "measured_links_GB_s_per_gpu": links,
-                                          "ipc": summarize(coll), "rccl": summarize(coll_rccl),
-                                          "rccl_native": summarize(coll_native),
-                                          "rccl_own_allreduce_f32": native}
-        if budget["steps"]:
-            budget["wall_s_at_json"] = round(time.time() - T_START, 1)
-            out["wall_budget"] = budget
-        if coll_extras is not None:
-            out["collectives_extras"] = coll_extras
-        if coll is not None:
-            out["collectives"] = coll
-        if coll_rccl is not None:
-            out["collectives_rccl_transport"] = coll_rccl
-        if coll_native is not None:
-            out["collectives_rccl_native_transport"] = coll_native
-        if rccl_native is not None:
-            out["rccl_native_allreduce_f32"] = rccl_native
-        if c3_variants:
-            out["c3_c4_engine_variants"] = c3_variants
+        if kids is not None:
+            out.update(collectives_report(kids))
         if per_op is not None:
             out["per_op_roofline_hbm"] = per_op
         if pack is not None:

@@ -81,3 +81,98 @@ def test_wall_budget_bounds_every_hung_child():
             assert ran[0] == "ipc_core"        # the headline configs always get their slot
     # the worst case the driver saw before the budget: ~1,380 s of child limits
     assert sum(bench.CHILD_CAP_S.values()) > bench.WALL_BUDGET_S
+
+
+_CHILDREN_SCRIPT = r'''
+import json, os, sys, time
+sys.path.insert(0, os.environ["REPO"])
+import torch.distributed as dist
+import bench
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+if os.environ.get("FAKE_LATE"):
+    bench.T_START = time.time() - (bench.WALL_BUDGET_S - bench.RESERVE_S - 1)
+calls = []
+def plane(bw):
+    return {"c3_allreduce_sum_f32": {"correct": True, "busbw_GB_s": bw, "seconds": 0.004},
+            "c4_reduce_scatter_max_f64": {"correct": True, "busbw_GB_s": bw / 2, "seconds": 0.009},
+            "c5_iallreduce_band_u64": {"correct": True, "busbw_GB_s": bw / 4, "seconds": 0.002}}
+class Fake:
+    @staticmethod
+    def collectives(world, rank, local, scale, transport, extra, tag, port_off, parts, timeout):
+        calls.append([transport, parts, tag, port_off, timeout])
+        if transport == "rccl" and rank == 1:
+            return {"error": {"stage": "c3", "text": "fake failure"}}
+        if rank != 0:
+            return {}
+        r = plane({"ipc": 400.0, "rccl": 300.0, "rccl_native": 350.0}[transport])
+        if transport == "ipc" and parts == "core":
+            r["peer_write_probe"] = {"outbound_GB_s_per_gpu": 500.0}
+        return r
+    @staticmethod
+    def rccl_allreduce(world, rank, local, scale, timeout):
+        return {"correct": True, "busbw_GB_s": 450.0} if rank == 0 else {}
+    @staticmethod
+    def multi_host(n, timeout):
+        return {"gpus": 2, "timeout": timeout}
+kids = bench.run_children(dist, world, rank, local=rank, scale=1.0, n=2, distinct=True, no_host_path=False,
+                          runners=Fake)
+if rank == 0:
+    print(json.dumps({"report": bench.collectives_report(kids), "calls": calls}))
+dist.barrier()
+dist.destroy_process_group()
+'''
+
+
+def _run_children(port, **env_extra):
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, REPO=REPO, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), MSX_BENCH_VARIANTS_AT="2", **env_extra)
+        procs.append(subprocess.Popen([sys.executable, "-c", _CHILDREN_SCRIPT], env=env, text=True,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+    import json
+    return json.loads(outs[0][0].strip().splitlines()[-1])
+
+
+def test_children_sequence_and_report_on_distinct_gpus():
+    """bench.py N > 1 on distinct GPUs (the driver's one-shot 8-GPU run, which
+    no test here can launch): two gloo ranks drive run_children with fake child
+    processes; every plane is summarized with its fraction of the measured
+    links, a non-zero rank's failure is reported by rank, the variant run and
+    the host split take their budgeted turns in CHILD_ORDER."""
+    res = _run_children(29611)
+    rep, calls = res["report"], res["calls"]
+    assert [c[:3] for c in calls] == [["ipc", "core", ""], ["rccl", "core", ""], ["rccl_native", "core", ""],
+                                      ["ipc", "c3c4", "_pipeline"], ["ipc", "extras", "_extras"]]
+    assert all(c[4] is not None and c[4] >= 20 for c in calls)
+    sm = rep["collectives_summary"]
+    assert sm["plane"] == "xgmi" and sm["measured_links_GB_s_per_gpu"] == 500.0
+    assert sm["ipc"]["c3"]["busbw_frac_measured_links"] == 0.8
+    assert sm["ipc"]["c4"]["busbw_frac_measured_links"] == 0.4
+    assert sm["rccl_native"]["c5"]["busbw_frac_measured_links"] == 0.175
+    assert sm["rccl"]["error"]["rank"] == 1                       # rank 1's failure, by rank
+    assert rep["collectives_rccl_transport"]["errors"][0]["text"] == "fake failure"
+    assert sm["rccl_own_allreduce_f32"]["busbw_frac_measured_links"] == 0.9
+    v = rep["c3_c4_engine_variants"]["pipeline"]
+    assert v["c3"]["busbw_GB_s"] == 400.0 and v["env"] == dict(__import__("bench").C3_VARIANTS)["pipeline"]
+    steps = [s["name"] for s in rep["wall_budget"]["steps"]]
+    assert steps == ["ipc_core", "rccl_core", "rccl_native_core", "rccl_allreduce", "variant_pipeline",
+                     "ipc_extras", "multi_host"]
+    assert [s["name"] for s in rep["wall_budget"]["steps"] if s.get("error")] == ["rccl_core"]
+    assert rep["host_path_multi_gpu"]["gpus"] == 2
+
+
+def test_children_skipped_when_the_budget_is_spent():
+    """Started with the wall budget already spent: every child is skipped (and
+    recorded as such), no child process runs, the report still forms."""
+    res = _run_children(29613, FAKE_LATE="1")
+    rep, calls = res["report"], res["calls"]
+    assert calls == []
+    assert all(s.get("skipped") == "wall budget" for s in rep["wall_budget"]["steps"])
+    assert rep["collectives"] == {"skipped": "wall budget"}
+    assert "skipped" in rep["c3_c4_engine_variants"]           # follows the skipped IPC core child
+    assert rep["collectives_summary"]["ipc"] == {"skipped": "wall budget"}
