@@ -218,7 +218,6 @@ int ensure_device()
     return MPI_SUCCESS;
 }
 
-int current_device() { return ds().device; }
 hipStream_t internal_stream() { return ds().stream; }
 
 void set_staging_chunk(size_t bytes)
@@ -621,7 +620,6 @@ std::atomic<int> g_host_mode{0};
 }
 
 void set_host_mode(int mode) { g_host_mode.store(mode); }
-int host_mode() { return g_host_mode.load(); }
 
 int reduce_local_any(int opidx, Kind k, const void* in, void* inout, size_t count)
 {

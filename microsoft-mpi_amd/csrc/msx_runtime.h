@@ -47,7 +47,6 @@ void set_diag_rank(int rank);   // the rank named in MSX_STUCK lines
 
 // Device bring-up.  Returns MPI_SUCCESS or MPI_ERR_OTHER (no usable GPU).
 int ensure_device();
-int current_device();
 hipStream_t internal_stream();
 int device_count_noinit();
 
@@ -100,7 +99,6 @@ void set_staging_chunk(size_t bytes);
 // pageable memory pinned for the call and combined the same way; 1 = every
 // host operand staged through HBM; 2 = pinned in place, pageable staged
 void set_host_mode(int mode);
-int host_mode();
 
 // inout = inout (op) in over `count` elements on any combination of host and
 // device buffers; blocking (returns after the result is in `inout`).
