@@ -330,6 +330,95 @@ private:
 };
 
 // ===========================================================================
+// Uncached device memory: taken from the driver, never given back
+// ===========================================================================
+// Engine windows and RMA staging areas are uncached device memory
+// (hipDeviceMallocUncached) that the peers map over IPC.  hipFree of such
+// memory leaves this ROCm stack returning wrong data to later allocations'
+// kernels and copies in the same process: after uncached buffers were used and
+// freed, torch.equal(a, a.clone()) on fresh tensors failed in 4-30 of 96 cases
+// per variant and a kernel write + copy check of a fresh plain buffer in 3 of
+// 32; with the uncached buffers kept, 0 of 192 and 0 of 32; plain buffers or
+// page-locked host memory freed the same way, 0 (scripts/va_reuse_probe.py,
+// profiles/r06/va_reuse/).  So a freed communicator's window returns to this
+// pool and serves the next window of the process (best fit), and imported peer
+// windows stay mapped (ipc_imports); creating and freeing communicators then
+// also costs no further 2 GiB allocations.
+struct UcPool {
+    struct Block {
+        void* p;
+        size_t cap;
+        bool used;
+    };
+    std::mutex mu;
+    std::vector<Block> blocks;
+};
+
+UcPool& uc_pool()
+{
+    static UcPool* pool = new UcPool();   // outlives static destruction: nothing is freed at exit either
+    return *pool;
+}
+
+// `bytes` of zeroed uncached device memory on the current device.
+hipError_t uc_alloc(size_t bytes, void** out)
+{
+    UcPool& pool = uc_pool();
+    std::lock_guard<std::mutex> g(pool.mu);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    UcPool::Block* best = nullptr;
+    for (auto& b : pool.blocks) {
+        hipPointerAttribute_t a;
+        if (b.used || b.cap < bytes || (best && b.cap >= best->cap)) continue;
+        if (hipPointerGetAttributes(&a, b.p) != hipSuccess || a.device != dev) {
+            (void)hipGetLastError();
+            continue;
+        }
+        best = &b;
+    }
+    void* p = nullptr;
+    if (best) {
+        p = best->p;
+    } else {
+        hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+        if (e != hipSuccess) return e;
+        pool.blocks.push_back({p, bytes, false});
+        best = &pool.blocks.back();
+    }
+    hipError_t e = hipMemset(p, 0, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    best->used = true;
+    *out = p;
+    return hipSuccess;
+}
+
+void uc_release(void* p)
+{
+    if (!p) return;
+    UcPool& pool = uc_pool();
+    std::lock_guard<std::mutex> g(pool.mu);
+    for (auto& b : pool.blocks)
+        if (b.p == p) b.used = false;
+}
+
+// Peer windows imported over IPC, by handle, for the life of the process (an
+// imported window is uncached memory too; closing the mapping is the same
+// release as a free).  The exporter never frees a window (uc_pool), so a
+// handle keeps naming the same memory.
+struct IpcImports {
+    std::mutex mu;
+    std::map<std::string, void*> opened;
+};
+
+IpcImports& ipc_imports()
+{
+    static IpcImports* m = new IpcImports();
+    return *m;
+}
+
+// ===========================================================================
 // IPC transport
 // ===========================================================================
 struct IpcRec {
@@ -345,9 +434,8 @@ class IpcTransport : public Transport {
 public:
     ~IpcTransport() override
     {
-        for (auto& kv : opened_) (void)hipIpcCloseMemHandle(kv.second);
-        if (win_) (void)hipFree(win_);
-        if (rwin_) (void)hipFree(rwin_);
+        uc_release(win_);    // windows go back to the pool, imports stay mapped (uc_pool)
+        uc_release(rwin_);
         if (counter_) (void)hipFree(counter_);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
@@ -452,9 +540,11 @@ public:
             }
             if (r == rank) { out[r] = const_cast<char*>(static_cast<const char*>(ptr)); continue; }
             std::string key(reinterpret_cast<const char*>(&all[r].h), sizeof(hipIpcMemHandle_t));
-            auto it = opened_.find(key);
+            IpcImports& imp = ipc_imports();
+            std::lock_guard<std::mutex> g(imp.mu);
+            auto it = imp.opened.find(key);
             void* pbase = nullptr;
-            if (it != opened_.end()) {
+            if (it != imp.opened.end()) {
                 pbase = it->second;
             } else {
                 {
@@ -467,7 +557,7 @@ public:
                     set_error("ipc error: op=map_peers rank=%d phase=ipc_open peer=%d (%s)", rank, r, hipGetErrorString(e));
                     return MPI_ERR_OTHER;
                 }
-                opened_[key] = pbase;
+                imp.opened[key] = pbase;
             }
             out[r] = static_cast<char*>(pbase) + all[r].offset;
         }
@@ -478,10 +568,8 @@ public:
     {
         // Collective: every rank asks for the same size.
         if (bytes > win_bytes_) {
-            if (win_) {
-                (void)hipFree(win_);
-                win_ = nullptr;
-            }
+            uc_release(win_);
+            win_ = nullptr;
             size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
             // Uncached device memory: peers write it over xGMI, which does not
             // snoop this GPU's L2, so no reader (kernel, blit or DMA) may hold a
@@ -492,14 +580,14 @@ public:
             // writes back or invalidates a whole XCD L2; rounds 1-2 had them and
             // they halved the collectives' throughput: p = 2 reduce_scatter
             // 4.17 -> 2.17 ms, allreduce 64 MiB 511 -> 178 us without).
-            hipError_t e = hipExtMallocWithFlags(&win_, want, hipDeviceMallocUncached);
+            // zeroed (uc_alloc) before any peer can map it (map_peers below is
+            // collective): the arrival flags behind the data areas start at 0
+            hipError_t e = uc_alloc(want, &win_);
             trace("window: %zu bytes uncached rc=%d", want, (int)e);
-            if (e != hipSuccess) return hip_fail(e, "window allocation");
-            // zeroed before any peer can map it (map_peers below is collective):
-            // the arrival flags behind the data areas must start at 0
-            e = hipMemset(win_, 0, want);
-            if (e == hipSuccess) e = hipDeviceSynchronize();
-            if (e != hipSuccess) return hip_fail(e, "window clear");
+            if (e != hipSuccess) {
+                win_ = nullptr;
+                return hip_fail(e, "window allocation");
+            }
             win_bytes_ = want;
             win_peers_.clear();
         }
@@ -537,7 +625,7 @@ public:
             for (uint64_t v : all) lo = std::min(lo, v);
             const size_t bytes = (size_t)lo;
             trace("rma window: %d rank(s) on this GPU, %zu bytes here, %zu agreed", share, (size_t)mine, bytes);
-            hipError_t e = hipExtMallocWithFlags(&rwin_, bytes, hipDeviceMallocUncached);
+            hipError_t e = uc_alloc(bytes, &rwin_);
             trace("rma window: %zu bytes rc=%d", bytes, (int)e);
             if (e != hipSuccess) {
                 rwin_ = nullptr;
@@ -557,7 +645,6 @@ private:
     ShmBarrier shm_;
     hipStream_t stream_ = nullptr;
     unsigned* counter_ = nullptr;
-    std::map<std::string, void*> opened_;
     void* win_ = nullptr;
     size_t win_bytes_ = 0;
     std::vector<char*> win_peers_;

@@ -33,7 +33,8 @@ def lib():
                             ("msxp_variant_count", i, []),
                             ("msxp_variant_name", ctypes.c_char_p, [i]),
                             ("msxp_variant_run", i, [i, p, p, i64, p]),
-                            ("msxp_tree8", i, [ctypes.POINTER(p), p, i64, i, p])):
+                            ("msxp_tree8", i, [ctypes.POINTER(p), p, i64, i, p]),
+                            ("msxp_spin_mark", i, [i64, p, ctypes.c_uint, p])):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -249,3 +249,23 @@ MSXP_EXPORT int msxp_tree8(const void* const* srcs, void* out, int64_t n, int xg
                        static_cast<hipStream_t>(stream), a, static_cast<float*>(out), nvec, (size_t)0, 1);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// one workgroup: lane 0 waits `ticks` of s_memrealtime (100 MHz), then stores
+// `value` to *flag (page-locked host memory, system-scope release) -- a kernel
+// whose completion the host can see directly, to check that a stream or device
+// synchronisation returns only after it (scripts/sync_probe.py)
+__global__ __launch_bounds__(64) void k_probe_spin_mark(unsigned long long ticks, unsigned* flag, unsigned value)
+{
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+    __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+MSXP_EXPORT int msxp_spin_mark(int64_t ticks, void* flag_dev, unsigned value, void* stream)
+{
+    if (ticks < 0 || ticks > 100000000 || !flag_dev) return 1;   // at most 1 s
+    hipLaunchKernelGGL(k_probe_spin_mark, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       (unsigned long long)ticks, static_cast<unsigned*>(flag_dev), value);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
