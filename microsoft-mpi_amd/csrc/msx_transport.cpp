@@ -741,9 +741,14 @@ int transport_create(int rank, int size, Transport** out)
     return MPI_SUCCESS;
 }
 
+namespace {
+void rccl_forget(Transport* tp);   // the RCCL plane's per-transport state (below)
+}  // namespace
+
 void transport_destroy(Transport* t)
 {
     if (!t) return;
+    rccl_forget(t);
     if (t->aux) (void)hipStreamDestroy(t->aux);
     delete t;
 }
@@ -1678,12 +1683,29 @@ bool rccl_map(int opidx, Kind k, ncclRedOp_t* op, ncclDataType_t* t)
 }
 
 std::map<Transport*, ncclComm_t> g_rccl_comms;
+std::map<Transport*, bool> g_rccl_refused;
+// RCCL communicators of freed transports: retired, not destroyed.
+// ncclCommDestroy would release RCCL's device buffers, and freeing uncached
+// device memory corrupted later allocations on this stack.
+std::vector<ncclComm_t> g_rccl_retired;
+
+// Called when `tp` is destroyed (engine worker, or finalize): a later
+// transport may get the same address and must not find this one's state.
+void rccl_forget(Transport* tp)
+{
+    auto it = g_rccl_comms.find(tp);
+    if (it != g_rccl_comms.end()) {
+        g_rccl_retired.push_back(it->second);
+        g_rccl_comms.erase(it);
+    }
+    g_rccl_refused.erase(tp);
+}
 
 // Communicator for `tp` (collective on first use; nullptr = use IPC windows).
 ncclComm_t rccl_comm(Transport* tp)
 {
     auto& comms = g_rccl_comms;
-    static std::map<Transport*, bool> refused;
+    auto& refused = g_rccl_refused;
     auto it = comms.find(tp);
     if (it != comms.end()) return it->second;
     if (refused.count(tp)) return nullptr;
