@@ -13,7 +13,7 @@ A final part checks the engine's own case: pages of a plain buffer reused as an
 uncached window written by a kernel and read with plain and non-temporal loads.
 Prints one JSON line: per variant, trials, kernel-check failures, torch cases
 and torch.equal failures (with details of the first ones).
-usage: python scripts/va_reuse_probe.py [trials]    (GPU only)"""
+usage: python scripts/va_reuse_probe.py [trials] [plain]    (GPU only; "plain": the control variant only)"""
 import ctypes
 import json
 import os
@@ -27,6 +27,7 @@ from msx import probe  # noqa: E402
 
 P = probe.lib()
 trials = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+ONLY_PLAIN = len(sys.argv) > 2 and sys.argv[2] == "plain"   # scripts/va_reuse_xproc.sh
 dev = torch.device("cuda:0")
 dflt = torch.cuda.default_stream(dev)
 sp_d = ctypes.c_void_p(dflt.cuda_stream)
@@ -142,6 +143,8 @@ for name, kw in (("uncached_full", {}),
                  ("uncached_default_stream_kept (pool)", {"torch_stream": "default", "keep": True}),
                  ("host_register_unregister", {"host": "register"}),
                  ("host_malloc_free", {"host": "malloc"})):
+    if ONLY_PLAIN and kw != {"uncached": 0}:
+        continue
     summary[name] = variant(**kw)
     print(name, {k: v for k, v in summary[name].items() if k != "details"}, file=sys.stderr, flush=True)
 
@@ -149,6 +152,9 @@ for name, kw in (("uncached_full", {}),
 # an uncached window; a kernel writes the window (uncached stores, past this
 # GPU's L2, like a peer's xGMI writes) and the tree reads it with plain (MTYPE
 # UC) and non-temporal loads: a stale L2 line would return the plain data
+if ONLY_PLAIN:
+    print(json.dumps(summary))
+    sys.exit(0)
 pv = probe.variants()
 PLAIN_LD, NT_LD = pv["u1_b64_plain_rr"], pv["u1_b64_ntld_rr"]
 k_fail = k_reuse = 0
